@@ -1,0 +1,210 @@
+#!/usr/bin/env python3
+"""Benchmark of FMI's bucket reduction on MI355X (BASELINE.json metric:
+"GiB/s device-resident float32 sum-reduce, 256 MiB buckets, 1/2/4/8 GPU").
+
+One *step* = one pass of the hot path over one batch of synthetic, HBM-resident buckets:
+  N = 1  (config C2): each GPU holds two peers' 256 MiB float32 buckets and performs the pairwise
+         combine a = a + b — the reference's `f.f(a, b)` (include/Communicator.h:180-189) on the device.
+  N > 1: each GPU still holds two peers' 256 MiB buckets (weak scaling, 2N peers in total): the local
+         pairwise combine is the first round of the reference's recursive-doubling allreduce, the
+         remaining rounds run across GPUs as an all-to-all of shards over RCCL/xGMI + our fused P-way
+         kernel in allreduce_no_order order + an all-gather (fmi_amd/collectives.py), so every GPU ends
+         with the full reduced 256 MiB bucket, bit-identical to the reference's 2N-peer allreduce.
+value = (N × 256 MiB of reduced bucket delivered) / (wall time per step, max over ranks), in GiB/s.
+
+Also reported (one JSON line on rank 0):
+  roofline     — the dominant kernel (pairwise combine at N=1): algorithmic bytes 3·n·4 per launch ÷
+                 its mean duration from HIP events on the stream it runs on; peak = 8000 GB/s HBM3E;
+                 traffic from the committed rocprofv3 PMC summary of the same kernel (profiles/).
+  cpu_baseline — oracle/cpu_baseline (a C++ port of the reference's CPU path) on this host: the
+                 reference-faithful 6-copy adapter around std::transform, 1 thread, same 256 MiB buckets.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+MIB = 1 << 20
+GIB = 1 << 30
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak, MI355X_MICROARCH.md §Chip-level parameters
+METRIC = "GiB/s device-resident float32 sum-reduce, 256 MiB buckets, 1/2/4/8 GPU"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--bucket-mib", type=int, default=256)
+    ap.add_argument("--sets", type=int, default=4, help="rotating bucket sets (defeats the 256 MiB MALL)")
+    ap.add_argument("--path", default="tree", choices=["tree", "rccl"],
+                    help="N>1 exchange: tree = all-to-all + fused kernel (bit-exact), rccl = reduce-scatter")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-reps", type=int, default=7)
+    return ap.parse_args()
+
+
+def pmc_traffic(kernel_substr: str):
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary."""
+    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    if not os.path.exists(path):
+        return None, None
+    try:
+        data = json.load(open(path))
+        for k in data.get("kernels", []):
+            if kernel_substr in k.get("kernel", ""):
+                return k.get("hbm_bytes_per_launch"), data.get("source")
+    except Exception:
+        return None, None
+    return None, None
+
+
+def cpu_baseline(args):
+    exe = os.path.join(ROOT, "oracle", "build", "cpu_baseline")
+    if not os.path.exists(exe):
+        return None
+    try:
+        out = subprocess.run([exe, "--mode", "adapter", "--dtype", "f32", "--op", "sum", "--mib", str(args.bucket_mib),
+                              "--reps", str(args.cpu_reps)], check=True, capture_output=True, text=True, timeout=600)
+        adapter = json.loads(out.stdout.strip().splitlines()[-1])
+        out = subprocess.run([exe, "--mode", "bare", "--dtype", "f32", "--op", "sum", "--mib", str(args.bucket_mib),
+                              "--reps", "9"], check=True, capture_output=True, text=True, timeout=600)
+        bare = json.loads(out.stdout.strip().splitlines()[-1])
+    except Exception as e:  # the baseline is reported, never required
+        return {"error": str(e)}
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {
+        "value": round(adapter["bucket_gib_s"], 4),
+        "unit": "GiB/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": (f"reference-faithful adapter (include/Communicator.h:182-187, 6 bucket copies) around "
+                   f"std::transform(std::plus<float>), 1 thread, {args.bucket_mib} MiB f32 pair, median of "
+                   f"{adapter['reps']} after 1 warm-up: {adapter['median_ms']:.1f} ms/combine; bare std::transform "
+                   f"1 thread: {bare['median_ms']:.2f} ms = {bare['bucket_gib_s']:.2f} GiB/s; host '{model}', "
+                   f"{os.cpu_count()} CPUs visible"),
+        "bare_loop_gib_s": round(bare["bucket_gib_s"], 4),
+    }
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if args.gpus > 1 and world == 1:
+            raise SystemExit(f"--gpus {args.gpus} needs torch.distributed.run with {args.gpus} processes")
+        args.gpus = world
+
+    import numpy as np
+
+    dist = None
+    if world > 1:
+        # torch first: libfmi_dev.so then binds to the HIP runtime torch already loaded (one runtime
+        # per process, shared streams/pointers with RCCL) — see DESIGN.md §Runtime.
+        import torch
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    import fmi_amd
+    from fmi_amd import Bucket, Event, Op
+
+    fmi_amd.init(local_rank)
+    n = args.bucket_mib * MIB // 4
+    nbytes = n * 4
+
+    if world == 1:
+        sets = [(Bucket(n, np.float32).fill_synthetic(42 + s, 0), Bucket(n, np.float32).fill_synthetic(42 + s, 1))
+                for s in range(args.sets)]
+        fmi_amd.sync()
+
+        def step(k):
+            a, b = sets[k % len(sets)]
+            fmi_amd.reduce_pair(Op.SUM, a, b)
+
+        for k in range(args.warmup):
+            step(k)
+        fmi_amd.sync()
+        starts = [Event() for _ in range(args.steps)]
+        stops = [Event() for _ in range(args.steps)]
+        t0 = time.perf_counter()
+        for k in range(args.steps):
+            starts[k].record()
+            step(k)
+            stops[k].record()
+        fmi_amd.sync()
+        t1 = time.perf_counter()
+        kernel_ms = [starts[k].elapsed_ms(stops[k]) for k in range(args.steps)]
+        wall_ms = (t1 - t0) * 1e3 / args.steps
+        step_ms = wall_ms
+        dominant = "pair_tile"
+        algo_bytes = 3 * nbytes
+        workload = "C2: 1-GPU pairwise float32 sum-reduce of two 256 MiB device-resident peer buckets"
+        parallelism = "single GPU (2 peers resident)"
+        extra = {}
+    else:
+        from fmi_amd.collectives import ShardedAllreduce
+
+        ar = ShardedAllreduce(dist.group.WORLD, path=args.path)
+        step_ms, kernel_ms, extra = ar.bench(n, steps=args.steps, warmup=args.warmup, sets=args.sets)
+        dominant = "tree_kernel" if args.path == "tree" else "pair_tile"
+        algo_bytes = extra.pop("kernel_algo_bytes")
+        workload = (f"C4-shaped: {2 * world}-peer float32 sum-allreduce of 256 MiB buckets, 2 peers per GPU, "
+                    f"sharded over {world} GPUs")
+        parallelism = f"shard{world} ({args.path}: all-to-all + fused tree + all-gather over RCCL)" \
+            if args.path == "tree" else f"shard{world} (RCCL reduce-scatter + all-gather)"
+
+    kernel_avg_ms = float(sum(kernel_ms) / len(kernel_ms))
+    value = args.gpus * (nbytes / GIB) / (step_ms * 1e-3)
+    achieved = algo_bytes / (kernel_avg_ms * 1e-3) / 1e9
+    traffic, traffic_src = pmc_traffic(dominant)
+    line = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "GiB/s",
+        "n_gpus": args.gpus,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(step_ms, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (splitmix64 counter generator, SURVEY.md §8d), device-resident in HBM",
+        "config": {"workload": workload, "bucket_mib": args.bucket_mib, "elements": n,
+                   "peers": 2 * args.gpus, "parallelism": parallelism, "rotating_sets": args.sets},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "kernel": dominant, "kernel_avg_us": round(kernel_avg_ms * 1e3, 2),
+                     "algorithmic_bytes_per_launch": algo_bytes,
+                     "traffic_source": traffic_src},
+    }
+    line["config"].update(extra)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(args)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,20 @@
+"""fmi_amd — MI355X-native (gfx950) engine for FMI's bucket reduction (reduce / allreduce / scan).
+
+Layout:
+  include/fmi_dev.h          C-ABI (the drop-in boundary)
+  fmi_amd/csrc/              HIP kernels + C-ABI implementation → fmi_amd/lib/libfmi_dev.so
+  fmi_amd/cpp/include/fmi/   C++ mirror of the FMI::Communicator surface (reference include/)
+  fmi_amd/device.py          Python handle over the C-ABI (ctypes)
+  fmi_amd/collectives.py     multi-GPU sharded allreduce over torch.distributed (RCCL over xGMI)
+"""
+from ._lib import FmiError, LIB_PATH, load  # noqa: F401
+from .device import (  # noqa: F401
+    Alg, Bucket, DType, Event, Op, Stream, Tune, combine, describe, device_count, finalize, host_reduce_pair,
+    init, reduce_pair, reduce_tree, scan_peers, schedule_expr, sync, tune_get, tune_set,
+)
+
+__all__ = [
+    "Alg", "Bucket", "DType", "Event", "FmiError", "LIB_PATH", "Op", "Stream", "Tune", "combine", "describe",
+    "device_count", "finalize", "host_reduce_pair", "init", "load", "reduce_pair", "reduce_tree", "scan_peers",
+    "schedule_expr", "sync", "tune_get", "tune_set",
+]

@@ -1,0 +1,556 @@
+// fmi_dev.hip — C-ABI implementation (include/fmi_dev.h): device state, memory, streams, events, the
+// pairwise hot kernel's launch policy, P-way dispatch, the host-ingress pipeline and synthetic buckets.
+#include <algorithm>
+#include <atomic>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "fmi_internal.h"
+
+namespace fmi::dev {
+
+namespace {
+
+thread_local std::string t_last_error;
+
+struct DeviceState {
+    int device = -1;
+    int num_cus = 256;
+    hipStream_t stream = nullptr;
+    // host-ingress pipeline scratch (fmi_host_reduce_pair): two slots of (a, b) staging + two streams
+    void* stage[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
+    size_t stage_bytes = 0;
+    hipStream_t pipe[2] = {nullptr, nullptr};
+};
+
+std::mutex g_mu;
+DeviceState g_state;  // one process drives one device (one process per GPU, as FMI runs one peer per process)
+
+std::atomic<long long> g_tune[5] = {0 /*variant: tiles*/, 4 /*unroll*/, 256 /*block*/, 8 /*grid per CU*/,
+                                    64ll << 20 /*host chunk*/};
+
+int hip_fail(const char* what, hipError_t e) {
+    return fail(FMI_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define FMI_HIP_TRY(call)                                   \
+    do {                                                    \
+        const hipError_t fmi_e_ = (call);                   \
+        if (fmi_e_ != hipSuccess) return hip_fail(#call, fmi_e_); \
+    } while (0)
+
+int require_device() {
+    if (g_state.device < 0) return fail(FMI_ERR_NO_DEVICE, "fmi_dev_init has not been called");
+    int cur = -1;
+    if (hipGetDevice(&cur) != hipSuccess || cur != g_state.device) FMI_HIP_TRY(hipSetDevice(g_state.device));
+    return FMI_OK;
+}
+
+hipStream_t resolve(fmi_stream_t s) { return s ? static_cast<hipStream_t>(s) : g_state.stream; }
+
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+// ----------------------------------------------------------------------------------------------------
+// Pairwise launch policy.
+// ----------------------------------------------------------------------------------------------------
+template <class Op, class T, bool NT>
+int launch_pair_vec(T* out, const T* a, const T* b, size_t n, hipStream_t s) {
+    const long long variant = g_tune[FMI_TUNE_PAIR_VARIANT].load();
+    const long long unroll = g_tune[FMI_TUNE_PAIR_UNROLL].load();
+    const unsigned block = static_cast<unsigned>(g_tune[FMI_TUNE_BLOCK].load());
+    const size_t nvec = n / kVecLanes<T>;
+    const size_t per_block = static_cast<size_t>(block) * static_cast<size_t>(unroll);
+    const size_t ntiles = std::max<size_t>(1, (nvec + per_block - 1) / per_block);
+    if (variant == 1) {
+        const size_t cap = static_cast<size_t>(g_state.num_cus) * static_cast<size_t>(g_tune[FMI_TUNE_GRID_PER_CU].load());
+        const unsigned grid = static_cast<unsigned>(std::max<size_t>(1, std::min(ntiles, cap)));
+        switch (unroll) {
+            case 1: pair_stride<Op, T, 1, NT><<<grid, block, 0, s>>>(out, a, b, n); break;
+            case 2: pair_stride<Op, T, 2, NT><<<grid, block, 0, s>>>(out, a, b, n); break;
+            case 4: pair_stride<Op, T, 4, NT><<<grid, block, 0, s>>>(out, a, b, n); break;
+            case 8: pair_stride<Op, T, 8, NT><<<grid, block, 0, s>>>(out, a, b, n); break;
+            default: return fail(FMI_ERR_INVALID, "unroll must be 1, 2, 4 or 8");
+        }
+    } else {
+        const unsigned grid = static_cast<unsigned>(ntiles);
+        switch (unroll) {
+            case 1: pair_tile<Op, T, 1, NT><<<grid, block, 0, s>>>(out, a, b, n); break;
+            case 2: pair_tile<Op, T, 2, NT><<<grid, block, 0, s>>>(out, a, b, n); break;
+            case 4: pair_tile<Op, T, 4, NT><<<grid, block, 0, s>>>(out, a, b, n); break;
+            case 8: pair_tile<Op, T, 8, NT><<<grid, block, 0, s>>>(out, a, b, n); break;
+            default: return fail(FMI_ERR_INVALID, "unroll must be 1, 2, 4 or 8");
+        }
+    }
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail("pairwise kernel launch", e);
+    return FMI_OK;
+}
+
+int launch_combine(int op, int dtype, void* out, const void* a, const void* b, size_t n, hipStream_t s) {
+    if (n == 0) return FMI_OK;
+    if (!out || !a || !b) return fail(FMI_ERR_INVALID, "null buffer");
+    return with_op_dtype(op, dtype, [&]<class Op, class T>() -> int {
+        T* o = static_cast<T*>(out);
+        const T* x = static_cast<const T*>(a);
+        const T* y = static_cast<const T*>(b);
+        if (aligned16(o) && aligned16(x) && aligned16(y)) {
+            if (g_tune[FMI_TUNE_PAIR_VARIANT].load() == 2) return launch_pair_vec<Op, T, true>(o, x, y, n, s);
+            return launch_pair_vec<Op, T, false>(o, x, y, n, s);
+        }
+        const unsigned grid = static_cast<unsigned>(std::min<size_t>(grid_for(n, 256), 65536));
+        pair_scalar<Op, T><<<grid, 256, 0, s>>>(o, x, y, n);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return hip_fail("pairwise scalar kernel launch", e);
+        return FMI_OK;
+    });
+}
+
+// ----------------------------------------------------------------------------------------------------
+// P-way programs for P > 16 or unaligned buckets: the same schedule, one pairwise pass per step, temp
+// buckets recycled as soon as their value is dead (stream-ordered allocation).
+// ----------------------------------------------------------------------------------------------------
+int run_program_stepwise(int op, int dtype, const sched::HostProgram& prog, void* const* outs, int nouts,
+                         const int* out_value, const void* const* ins, size_t n, hipStream_t s) {
+    const size_t esz = dtype_size(dtype);
+    const int P = prog.peers;
+    const int nv = prog.nvalues();
+    std::vector<int> last_use(nv, -1);
+    for (int st = 0; st < prog.nsteps; ++st) {
+        last_use[prog.step[st].a] = st;
+        last_use[prog.step[st].b] = st;
+    }
+    for (int k = 0; k < nouts; ++k) last_use[out_value[k]] = prog.nsteps;  // outputs live to the end
+    std::vector<void*> buf(nv, nullptr);
+    for (int p = 0; p < P; ++p) buf[p] = const_cast<void*>(ins[p]);
+    std::vector<void*> free_list, owned;
+    int rc = FMI_OK;
+    for (int st = 0; st < prog.nsteps && rc == FMI_OK; ++st) {
+        void* dst = nullptr;
+        if (!free_list.empty()) {
+            dst = free_list.back();
+            free_list.pop_back();
+        } else {
+            const hipError_t e = hipMallocAsync(&dst, std::max<size_t>(n * esz, 16), s);
+            if (e != hipSuccess) {
+                rc = fail(FMI_ERR_ALLOC, std::string("hipMallocAsync (P-way scratch): ") + hipGetErrorString(e));
+                break;
+            }
+            owned.push_back(dst);
+        }
+        const int v = P + st;
+        buf[v] = dst;
+        rc = launch_combine(op, dtype, dst, buf[prog.step[st].a], buf[prog.step[st].b], n, s);
+        for (int operand : {static_cast<int>(prog.step[st].a), static_cast<int>(prog.step[st].b)})
+            if (operand >= P && last_use[operand] == st && buf[operand]) {
+                free_list.push_back(buf[operand]);
+                buf[operand] = nullptr;
+            }
+    }
+    for (int k = 0; k < nouts && rc == FMI_OK; ++k) {
+        const void* src = buf[out_value[k]];
+        if (src != outs[k] && n > 0) {
+            const hipError_t e = hipMemcpyAsync(outs[k], src, n * esz, hipMemcpyDeviceToDevice, s);
+            if (e != hipSuccess) rc = hip_fail("hipMemcpyAsync (P-way result)", e);
+        }
+    }
+    for (void* p : owned) (void)hipFreeAsync(p, s);
+    return rc;
+}
+
+int check_peer_args(int op, int dtype, int P) {
+    if (op < FMI_OP_SUM || op > FMI_OP_MIN) return fail(FMI_ERR_INVALID, "unknown op " + std::to_string(op));
+    if (dtype_size(dtype) == 0) return fail(FMI_ERR_INVALID, "unknown dtype " + std::to_string(dtype));
+    if (P < 1 || P > sched::kMaxPeers)
+        return fail(FMI_ERR_INVALID, "P must be in [1, " + std::to_string(sched::kMaxPeers) + "], got " + std::to_string(P));
+    return FMI_OK;
+}
+
+// Symbolic evaluation of a program, for fmi_schedule_expr.
+std::string expr_of(const sched::HostProgram& prog, int v) {
+    if (v < prog.peers) return "x" + std::to_string(v);
+    const sched::Step& st = prog.step[v - prog.peers];
+    return "(" + expr_of(prog, st.a) + "+" + expr_of(prog, st.b) + ")";
+}
+
+}  // namespace
+
+int fail(int code, const std::string& msg) {
+    t_last_error = msg;
+    return code;
+}
+
+}  // namespace fmi::dev
+
+using namespace fmi::dev;
+namespace sched = fmi::sched;
+
+extern "C" {
+
+int fmi_abi_version(void) { return FMI_DEV_ABI_VERSION; }
+
+const char* fmi_last_error(void) { return t_last_error.c_str(); }
+
+int fmi_dev_count(int* count) {
+    if (!count) return fail(FMI_ERR_INVALID, "count is null");
+    int c = 0;
+    if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
+    *count = c;
+    return FMI_OK;
+}
+
+int fmi_dev_init(int device) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count == 0)
+        return fail(FMI_ERR_NO_DEVICE, "no HIP device visible");
+    if (device < 0 || device >= count)
+        return fail(FMI_ERR_NO_DEVICE, "device " + std::to_string(device) + " out of range (" + std::to_string(count) + " visible)");
+    hipDeviceProp_t prop;
+    FMI_HIP_TRY(hipGetDeviceProperties(&prop, device));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(FMI_ERR_NO_DEVICE, std::string("device arch ") + prop.gcnArchName + " is not gfx950 (MI355X)");
+    if (g_state.device == device && g_state.stream) return FMI_OK;
+    FMI_HIP_TRY(hipSetDevice(device));
+    hipStream_t s = nullptr;
+    FMI_HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    g_state.device = device;
+    g_state.num_cus = prop.multiProcessorCount;
+    g_state.stream = s;
+    return FMI_OK;
+}
+
+int fmi_dev_finalize(void) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (g_state.device < 0) return FMI_OK;
+    (void)hipSetDevice(g_state.device);
+    (void)hipDeviceSynchronize();
+    for (int k = 0; k < 2; ++k) {
+        for (int j = 0; j < 2; ++j)
+            if (g_state.stage[k][j]) (void)hipFree(g_state.stage[k][j]);
+        if (g_state.pipe[k]) (void)hipStreamDestroy(g_state.pipe[k]);
+    }
+    if (g_state.stream) (void)hipStreamDestroy(g_state.stream);
+    g_state = DeviceState{};
+    return FMI_OK;
+}
+
+int fmi_dev_sync(void) {
+    if (int rc = require_device()) return rc;
+    FMI_HIP_TRY(hipDeviceSynchronize());
+    return FMI_OK;
+}
+
+int fmi_dev_describe(char* buf, size_t len) {
+    if (!buf || len == 0) return fail(FMI_ERR_INVALID, "null buffer");
+    if (int rc = require_device()) return rc;
+    hipDeviceProp_t prop;
+    FMI_HIP_TRY(hipGetDeviceProperties(&prop, g_state.device));
+    std::string d = std::string(prop.name) + " " + prop.gcnArchName + " CUs=" + std::to_string(prop.multiProcessorCount) +
+                    " HBM=" + std::to_string(prop.totalGlobalMem >> 20) + "MiB";
+    std::snprintf(buf, len, "%s", d.c_str());
+    return FMI_OK;
+}
+
+// ---- memory ----------------------------------------------------------------------------------------
+int fmi_dev_alloc(void** ptr, size_t bytes) {
+    if (!ptr) return fail(FMI_ERR_INVALID, "ptr is null");
+    if (int rc = require_device()) return rc;
+    const hipError_t e = hipMalloc(ptr, std::max<size_t>(bytes, 1));
+    if (e != hipSuccess) return fail(FMI_ERR_ALLOC, "hipMalloc(" + std::to_string(bytes) + "): " + hipGetErrorString(e));
+    return FMI_OK;
+}
+
+int fmi_dev_free(void* ptr) {
+    if (!ptr) return FMI_OK;
+    if (int rc = require_device()) return rc;
+    FMI_HIP_TRY(hipFree(ptr));
+    return FMI_OK;
+}
+
+int fmi_host_pin_alloc(void** ptr, size_t bytes) {
+    if (!ptr) return fail(FMI_ERR_INVALID, "ptr is null");
+    if (int rc = require_device()) return rc;
+    const hipError_t e = hipHostMalloc(ptr, std::max<size_t>(bytes, 1), hipHostMallocDefault);
+    if (e != hipSuccess) return fail(FMI_ERR_ALLOC, "hipHostMalloc(" + std::to_string(bytes) + "): " + hipGetErrorString(e));
+    return FMI_OK;
+}
+
+int fmi_host_pin_free(void* ptr) {
+    if (!ptr) return FMI_OK;
+    FMI_HIP_TRY(hipHostFree(ptr));
+    return FMI_OK;
+}
+
+static int copy_async(void* dst, const void* src, size_t bytes, hipMemcpyKind kind, fmi_stream_t stream) {
+    if (bytes == 0) return FMI_OK;
+    if (!dst || !src) return fail(FMI_ERR_INVALID, "null buffer");
+    if (int rc = require_device()) return rc;
+    FMI_HIP_TRY(hipMemcpyAsync(dst, src, bytes, kind, resolve(stream)));
+    return FMI_OK;
+}
+
+int fmi_dev_h2d_async(void* dst, const void* src, size_t bytes, fmi_stream_t stream) {
+    return copy_async(dst, src, bytes, hipMemcpyHostToDevice, stream);
+}
+int fmi_dev_d2h_async(void* dst, const void* src, size_t bytes, fmi_stream_t stream) {
+    return copy_async(dst, src, bytes, hipMemcpyDeviceToHost, stream);
+}
+int fmi_dev_d2d_async(void* dst, const void* src, size_t bytes, fmi_stream_t stream) {
+    return copy_async(dst, src, bytes, hipMemcpyDeviceToDevice, stream);
+}
+
+int fmi_dev_memset_async(void* dst, int value, size_t bytes, fmi_stream_t stream) {
+    if (bytes == 0) return FMI_OK;
+    if (!dst) return fail(FMI_ERR_INVALID, "null buffer");
+    if (int rc = require_device()) return rc;
+    FMI_HIP_TRY(hipMemsetAsync(dst, value, bytes, resolve(stream)));
+    return FMI_OK;
+}
+
+// ---- streams / events --------------------------------------------------------------------------------
+int fmi_stream_create(fmi_stream_t* stream) {
+    if (!stream) return fail(FMI_ERR_INVALID, "stream is null");
+    if (int rc = require_device()) return rc;
+    hipStream_t s = nullptr;
+    FMI_HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    *stream = s;
+    return FMI_OK;
+}
+
+int fmi_stream_destroy(fmi_stream_t stream) {
+    if (!stream) return FMI_OK;
+    FMI_HIP_TRY(hipStreamDestroy(static_cast<hipStream_t>(stream)));
+    return FMI_OK;
+}
+
+int fmi_stream_sync(fmi_stream_t stream) {
+    if (int rc = require_device()) return rc;
+    FMI_HIP_TRY(hipStreamSynchronize(resolve(stream)));
+    return FMI_OK;
+}
+
+int fmi_event_create(fmi_event_t* event) {
+    if (!event) return fail(FMI_ERR_INVALID, "event is null");
+    if (int rc = require_device()) return rc;
+    hipEvent_t e = nullptr;
+    FMI_HIP_TRY(hipEventCreate(&e));
+    *event = e;
+    return FMI_OK;
+}
+
+int fmi_event_destroy(fmi_event_t event) {
+    if (!event) return FMI_OK;
+    FMI_HIP_TRY(hipEventDestroy(static_cast<hipEvent_t>(event)));
+    return FMI_OK;
+}
+
+int fmi_event_record(fmi_event_t event, fmi_stream_t stream) {
+    if (!event) return fail(FMI_ERR_INVALID, "event is null");
+    if (int rc = require_device()) return rc;
+    FMI_HIP_TRY(hipEventRecord(static_cast<hipEvent_t>(event), resolve(stream)));
+    return FMI_OK;
+}
+
+int fmi_event_sync(fmi_event_t event) {
+    if (!event) return fail(FMI_ERR_INVALID, "event is null");
+    FMI_HIP_TRY(hipEventSynchronize(static_cast<hipEvent_t>(event)));
+    return FMI_OK;
+}
+
+int fmi_event_elapsed_ms(float* ms, fmi_event_t start, fmi_event_t stop) {
+    if (!ms || !start || !stop) return fail(FMI_ERR_INVALID, "null argument");
+    FMI_HIP_TRY(hipEventElapsedTime(ms, static_cast<hipEvent_t>(start), static_cast<hipEvent_t>(stop)));
+    return FMI_OK;
+}
+
+// ---- hot path ----------------------------------------------------------------------------------------
+int fmi_dev_reduce_pair(int op, int dtype, void* inout, const void* in, size_t n, fmi_stream_t stream) {
+    if (int rc = require_device()) return rc;
+    return launch_combine(op, dtype, inout, inout, in, n, resolve(stream));
+}
+
+int fmi_dev_combine(int op, int dtype, void* out, const void* a, const void* b, size_t n, fmi_stream_t stream) {
+    if (int rc = require_device()) return rc;
+    return launch_combine(op, dtype, out, a, b, n, resolve(stream));
+}
+
+int fmi_dev_reduce_tree(int op, int dtype, int alg, void* out, const void* const* ins, int P, int rank, size_t n,
+                        fmi_stream_t stream) {
+    if (int rc = check_peer_args(op, dtype, P)) return rc;
+    if (alg != FMI_ALG_ALLREDUCE && alg != FMI_ALG_REDUCE && alg != FMI_ALG_REDUCE_LTR)
+        return fail(FMI_ERR_INVALID, "fmi_dev_reduce_tree: alg must be ALLREDUCE, REDUCE or REDUCE_LTR");
+    if (rank < 0 || rank >= P) return fail(FMI_ERR_INVALID, "rank/root out of range");
+    if (!out || !ins) return fail(FMI_ERR_INVALID, "null buffer");
+    for (int p = 0; p < P; ++p)
+        if (!ins[p]) return fail(FMI_ERR_INVALID, "null input bucket");
+    if (int rc = require_device()) return rc;
+    if (n == 0) return FMI_OK;
+    hipStream_t s = resolve(stream);
+    // reduce_no_order works on transformed ids t = (id - root) mod P (PeerToPeer.cpp:287-293):
+    // input slot t takes real peer (t + root) % P.
+    std::vector<const void*> order(P);
+    for (int t = 0; t < P; ++t) order[t] = ins[alg == FMI_ALG_REDUCE ? (t + rank) % P : t];
+    bool aligned = aligned16(out);
+    for (int p = 0; p < P; ++p) aligned = aligned && aligned16(order[p]);
+    if (P >= 2 && P <= sched::kMaxFusedPeers && aligned) {
+        PeerPtrs ptrs{};
+        for (int p = 0; p < P; ++p) ptrs.in[p] = order[p];
+        ptrs.out[0] = out;
+        switch (alg) {
+            case FMI_ALG_ALLREDUCE: return launch_fused_allreduce(op, dtype, P, ptrs, n, rank, s);
+            case FMI_ALG_REDUCE: return launch_fused_reduce(op, dtype, P, ptrs, n, s);
+            default: return launch_fused_reduce_ltr(op, dtype, P, ptrs, n, s);
+        }
+    }
+    const sched::HostProgram prog = sched::build_host(alg, P);
+    if (!prog.ok) return fail(FMI_ERR_INVALID, "schedule construction failed");
+    const int value = prog.out[alg == FMI_ALG_ALLREDUCE ? rank : 0];
+    void* outs[1] = {out};
+    return run_program_stepwise(op, dtype, prog, outs, 1, &value, order.data(), n, s);
+}
+
+int fmi_dev_scan_peers(int op, int dtype, int alg, void* const* outs, const void* const* ins, int P, size_t n,
+                       fmi_stream_t stream) {
+    if (int rc = check_peer_args(op, dtype, P)) return rc;
+    if (alg != FMI_ALG_SCAN && alg != FMI_ALG_SCAN_LTR)
+        return fail(FMI_ERR_INVALID, "fmi_dev_scan_peers: alg must be SCAN or SCAN_LTR");
+    if (!outs || !ins) return fail(FMI_ERR_INVALID, "null buffer");
+    for (int p = 0; p < P; ++p)
+        if (!ins[p] || !outs[p]) return fail(FMI_ERR_INVALID, "null bucket");
+    if (int rc = require_device()) return rc;
+    if (n == 0) return FMI_OK;
+    hipStream_t s = resolve(stream);
+    bool aligned = true;
+    for (int p = 0; p < P; ++p) aligned = aligned && aligned16(ins[p]) && aligned16(outs[p]);
+    if (P >= 2 && P <= sched::kMaxFusedPeers && aligned) {
+        PeerPtrs ptrs{};
+        for (int p = 0; p < P; ++p) {
+            ptrs.in[p] = ins[p];
+            ptrs.out[p] = outs[p];
+        }
+        return alg == FMI_ALG_SCAN ? launch_fused_scan(op, dtype, P, ptrs, n, s)
+                                   : launch_fused_scan_ltr(op, dtype, P, ptrs, n, s);
+    }
+    const sched::HostProgram prog = sched::build_host(alg, P);
+    if (!prog.ok) return fail(FMI_ERR_INVALID, "schedule construction failed");
+    std::vector<int> values(P);
+    for (int p = 0; p < P; ++p) values[p] = prog.out[p];
+    return run_program_stepwise(op, dtype, prog, outs, P, values.data(), ins, n, s);
+}
+
+// Host-ingress pipeline: chunk c uses slot c % 2 (its own staging pair and its own stream). Stream order
+// keeps a slot's staging from being overwritten before its previous D2H finished, while the other slot's
+// H2D overlaps this slot's kernel + D2H.
+int fmi_host_reduce_pair(int op, int dtype, void* inout, const void* in, size_t n) {
+    if (op < FMI_OP_SUM || op > FMI_OP_MIN) return fail(FMI_ERR_INVALID, "unknown op " + std::to_string(op));
+    const size_t esz = dtype_size(dtype);
+    if (esz == 0) return fail(FMI_ERR_INVALID, "unknown dtype " + std::to_string(dtype));
+    if (n == 0) return FMI_OK;
+    if (!inout || !in) return fail(FMI_ERR_INVALID, "null buffer");
+    if (int rc = require_device()) return rc;
+    std::lock_guard<std::mutex> lk(g_mu);
+    size_t chunk_elems = static_cast<size_t>(std::max<long long>(g_tune[FMI_TUNE_HOST_CHUNK].load(), 1 << 16)) / esz;
+    chunk_elems = std::max<size_t>(16, chunk_elems / 16 * 16);
+    const size_t chunk_bytes = chunk_elems * esz;
+    if (g_state.stage_bytes < chunk_bytes) {
+        for (int k = 0; k < 2; ++k)
+            for (int j = 0; j < 2; ++j) {
+                if (g_state.stage[k][j]) FMI_HIP_TRY(hipFree(g_state.stage[k][j]));
+                g_state.stage[k][j] = nullptr;
+            }
+        for (int k = 0; k < 2; ++k)
+            for (int j = 0; j < 2; ++j) {
+                const hipError_t e = hipMalloc(&g_state.stage[k][j], chunk_bytes);
+                if (e != hipSuccess) {
+                    g_state.stage_bytes = 0;
+                    return fail(FMI_ERR_ALLOC, std::string("hipMalloc (host pipeline staging): ") + hipGetErrorString(e));
+                }
+            }
+        g_state.stage_bytes = chunk_bytes;
+    }
+    for (int k = 0; k < 2; ++k)
+        if (!g_state.pipe[k]) FMI_HIP_TRY(hipStreamCreateWithFlags(&g_state.pipe[k], hipStreamNonBlocking));
+    char* hx = static_cast<char*>(inout);
+    const char* hy = static_cast<const char*>(in);
+    int rc = FMI_OK;
+    size_t chunk = 0;
+    for (size_t off = 0; off < n && rc == FMI_OK; off += chunk_elems, ++chunk) {
+        const int slot = static_cast<int>(chunk & 1);
+        hipStream_t s = g_state.pipe[slot];
+        const size_t cnt = std::min(chunk_elems, n - off);
+        const size_t bytes = cnt * esz;
+        void* da = g_state.stage[slot][0];
+        void* db = g_state.stage[slot][1];
+        FMI_HIP_TRY(hipMemcpyAsync(da, hx + off * esz, bytes, hipMemcpyHostToDevice, s));
+        FMI_HIP_TRY(hipMemcpyAsync(db, hy + off * esz, bytes, hipMemcpyHostToDevice, s));
+        rc = launch_combine(op, dtype, da, da, db, cnt, s);
+        if (rc != FMI_OK) break;
+        FMI_HIP_TRY(hipMemcpyAsync(hx + off * esz, da, bytes, hipMemcpyDeviceToHost, s));
+    }
+    for (int k = 0; k < 2; ++k) FMI_HIP_TRY(hipStreamSynchronize(g_state.pipe[k]));
+    return rc;
+}
+
+int fmi_dev_fill_synthetic(int dtype, void* buf, size_t n, uint64_t seed, uint32_t peer, fmi_stream_t stream) {
+    if (n == 0) return FMI_OK;
+    if (!buf) return fail(FMI_ERR_INVALID, "null buffer");
+    if (int rc = require_device()) return rc;
+    hipStream_t s = resolve(stream);
+    const unsigned grid = static_cast<unsigned>(std::min<size_t>(grid_for(n, 256), 16384));
+    switch (dtype) {
+        case FMI_F32: synth_kernel<float><<<grid, 256, 0, s>>>(static_cast<float*>(buf), n, seed, peer); break;
+        case FMI_F64: synth_kernel<double><<<grid, 256, 0, s>>>(static_cast<double*>(buf), n, seed, peer); break;
+        case FMI_I32: synth_kernel<int32_t><<<grid, 256, 0, s>>>(static_cast<int32_t*>(buf), n, seed, peer); break;
+        case FMI_I64: synth_kernel<int64_t><<<grid, 256, 0, s>>>(static_cast<int64_t*>(buf), n, seed, peer); break;
+        default: return fail(FMI_ERR_INVALID, "unknown dtype " + std::to_string(dtype));
+    }
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail("synthetic fill launch", e);
+    return FMI_OK;
+}
+
+int fmi_schedule_expr(int alg, int P, int rank, char* buf, size_t len) {
+    if (!buf || len == 0) return fail(FMI_ERR_INVALID, "null buffer");
+    if (P < 1 || P > sched::kMaxPeers) return fail(FMI_ERR_INVALID, "P out of range");
+    if (rank < 0 || rank >= P) return fail(FMI_ERR_INVALID, "rank out of range");
+    const sched::HostProgram prog = sched::build_host(alg, P);
+    if (!prog.ok) return fail(FMI_ERR_INVALID, "unknown algorithm " + std::to_string(alg));
+    const std::string e = expr_of(prog, prog.out[rank]);
+    if (e.size() + 1 > len) return fail(FMI_ERR_INVALID, "buffer too small (" + std::to_string(e.size() + 1) + " needed)");
+    std::memcpy(buf, e.c_str(), e.size() + 1);
+    return FMI_OK;
+}
+
+int fmi_tune_set(int key, long long value) {
+    switch (key) {
+        case FMI_TUNE_PAIR_VARIANT:
+            if (value < 0 || value > 2) return fail(FMI_ERR_INVALID, "variant must be 0, 1 or 2");
+            break;
+        case FMI_TUNE_PAIR_UNROLL:
+            if (value != 1 && value != 2 && value != 4 && value != 8) return fail(FMI_ERR_INVALID, "unroll must be 1, 2, 4 or 8");
+            break;
+        case FMI_TUNE_BLOCK:
+            if (value != 64 && value != 128 && value != 256 && value != 512 && value != 1024)
+                return fail(FMI_ERR_INVALID, "block must be 64..1024 (power of two)");
+            break;
+        case FMI_TUNE_GRID_PER_CU:
+            if (value < 1 || value > 64) return fail(FMI_ERR_INVALID, "grid per CU must be in [1, 64]");
+            break;
+        case FMI_TUNE_HOST_CHUNK:
+            if (value < (1 << 16)) return fail(FMI_ERR_INVALID, "host chunk must be >= 64 KiB");
+            break;
+        default: return fail(FMI_ERR_INVALID, "unknown tuning key");
+    }
+    g_tune[key].store(value);
+    return FMI_OK;
+}
+
+int fmi_tune_get(int key, long long* value) {
+    if (!value || key < 0 || key > FMI_TUNE_HOST_CHUNK) return fail(FMI_ERR_INVALID, "bad tuning query");
+    *value = g_tune[key].load();
+    return FMI_OK;
+}
+
+}  // extern "C"

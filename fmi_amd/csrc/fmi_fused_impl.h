@@ -1,0 +1,51 @@
+// fmi_fused_impl.h — launch tables for the fused P-way kernels (included by one TU per algorithm).
+#pragma once
+
+#include <array>
+#include <type_traits>
+
+#include "fmi_internal.h"
+
+namespace fmi::dev {
+
+inline int check_launch(const char* what) {
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(FMI_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+    return FMI_OK;
+}
+
+constexpr unsigned kFusedBlock = 256;
+
+using FusedFn = void (*)(const PeerPtrs&, size_t, int, hipStream_t);
+
+template <class Op, class T, int ALG, bool ALL_RANKS, int P>
+void fused_one(const PeerPtrs& ptrs, size_t n, int rank, hipStream_t s) {
+    const size_t nvec = n / kVecLanes<T>;
+    if constexpr (ALG == sched::kScan || ALG == sched::kScanLtr)
+        scan_kernel<Op, T, ALG, P><<<grid_for(nvec, kFusedBlock), kFusedBlock, 0, s>>>(ptrs, n);
+    else
+        tree_kernel<Op, T, ALG, P, ALL_RANKS><<<grid_for(nvec, kFusedBlock), kFusedBlock, 0, s>>>(ptrs, n, rank);
+}
+
+template <class Op, class T, int ALG, bool ALL_RANKS, int... I>
+constexpr std::array<FusedFn, sizeof...(I)> fused_table(std::integer_sequence<int, I...>) {
+    return {&fused_one<Op, T, ALG, ALL_RANKS, I + 2>...};
+}
+
+// RANK_AWARE: the algorithm hands different operand orders to different peers (allreduce); the
+// rank-selecting kernel is instantiated only where that can change bits (float max/min).
+template <int ALG, bool RANK_AWARE>
+int launch_fused(int op, int dtype, int P, const PeerPtrs& ptrs, size_t n, int rank, hipStream_t s) {
+    if (P < 2 || P > sched::kMaxFusedPeers)
+        return fail(FMI_ERR_INVALID, "fused kernel needs 2 <= P <= 16, got " + std::to_string(P));
+    return with_op_dtype(op, dtype, [&]<class Op, class T>() -> int {
+        constexpr bool order_sensitive =
+            RANK_AWARE && std::is_floating_point_v<T> && (std::is_same_v<Op, OpMax> || std::is_same_v<Op, OpMin>);
+        static constexpr auto table =
+            fused_table<Op, T, ALG, order_sensitive>(std::make_integer_sequence<int, sched::kMaxFusedPeers - 1>{});
+        table[P - 2](ptrs, n, order_sensitive ? rank : 0, s);
+        return check_launch("fused P-way kernel launch");
+    });
+}
+
+}  // namespace fmi::dev

@@ -1,0 +1,12 @@
+// Fused single-pass peer-axis scans in the order of reference PeerToPeer::scan_no_order
+// (src/comm/PeerToPeer.cpp:154-184) and PeerToPeer::scan_ltr (src/comm/PeerToPeer.cpp:141-152).
+#include "fmi_fused_impl.h"
+
+namespace fmi::dev {
+int launch_fused_scan(int op, int dtype, int P, const PeerPtrs& ptrs, size_t n, hipStream_t s) {
+    return launch_fused<sched::kScan, false>(op, dtype, P, ptrs, n, 0, s);
+}
+int launch_fused_scan_ltr(int op, int dtype, int P, const PeerPtrs& ptrs, size_t n, hipStream_t s) {
+    return launch_fused<sched::kScanLtr, false>(op, dtype, P, ptrs, n, 0, s);
+}
+}  // namespace fmi::dev

@@ -1,0 +1,66 @@
+// fmi_internal.h — declarations shared by the translation units of libfmi_dev.so (not installed).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <string>
+
+#include "../../include/fmi_dev.h"
+#include "fmi_kernels.h"
+
+namespace fmi::dev {
+
+// Records a failure message for fmi_last_error() and returns `code`.
+int fail(int code, const std::string& msg);
+
+// Invoke f.template operator()<Op, T>() for a runtime (op, dtype); returns FMI_ERR_INVALID if unknown.
+template <class F>
+int with_op_dtype(int op, int dtype, F&& f) {
+    auto by_dtype = [&]<class Op>() -> int {
+        switch (dtype) {
+            case FMI_F32: return f.template operator()<Op, float>();
+            case FMI_F64: return f.template operator()<Op, double>();
+            case FMI_I32: return f.template operator()<Op, int32_t>();
+            case FMI_I64: return f.template operator()<Op, int64_t>();
+            default: return fail(FMI_ERR_INVALID, "unknown dtype " + std::to_string(dtype));
+        }
+    };
+    switch (op) {
+        case FMI_OP_SUM: return by_dtype.template operator()<OpSum>();
+        case FMI_OP_PROD: return by_dtype.template operator()<OpProd>();
+        case FMI_OP_MAX: return by_dtype.template operator()<OpMax>();
+        case FMI_OP_MIN: return by_dtype.template operator()<OpMin>();
+        default: return fail(FMI_ERR_INVALID, "unknown op " + std::to_string(op));
+    }
+}
+
+inline size_t dtype_size(int dtype) {
+    switch (dtype) {
+        case FMI_F32: return 4;
+        case FMI_F64: return 8;
+        case FMI_I32: return 4;
+        case FMI_I64: return 8;
+        default: return 0;
+    }
+}
+
+inline bool is_float(int dtype) { return dtype == FMI_F32 || dtype == FMI_F64; }
+
+// Fused single-pass launches (P in [2, kMaxFusedPeers], all pointers 16-B aligned). One function per
+// algorithm family, each defined in its own translation unit so the ~1.2k instantiations build in
+// parallel. Return 0 or a negative fmi_status_t.
+int launch_fused_allreduce(int op, int dtype, int P, const PeerPtrs& ptrs, size_t n, int rank, hipStream_t s);
+int launch_fused_reduce(int op, int dtype, int P, const PeerPtrs& ptrs, size_t n, hipStream_t s);
+int launch_fused_reduce_ltr(int op, int dtype, int P, const PeerPtrs& ptrs, size_t n, hipStream_t s);
+int launch_fused_scan(int op, int dtype, int P, const PeerPtrs& ptrs, size_t n, hipStream_t s);
+int launch_fused_scan_ltr(int op, int dtype, int P, const PeerPtrs& ptrs, size_t n, hipStream_t s);
+
+inline unsigned grid_for(size_t items, unsigned block) {
+    size_t g = (items + block - 1) / block;
+    if (g == 0) g = 1;
+    return static_cast<unsigned>(g);
+}
+
+}  // namespace fmi::dev

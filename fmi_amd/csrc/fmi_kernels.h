@@ -1,0 +1,304 @@
+// fmi_kernels.h — gfx950 (CDNA4) kernels for FMI's bucket reduction.
+//
+// All kernels here are HBM-streaming element-wise kernels (≈1/12 flop per byte for f32 add): there is
+// no dense contraction, so no MFMA and no LDS staging — the work is to keep enough 16-byte
+// loads in flight per CU that HBM3E, not latency, is the limit (MI355X_MICROARCH.md §HBM).
+//
+//   pair_tile / pair_stride   out[i] = op(a[i], b[i])          one pass: 2 reads + 1 write per element
+//   tree_kernel               out    = program(x0..x{P-1})     one pass: P reads + 1 write
+//   scan_kernel               outs[k]= program_k(x0..x{P-1})   one pass: P reads + P writes
+//   synth_kernel              counter-based synthetic buckets (splitmix64), identical to the host
+//
+// Every access is a 16-B global_load_dwordx4 / global_store_dwordx4 (4 f32/i32 or 2 f64/i64 lanes);
+// the < 16-B remainder of a bucket is handled by the first threads of block 0 with scalar accesses,
+// so a launch never touches a byte outside [0, n).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <type_traits>
+#include <utility>
+
+#include "fmi_schedule.h"
+
+namespace fmi::dev {
+
+// ---------------------------------------------------------------------------------------------------
+// Element ops. Semantics are the reference's built-ins (reference python/PythonCommunicator.h:131-149):
+// std::plus, std::multiplies, std::max(a,b) = (a<b)?b:a, std::min(a,b) = (b<a)?b:a — NOT fmaxf/fminf,
+// which differ on NaN and on signed zeros. Integer sum/prod wrap (computed in the unsigned type).
+// ---------------------------------------------------------------------------------------------------
+template <class T>
+struct Wrap {
+    using type = T;
+};
+template <>
+struct Wrap<int32_t> {
+    using type = uint32_t;
+};
+template <>
+struct Wrap<int64_t> {
+    using type = uint64_t;
+};
+
+struct OpSum {
+    template <class T>
+    __device__ __forceinline__ static T apply(T a, T b) {
+        using U = typename Wrap<T>::type;
+        return static_cast<T>(static_cast<U>(a) + static_cast<U>(b));
+    }
+};
+struct OpProd {
+    template <class T>
+    __device__ __forceinline__ static T apply(T a, T b) {
+        using U = typename Wrap<T>::type;
+        return static_cast<T>(static_cast<U>(a) * static_cast<U>(b));
+    }
+};
+struct OpMax {
+    template <class T>
+    __device__ __forceinline__ static T apply(T a, T b) {
+        return (a < b) ? b : a;
+    }
+};
+struct OpMin {
+    template <class T>
+    __device__ __forceinline__ static T apply(T a, T b) {
+        return (b < a) ? b : a;
+    }
+};
+
+// ---------------------------------------------------------------------------------------------------
+// 16-byte lane groups and their loads/stores.
+// ---------------------------------------------------------------------------------------------------
+template <class T, int W>
+struct alignas(sizeof(T) * W) Lanes {
+    T v[W];
+};
+
+template <class T>
+inline constexpr int kVecLanes = 16 / static_cast<int>(sizeof(T));
+
+using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
+
+template <bool NT, class T, int W>
+__device__ __forceinline__ Lanes<T, W> load_lanes(const T* p) {
+    if constexpr (NT && sizeof(T) * W == 16) {
+        const u32x4 r = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+        return __builtin_bit_cast(Lanes<T, W>, r);
+    } else {
+        return *reinterpret_cast<const Lanes<T, W>*>(p);
+    }
+}
+
+template <bool NT, class T, int W>
+__device__ __forceinline__ void store_lanes(T* p, const Lanes<T, W>& x) {
+    if constexpr (NT && sizeof(T) * W == 16) {
+        __builtin_nontemporal_store(__builtin_bit_cast(u32x4, x), reinterpret_cast<u32x4*>(p));
+    } else {
+        *reinterpret_cast<Lanes<T, W>*>(p) = x;
+    }
+}
+
+template <class Op, class T, int W>
+__device__ __forceinline__ Lanes<T, W> combine(const Lanes<T, W>& a, const Lanes<T, W>& b) {
+    Lanes<T, W> r;
+#pragma unroll
+    for (int k = 0; k < W; ++k) r.v[k] = Op::template apply<T>(a.v[k], b.v[k]);
+    return r;
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Pairwise combine. A "tile" is U vectors per thread: thread t of block b owns vectors
+// b*U*B + u*B + t (u < U), so each of the U wave-instructions is one contiguous 1-KiB access and each
+// thread keeps 2U independent 16-B loads in flight before its first add.
+// ---------------------------------------------------------------------------------------------------
+template <class Op, class T, int U, bool NT>
+__device__ __forceinline__ void pair_tile_body(T* out, const T* a, const T* b, size_t nvec, size_t tile) {
+    constexpr int W = kVecLanes<T>;
+    using L = Lanes<T, W>;
+    const size_t B = blockDim.x;
+    const size_t base = tile * U * B + threadIdx.x;
+    L va[U], vb[U];
+    if (tile * U * B + U * B <= nvec) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            va[u] = load_lanes<NT, T, W>(a + (base + u * B) * W);
+            vb[u] = load_lanes<NT, T, W>(b + (base + u * B) * W);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) store_lanes<NT, T, W>(out + (base + u * B) * W, combine<Op, T, W>(va[u], vb[u]));
+    } else {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const size_t i = base + u * B;
+            if (i < nvec) {
+                va[u] = load_lanes<NT, T, W>(a + i * W);
+                vb[u] = load_lanes<NT, T, W>(b + i * W);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const size_t i = base + u * B;
+            if (i < nvec) store_lanes<NT, T, W>(out + i * W, combine<Op, T, W>(va[u], vb[u]));
+        }
+    }
+}
+
+template <class Op, class T>
+__device__ __forceinline__ void pair_tail(T* out, const T* a, const T* b, size_t n) {
+    constexpr int W = kVecLanes<T>;
+    const size_t first = (n / W) * W;
+    if (blockIdx.x == 0 && first + threadIdx.x < n) {
+        const size_t i = first + threadIdx.x;
+        out[i] = Op::template apply<T>(a[i], b[i]);
+    }
+}
+
+// One-shot grid: one tile per workgroup. Pointers must be 16-B aligned.
+template <class Op, class T, int U, bool NT>
+__global__ void __launch_bounds__(1024) pair_tile(T* out, const T* a, const T* b, size_t n) {
+    const size_t nvec = n / kVecLanes<T>;
+    pair_tile_body<Op, T, U, NT>(out, a, b, nvec, blockIdx.x);
+    pair_tail<Op, T>(out, a, b, n);
+}
+
+// Grid-stride: a fixed grid (k workgroups per CU) walks the tiles. Pointers must be 16-B aligned.
+template <class Op, class T, int U, bool NT>
+__global__ void __launch_bounds__(1024) pair_stride(T* out, const T* a, const T* b, size_t n) {
+    const size_t nvec = n / kVecLanes<T>;
+    const size_t ntiles = (nvec + static_cast<size_t>(U) * blockDim.x - 1) / (static_cast<size_t>(U) * blockDim.x);
+    for (size_t t = blockIdx.x; t < ntiles; t += gridDim.x) pair_tile_body<Op, T, U, NT>(out, a, b, nvec, t);
+    pair_tail<Op, T>(out, a, b, n);
+}
+
+// Any alignment: scalar grid-stride loop.
+template <class Op, class T>
+__global__ void __launch_bounds__(256) pair_scalar(T* out, const T* a, const T* b, size_t n) {
+    for (size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+         i += static_cast<size_t>(gridDim.x) * blockDim.x)
+        out[i] = Op::template apply<T>(a[i], b[i]);
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Fused P-way kernels: evaluate a sched::Fused<ALG,P> program per 16-B lane group, every value in
+// registers. Indices into the value array are template constants (fold over index_sequence), so the
+// array is promoted to VGPRs — no scratch.
+// ---------------------------------------------------------------------------------------------------
+struct PeerPtrs {
+    const void* in[sched::kMaxFusedPeers];
+    void* out[sched::kMaxFusedPeers];
+};
+
+// Program fields as integral constants: reading them through these variable templates guarantees the
+// value-array indices are folded in the front end, so SROA keeps every value in VGPRs (no scratch).
+template <int ALG, int P, size_t S>
+inline constexpr int kStepA = sched::Fused<ALG, P>::prog.step[S].a;
+template <int ALG, int P, size_t S>
+inline constexpr int kStepB = sched::Fused<ALG, P>::prog.step[S].b;
+template <int ALG, int P, size_t R>
+inline constexpr int kOut = sched::Fused<ALG, P>::prog.out[R];
+template <int ALG, int P>
+inline constexpr int kNumSteps = sched::Fused<ALG, P>::prog.nsteps;
+
+template <class Op, class T, int W, int ALG, int P, size_t... S>
+__device__ __forceinline__ void run_steps(Lanes<T, W>* v, std::index_sequence<S...>) {
+    ((v[P + S] = combine<Op, T, W>(v[kStepA<ALG, P, S>], v[kStepB<ALG, P, S>])), ...);
+}
+
+template <class T, int W, int P, size_t... I>
+__device__ __forceinline__ void load_peers(Lanes<T, W>* v, const PeerPtrs& ptrs, size_t elem,
+                                           std::index_sequence<I...>) {
+    ((v[I] = load_lanes<false, T, W>(static_cast<const T*>(ptrs.in[I]) + elem)), ...);
+}
+
+template <class T, int W, int ALG, int P, size_t... R>
+__device__ __forceinline__ Lanes<T, W> pick_rank(const Lanes<T, W>* v, int rank, std::index_sequence<R...>) {
+    Lanes<T, W> r = v[kOut<ALG, P, 0>];
+    ((r = (rank == static_cast<int>(R)) ? v[kOut<ALG, P, R>] : r), ...);
+    return r;
+}
+
+template <class T, int W, int ALG, int P, size_t... R>
+__device__ __forceinline__ void store_all(const Lanes<T, W>* v, const PeerPtrs& ptrs, size_t elem,
+                                          std::index_sequence<R...>) {
+    ((store_lanes<false, T, W>(static_cast<T*>(ptrs.out[R]) + elem, v[kOut<ALG, P, R>])), ...);
+}
+
+// ALL_RANKS: honour `rank` (output = the value peer `rank` holds). Needed only where operand order can
+// change bits (float max/min on ±0); otherwise rank 0's expression is bit-identical for every peer.
+template <class Op, class T, int ALG, int P, bool ALL_RANKS, int W>
+__device__ __forceinline__ void tree_group(const PeerPtrs& ptrs, int rank, size_t elem) {
+    Lanes<T, W> v[P + kNumSteps<ALG, P>];
+    load_peers<T, W, P>(v, ptrs, elem, std::make_index_sequence<P>{});
+    run_steps<Op, T, W, ALG, P>(v, std::make_index_sequence<kNumSteps<ALG, P>>{});
+    Lanes<T, W> r;
+    if constexpr (ALL_RANKS)
+        r = pick_rank<T, W, ALG, P>(v, rank, std::make_index_sequence<P>{});
+    else
+        r = v[kOut<ALG, P, 0>];
+    store_lanes<false, T, W>(static_cast<T*>(ptrs.out[0]) + elem, r);
+}
+
+template <class Op, class T, int ALG, int P, bool ALL_RANKS>
+__global__ void __launch_bounds__(256) tree_kernel(PeerPtrs ptrs, size_t n, int rank) {
+    constexpr int W = kVecLanes<T>;
+    const size_t nvec = n / W;
+    const size_t g = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (g < nvec) tree_group<Op, T, ALG, P, ALL_RANKS, W>(ptrs, rank, g * W);
+    const size_t first = nvec * W;
+    if (blockIdx.x == 0 && first + threadIdx.x < n) tree_group<Op, T, ALG, P, ALL_RANKS, 1>(ptrs, rank, first + threadIdx.x);
+}
+
+template <class Op, class T, int ALG, int P, int W>
+__device__ __forceinline__ void scan_group(const PeerPtrs& ptrs, size_t elem) {
+    Lanes<T, W> v[P + kNumSteps<ALG, P>];
+    load_peers<T, W, P>(v, ptrs, elem, std::make_index_sequence<P>{});
+    run_steps<Op, T, W, ALG, P>(v, std::make_index_sequence<kNumSteps<ALG, P>>{});
+    store_all<T, W, ALG, P>(v, ptrs, elem, std::make_index_sequence<P>{});
+}
+
+template <class Op, class T, int ALG, int P>
+__global__ void __launch_bounds__(256) scan_kernel(PeerPtrs ptrs, size_t n) {
+    constexpr int W = kVecLanes<T>;
+    const size_t nvec = n / W;
+    const size_t g = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (g < nvec) scan_group<Op, T, ALG, P, W>(ptrs, g * W);
+    const size_t first = nvec * W;
+    if (blockIdx.x == 0 && first + threadIdx.x < n) scan_group<Op, T, ALG, P, 1>(ptrs, first + threadIdx.x);
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Synthetic buckets: h = splitmix64(seed ^ (peer << 40) ^ i).
+// ---------------------------------------------------------------------------------------------------
+__host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+    uint64_t z = x + 0x9e3779b97f4a7c15ull;
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+
+template <class T>
+__host__ __device__ __forceinline__ T synth_value(uint64_t h) {
+    if constexpr (std::is_same_v<T, float>) {
+        return static_cast<float>(h >> 40) * 0x1p-24f * 2.0f - 1.0f;
+    } else if constexpr (std::is_same_v<T, double>) {
+        return static_cast<double>(h >> 11) * 0x1p-53 * 2.0 - 1.0;
+    } else if constexpr (std::is_same_v<T, int32_t>) {
+        return static_cast<int32_t>(static_cast<uint32_t>(h >> 32));
+    } else {
+        return static_cast<int64_t>(h);
+    }
+}
+
+template <class T>
+__global__ void __launch_bounds__(256) synth_kernel(T* buf, size_t n, uint64_t seed, uint32_t peer) {
+    const uint64_t key = seed ^ (static_cast<uint64_t>(peer) << 40);
+    for (size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+         i += static_cast<size_t>(gridDim.x) * blockDim.x)
+        buf[i] = synth_value<T>(splitmix64(key ^ i));
+}
+
+}  // namespace fmi::dev

@@ -1,0 +1,171 @@
+// fmi_schedule.h — combine order of FMI's PeerToPeer collectives as a static single-assignment program.
+//
+// Each reference collective (reference src/comm/PeerToPeer.cpp) is a fixed pattern of sends, receives
+// and local combines `f.f(mine, received)`. Because every peer's sequence depends only on (P, peer id),
+// the whole collective collapses into a straight-line program over value ids:
+//
+//     values 0..P-1          = the peers' input buckets (x0 .. x{P-1})
+//     value  P+s             = op(value[step[s].a], value[step[s].b])     (left operand = arg 0 of f.f)
+//     out[r]                 = the value id peer r holds when the collective returns
+//
+// The fused HIP kernels (fmi_kernels.h) evaluate this program per element with every value in VGPRs,
+// so P buckets resident on one device reduce in ONE pass over HBM with the reference's exact bracketing.
+// Everything here is constexpr: the device instantiates programs at compile time (static register
+// indices after unrolling), the host builds the same programs at run time for P > kMaxFusedPeers.
+//
+// Round-synchronous restatement: in every round of every algorithm below a peer either sends or
+// receives+combines, never both, so a peer's outgoing value in round i is its value after round i-1.
+// That is why a single pass over peers per round reproduces the message-passing order exactly.
+#pragma once
+
+#include <cstdint>
+
+namespace fmi::sched {
+
+enum Alg : int {
+    kAllreduce = 0,  // reference PeerToPeer::allreduce_no_order  (src/comm/PeerToPeer.cpp:96-130)
+    kReduce = 1,     // reference PeerToPeer::reduce_no_order     (src/comm/PeerToPeer.cpp:59-84)
+    kReduceLtr = 2,  // reference PeerToPeer::reduce_ltr          (src/comm/PeerToPeer.cpp:44-57)
+    kScan = 3,       // reference PeerToPeer::scan_no_order       (src/comm/PeerToPeer.cpp:154-184)
+    kScanLtr = 4,    // reference PeerToPeer::scan_ltr            (src/comm/PeerToPeer.cpp:141-152)
+};
+
+inline constexpr int kMaxFusedPeers = 16;   // fused single-pass kernels are instantiated for P <= 16
+inline constexpr int kFusedStepCap = 80;    // >= max steps for P <= 16 (allreduce P=16: 64)
+inline constexpr int kMaxPeers = 64;        // run-time programs (pairwise passes) up to this P
+inline constexpr int kHostStepCap = 512;    // >= max steps for P <= 64 (allreduce P=64: 384)
+
+struct Step {
+    uint16_t a;  // left operand (the buffer f.f overwrites)
+    uint16_t b;  // right operand (the received buffer)
+};
+
+template <int CapSteps, int CapPeers>
+struct Program {
+    int peers = 0;
+    int nsteps = 0;
+    bool ok = true;  // false if the capacity was exceeded or arguments were invalid
+    Step step[CapSteps] = {};
+    uint16_t out[CapPeers] = {};
+
+    constexpr int nvalues() const { return peers + nsteps; }
+
+    constexpr uint16_t emit(uint16_t a, uint16_t b) {
+        if (nsteps >= CapSteps) {
+            ok = false;
+            return a;
+        }
+        step[nsteps] = Step{a, b};
+        return static_cast<uint16_t>(peers + nsteps++);
+    }
+};
+
+constexpr int floor_log2(int v) {
+    int r = 0;
+    while ((2 << r) <= v) ++r;
+    return r;
+}
+
+constexpr int ceil_log2(int v) {
+    int r = 0;
+    while ((1 << r) < v) ++r;
+    return r;
+}
+
+// Build the program of `alg` for P peers. Ids are *transformed* ids for kReduce (root -> 0, reference
+// PeerToPeer::transform_peer_id, src/comm/PeerToPeer.cpp:287-293): the caller rotates its inputs so
+// that input t is real peer (t + root) % P; out[0] is then the root's result.
+template <int CapSteps, int CapPeers>
+constexpr Program<CapSteps, CapPeers> build(int alg, int P) {
+    Program<CapSteps, CapPeers> prog{};
+    if (P < 1 || P > CapPeers) {
+        prog.ok = false;
+        return prog;
+    }
+    prog.peers = P;
+    uint16_t cur[CapPeers] = {};
+    for (int p = 0; p < P; ++p) cur[p] = static_cast<uint16_t>(p);
+
+    switch (alg) {
+        case kAllreduce: {
+            // Peers >= 2^floor(log2 P) first hand their bucket to peer - 2^k, which combines it as
+            // f(own, received) (:100-107); recursive doubling over the power-of-two group, every pair
+            // combining f(own, partner's value from the previous round) (:108-121); the folded peers
+            // get the final value back (:122-128).
+            const int rounds = floor_log2(P);
+            const int pow2 = 1 << rounds;
+            for (int p = pow2; p < P; ++p) cur[p - pow2] = prog.emit(cur[p - pow2], cur[p]);
+            for (int i = 0; i < rounds; ++i) {
+                uint16_t prev[CapPeers] = {};
+                for (int p = 0; p < pow2; ++p) prev[p] = cur[p];
+                for (int p = 0; p < pow2; ++p) cur[p] = prog.emit(prev[p], prev[p ^ (1 << i)]);
+            }
+            for (int p = pow2; p < P; ++p) cur[p] = cur[p - pow2];
+            break;
+        }
+        case kReduce: {
+            // Binomial tree on transformed ids: in round i every t that is a multiple of 2^(i+1)
+            // receives from t + 2^i (if it exists) and combines f(own, received) (:66-78).
+            const int rounds = ceil_log2(P);
+            for (int i = 0; i < rounds; ++i) {
+                const int span = 1 << i;
+                for (int t = 0; t + span < P; t += 2 * span) cur[t] = prog.emit(cur[t], cur[t + span]);
+            }
+            break;  // out[t != 0] is a non-root's partial; only out[0] (the root) is meaningful
+
+        }
+        case kReduceLtr: {
+            // Root gathers all buckets by real id and folds left to right: ((x0 + x1) + x2) + ... (:49-52).
+            // The allreduce variant broadcasts the root's result, so every peer ends with it.
+            uint16_t acc = 0;
+            for (int p = 1; p < P; ++p) acc = prog.emit(acc, static_cast<uint16_t>(p));
+            for (int p = 0; p < P; ++p) cur[p] = acc;
+            break;
+        }
+        case kScan: {
+            // Up-sweep: in round i a peer whose low i+1 bits are all ones receives from peer - 2^i and
+            // combines f(own, received); its partner (low i bits ones, bit i zero) sends (:156-168).
+            // Down-sweep from round floor(log2 P) to 1: peers with low i bits all ones send to
+            // peer + 2^(i-1); peers with only the low i-1 bits ones receive from peer - 2^(i-1) (if > 0)
+            // and combine f(own, received) (:169-182).
+            const int rounds = floor_log2(P);
+            for (int i = 0; i < rounds; ++i) {
+                const int full = (1 << (i + 1)) - 1;
+                for (int p = 0; p < P; ++p)
+                    if ((p & full) == full) cur[p] = prog.emit(cur[p], cur[p - (1 << i)]);
+            }
+            for (int i = rounds; i > 0; --i) {
+                const int hi = (1 << i) - 1;
+                const int lo = (1 << (i - 1)) - 1;
+                for (int p = 0; p < P; ++p) {
+                    if ((p & hi) == hi) continue;  // sender this round
+                    const int src = p - (1 << (i - 1));
+                    if ((p & lo) == lo && src > 0) cur[p] = prog.emit(cur[p], cur[src]);
+                }
+            }
+            break;
+        }
+        case kScanLtr: {
+            // Linear chain: peer k receives the prefix of k-1 and combines f(prefix, own) (:146-147).
+            for (int p = 1; p < P; ++p) cur[p] = prog.emit(cur[p - 1], static_cast<uint16_t>(p));
+            break;
+        }
+        default:
+            prog.ok = false;
+            return prog;
+    }
+    for (int p = 0; p < P; ++p) prog.out[p] = cur[p];
+    return prog;
+}
+
+template <int Alg_, int P>
+struct Fused {
+    static constexpr Program<kFusedStepCap, kMaxFusedPeers> prog = build<kFusedStepCap, kMaxFusedPeers>(Alg_, P);
+    static_assert(prog.ok, "fused schedule exceeds capacity");
+};
+
+using HostProgram = Program<kHostStepCap, kMaxPeers>;
+
+inline HostProgram build_host(int alg, int P) { return build<kHostStepCap, kMaxPeers>(alg, P); }
+
+}  // namespace fmi::sched

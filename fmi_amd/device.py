@@ -1,0 +1,285 @@
+"""Host-side handle to the gfx950 bucket-reduction engine (thin layer over include/fmi_dev.h).
+
+Names follow FMI's vocabulary: a *bucket* is one peer's contiguous buffer (reference
+include/comm/Data.h:50-73, `Data<std::vector<A>>`), an *op* is one of the reference's built-in
+reduction functions (reference python/PythonCommunicator.h:131-149), and the P-way entry points
+reproduce the combine order of a reference collective (reference src/comm/PeerToPeer.cpp).
+"""
+from __future__ import annotations
+
+import ctypes
+import enum
+from typing import Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+
+
+class Op(enum.IntEnum):
+    """Reference Python op enum SUM/PROD/MAX/MIN (reference python/PythonCommunicator.h:13-15)."""
+    SUM = 0
+    PROD = 1
+    MAX = 2
+    MIN = 3
+
+
+class DType(enum.IntEnum):
+    F32 = 0
+    F64 = 1
+    I32 = 2
+    I64 = 3
+
+
+class Alg(enum.IntEnum):
+    """Evaluation orders of the reference collectives (src/comm/PeerToPeer.cpp)."""
+    ALLREDUCE = 0   # allreduce_no_order  :96-130
+    REDUCE = 1      # reduce_no_order     :59-84
+    REDUCE_LTR = 2  # reduce_ltr          :44-57
+    SCAN = 3        # scan_no_order       :154-184
+    SCAN_LTR = 4    # scan_ltr            :141-152
+
+
+class Tune(enum.IntEnum):
+    PAIR_VARIANT = 0
+    PAIR_UNROLL = 1
+    BLOCK = 2
+    GRID_PER_CU = 3
+    HOST_CHUNK = 4
+
+
+NP_DTYPE = {DType.F32: np.float32, DType.F64: np.float64, DType.I32: np.int32, DType.I64: np.int64}
+
+
+def dtype_of(arr_or_dtype) -> DType:
+    dt = np.dtype(getattr(arr_or_dtype, "dtype", arr_or_dtype))
+    for k, v in NP_DTYPE.items():
+        if np.dtype(v) == dt:
+            return k
+    raise TypeError(f"unsupported bucket dtype {dt}; FMI device buckets are f32, f64, i32 or i64")
+
+
+def _ptr(x) -> Optional[int]:
+    if x is None:
+        return None
+    if isinstance(x, Bucket):
+        return x.ptr
+    if isinstance(x, int):
+        return x
+    raise TypeError(f"expected a Bucket or a raw device pointer, got {type(x)}")
+
+
+def _sptr(stream) -> Optional[int]:
+    if stream is None:
+        return None
+    return stream.handle if isinstance(stream, Stream) else int(stream)
+
+
+# ----------------------------------------------------------------------------------------------------
+# device / memory
+# ----------------------------------------------------------------------------------------------------
+def device_count() -> int:
+    c = ctypes.c_int(0)
+    _lib.call("fmi_dev_count", ctypes.byref(c))
+    return c.value
+
+
+def init(device: int = 0) -> None:
+    _lib.call("fmi_dev_init", device)
+
+
+def finalize() -> None:
+    _lib.call("fmi_dev_finalize")
+
+
+def sync() -> None:
+    _lib.call("fmi_dev_sync")
+
+
+def describe() -> str:
+    buf = ctypes.create_string_buffer(512)
+    _lib.call("fmi_dev_describe", buf, len(buf))
+    return buf.value.decode()
+
+
+class Bucket:
+    """A device-resident bucket of `n` elements of `dtype` (owns its HBM allocation unless `view`)."""
+
+    def __init__(self, n: int, dtype, ptr: Optional[int] = None, owner: Optional["Bucket"] = None):
+        self.dtype = dtype_of(dtype) if not isinstance(dtype, DType) else dtype
+        self.n = int(n)
+        self.itemsize = np.dtype(NP_DTYPE[self.dtype]).itemsize
+        self._owner = owner
+        if ptr is None:
+            p = ctypes.c_void_p()
+            _lib.call("fmi_dev_alloc", ctypes.byref(p), self.nbytes)
+            self.ptr = p.value
+            self._owns = True
+        else:
+            self.ptr = ptr
+            self._owns = False
+
+    @property
+    def nbytes(self) -> int:
+        return self.n * self.itemsize
+
+    @classmethod
+    def from_numpy(cls, arr: np.ndarray, stream=None) -> "Bucket":
+        arr = np.ascontiguousarray(arr)
+        b = cls(arr.size, dtype_of(arr))
+        b.upload(arr, stream)
+        return b
+
+    def view(self, offset: int, n: int) -> "Bucket":
+        """Sub-bucket starting `offset` elements in (used to exercise unaligned buckets)."""
+        if offset < 0 or offset + n > self.n:
+            raise ValueError("view out of range")
+        return Bucket(n, self.dtype, ptr=self.ptr + offset * self.itemsize, owner=self)
+
+    def upload(self, arr: np.ndarray, stream=None) -> None:
+        arr = np.ascontiguousarray(arr, dtype=NP_DTYPE[self.dtype])
+        if arr.size != self.n:
+            raise ValueError(f"size mismatch: bucket has {self.n} elements, array {arr.size}")
+        _lib.call("fmi_dev_h2d_async", self.ptr, arr.ctypes.data, self.nbytes, _sptr(stream))
+        _lib.call("fmi_stream_sync", _sptr(stream))
+
+    def numpy(self, stream=None) -> np.ndarray:
+        out = np.empty(self.n, dtype=NP_DTYPE[self.dtype])
+        _lib.call("fmi_dev_d2h_async", out.ctypes.data, self.ptr, self.nbytes, _sptr(stream))
+        _lib.call("fmi_stream_sync", _sptr(stream))
+        return out
+
+    def fill_synthetic(self, seed: int, peer: int, stream=None) -> "Bucket":
+        _lib.call("fmi_dev_fill_synthetic", int(self.dtype), self.ptr, self.n, seed, peer, _sptr(stream))
+        return self
+
+    def copy_from(self, other: "Bucket", stream=None) -> None:
+        if other.nbytes != self.nbytes:
+            raise ValueError("size mismatch")
+        _lib.call("fmi_dev_d2d_async", self.ptr, other.ptr, self.nbytes, _sptr(stream))
+
+    def free(self) -> None:
+        if self._owns and self.ptr:
+            _lib.call("fmi_dev_free", self.ptr)
+        self.ptr = 0
+        self._owns = False
+
+    def __del__(self):
+        try:
+            if getattr(self, "_owns", False) and self.ptr:
+                _lib.load().fmi_dev_free(self.ptr)
+        except Exception:
+            pass
+
+
+class Stream:
+    def __init__(self):
+        h = ctypes.c_void_p()
+        _lib.call("fmi_stream_create", ctypes.byref(h))
+        self.handle = h.value
+
+    def sync(self) -> None:
+        _lib.call("fmi_stream_sync", self.handle)
+
+    def destroy(self) -> None:
+        if self.handle:
+            _lib.call("fmi_stream_destroy", self.handle)
+            self.handle = None
+
+
+class Event:
+    def __init__(self):
+        h = ctypes.c_void_p()
+        _lib.call("fmi_event_create", ctypes.byref(h))
+        self.handle = h.value
+
+    def record(self, stream=None) -> "Event":
+        _lib.call("fmi_event_record", self.handle, _sptr(stream))
+        return self
+
+    def sync(self) -> None:
+        _lib.call("fmi_event_sync", self.handle)
+
+    def elapsed_ms(self, end: "Event") -> float:
+        ms = ctypes.c_float()
+        _lib.call("fmi_event_elapsed_ms", ctypes.byref(ms), self.handle, end.handle)
+        return float(ms.value)
+
+    def destroy(self) -> None:
+        if self.handle:
+            _lib.call("fmi_event_destroy", self.handle)
+            self.handle = None
+
+
+# ----------------------------------------------------------------------------------------------------
+# hot path
+# ----------------------------------------------------------------------------------------------------
+def reduce_pair(op: Op, inout: Bucket, src: Bucket, n: Optional[int] = None, stream=None) -> None:
+    """inout = op(inout, src) elementwise — one reference `f.f(a, b)` (include/Communicator.h:180-189)."""
+    n = inout.n if n is None else n
+    if src.dtype != inout.dtype or src.n < n or inout.n < n:
+        raise ValueError("reduce_pair: buckets must share dtype and hold n elements")
+    _lib.call("fmi_dev_reduce_pair", int(op), int(inout.dtype), inout.ptr, src.ptr, n, _sptr(stream))
+
+
+def combine(op: Op, out: Bucket, a: Bucket, b: Bucket, stream=None) -> None:
+    if not (out.dtype == a.dtype == b.dtype) or not (out.n == a.n == b.n):
+        raise ValueError("combine: buckets must share dtype and length")
+    _lib.call("fmi_dev_combine", int(op), int(out.dtype), out.ptr, a.ptr, b.ptr, out.n, _sptr(stream))
+
+
+def _ptr_array(buckets: Sequence[Bucket]):
+    arr = (ctypes.c_void_p * len(buckets))()
+    for i, b in enumerate(buckets):
+        arr[i] = b.ptr
+    return arr
+
+
+def reduce_tree(op: Op, alg: Alg, out: Bucket, ins: Sequence[Bucket], rank: int = 0, stream=None) -> None:
+    """P-way reduction with a reference collective's bracketing (see include/fmi_dev.h)."""
+    _check_peers(out, ins)
+    _lib.call("fmi_dev_reduce_tree", int(op), int(out.dtype), int(alg), out.ptr, _ptr_array(ins), len(ins), rank,
+              out.n, _sptr(stream))
+
+
+def scan_peers(op: Op, alg: Alg, outs: Sequence[Bucket], ins: Sequence[Bucket], stream=None) -> None:
+    """Peer-axis inclusive scan with the bracketing of reference scan_no_order / scan_ltr."""
+    if len(outs) != len(ins):
+        raise ValueError("scan_peers: one output bucket per peer")
+    for o in outs:
+        _check_peers(o, ins)
+    _lib.call("fmi_dev_scan_peers", int(op), int(outs[0].dtype), int(alg), _ptr_array(outs), _ptr_array(ins),
+              len(ins), outs[0].n, _sptr(stream))
+
+
+def host_reduce_pair(op: Op, inout: np.ndarray, src: np.ndarray) -> None:
+    """inout = op(inout, src) for host arrays, streamed through the device (H2D, kernel, D2H)."""
+    if inout.dtype != src.dtype or inout.size != src.size:
+        raise ValueError("host_reduce_pair: arrays must share dtype and size")
+    if not (inout.flags.c_contiguous and src.flags.c_contiguous):
+        raise ValueError("host_reduce_pair: arrays must be contiguous")
+    _lib.call("fmi_host_reduce_pair", int(op), int(dtype_of(inout)), inout.ctypes.data, src.ctypes.data, inout.size)
+
+
+def _check_peers(out: Bucket, ins: Sequence[Bucket]) -> None:
+    if not ins:
+        raise ValueError("need at least one peer bucket")
+    for b in ins:
+        if b.dtype != out.dtype or b.n != out.n:
+            raise ValueError("all peer buckets must share dtype and length")
+
+
+def schedule_expr(alg: Alg, P: int, rank: int) -> str:
+    buf = ctypes.create_string_buffer(1 << 16)
+    _lib.call("fmi_schedule_expr", int(alg), P, rank, buf, len(buf))
+    return buf.value.decode()
+
+
+def tune_set(key: Tune, value: int) -> None:
+    _lib.call("fmi_tune_set", int(key), int(value))
+
+
+def tune_get(key: Tune) -> int:
+    v = ctypes.c_longlong()
+    _lib.call("fmi_tune_get", int(key), ctypes.byref(v))
+    return v.value

@@ -1,0 +1,168 @@
+/*
+ * fmi_dev.h — C-ABI of the MI355X (gfx950) bucket-reduction engine behind FMI's collectives.
+ *
+ * This is the drop-in boundary for FMI's local element-wise bucket reduction. In the reference the
+ * reduction is an opaque host closure, `raw_func = std::function<void(char*, char*)>`
+ * (reference include/comm/Channel.h:16-23), built by Communicator::convert_to_raw_function
+ * (reference include/Communicator.h:170-189) and applied by the PeerToPeer collectives as
+ * `f.f(inout, in)` (reference src/comm/PeerToPeer.cpp:51,72,103,119,147,160,179).
+ * Here the same combine is a HIP kernel launch on device-resident buckets, addressed by an explicit
+ * op/dtype descriptor because the reference's closure carries neither.
+ *
+ * Conventions:
+ *   - every entry point returns int: 0 = success, negative = fmi_status_t error; the message of the
+ *     last failure on the calling thread is available from fmi_last_error(). No exception ever
+ *     crosses this boundary; the C++ layer (fmi_amd/cpp/include/fmi/) rethrows std::runtime_error.
+ *   - plain pointers and element counts only; no torch / HIP types in signatures. A stream is an
+ *     opaque handle (hipStream_t underneath); NULL means the library's default stream of the device
+ *     selected by fmi_dev_init.
+ *   - the caller owns every buffer passed in; the library owns only its streams, events and scratch.
+ *   - `inout`/`in` follow raw_func: argument 0 is overwritten, argument 1 is read-only, equal length.
+ *   - all launches are asynchronous on the given stream; fmi_stream_sync / fmi_dev_sync wait.
+ *
+ * Element semantics match the reference's built-in ops (reference python/PythonCommunicator.h:116-149):
+ *   SUM = a + b (std::plus), PROD = a * b (std::multiplies), MAX = std::max(a,b) = (a < b) ? b : a,
+ *   MIN = std::min(a,b) = (b < a) ? b : a. Integer SUM/PROD wrap modulo 2^bits (two's complement), as
+ *   the reference's int32 13! test relies on (reference tests/channels.cpp:419-465). Floats use IEEE
+ *   round-to-nearest-even with denormals preserved and no contraction: a single device combine is
+ *   bit-identical to the host one.
+ */
+#ifndef FMI_DEV_H
+#define FMI_DEV_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FMI_DEV_ABI_VERSION 1
+
+/* ---- status ------------------------------------------------------------------------------------ */
+typedef enum {
+    FMI_OK = 0,
+    FMI_ERR_INVALID = -1,     /* bad argument (null pointer, unknown op/dtype, P out of range ...) */
+    FMI_ERR_HIP = -2,         /* a HIP runtime call failed; message names the call */
+    FMI_ERR_NO_DEVICE = -3,   /* no gfx950 device visible / fmi_dev_init not called */
+    FMI_ERR_UNSUPPORTED = -4, /* combination not implemented */
+    FMI_ERR_ALLOC = -5        /* device or pinned allocation failed */
+} fmi_status_t;
+
+/* ---- op / dtype / algorithm descriptors -------------------------------------------------------- */
+/* Op ids mirror the reference Python enum SUM/PROD/MAX/MIN (reference python/PythonCommunicator.h:13-15). */
+typedef enum { FMI_OP_SUM = 0, FMI_OP_PROD = 1, FMI_OP_MAX = 2, FMI_OP_MIN = 3 } fmi_op_t;
+typedef enum { FMI_F32 = 0, FMI_F64 = 1, FMI_I32 = 2, FMI_I64 = 3 } fmi_dtype_t;
+
+/* Evaluation orders reproduced by the P-way kernels; each is the combine order of one reference
+ * collective, so a P-bucket reduction on one device is bit-identical to the distributed one. */
+typedef enum {
+    FMI_ALG_ALLREDUCE = 0,  /* recursive doubling + non-power-of-2 fold: PeerToPeer.cpp:96-130   */
+    FMI_ALG_REDUCE = 1,     /* binomial tree toward root (transformed ids): PeerToPeer.cpp:59-84  */
+    FMI_ALG_REDUCE_LTR = 2, /* gather + sequential left fold at root: PeerToPeer.cpp:44-57         */
+    FMI_ALG_SCAN = 3,       /* binomial up/down sweep, own-op-received: PeerToPeer.cpp:154-184     */
+    FMI_ALG_SCAN_LTR = 4    /* linear chain, prefix-op-own: PeerToPeer.cpp:141-152                 */
+} fmi_alg_t;
+
+typedef void* fmi_stream_t;
+typedef void* fmi_event_t;
+
+/* ---- library / device -------------------------------------------------------------------------- */
+int fmi_abi_version(void);
+/* Message of the last failed call on this thread ("" if none). Valid until the next failing call. */
+const char* fmi_last_error(void);
+/* Number of visible HIP devices (0 on a host without a GPU; never fails for lack of a device). */
+int fmi_dev_count(int* count);
+/* Select the device for this thread and create the library's default stream for it.
+ * Fails with FMI_ERR_NO_DEVICE if the device is missing or is not gfx950. */
+int fmi_dev_init(int device);
+/* Release the library's streams and scratch (mirrors Channel::finalize, reference
+ * include/comm/Channel.h:106). Buffers allocated by the caller are not touched. */
+int fmi_dev_finalize(void);
+/* Wait for all work on the selected device. */
+int fmi_dev_sync(void);
+/* Device name + arch string (e.g. "AMD Instinct MI355X gfx950"), NUL-terminated into buf. */
+int fmi_dev_describe(char* buf, size_t len);
+
+/* ---- memory (replaces the reference's new[]/std::vector bucket storage, include/comm/Data.h:50-97) */
+int fmi_dev_alloc(void** ptr, size_t bytes);
+int fmi_dev_free(void* ptr);
+int fmi_host_pin_alloc(void** ptr, size_t bytes);  /* page-locked host memory for recv buffers */
+int fmi_host_pin_free(void* ptr);
+int fmi_dev_h2d_async(void* dst, const void* src, size_t bytes, fmi_stream_t stream);
+int fmi_dev_d2h_async(void* dst, const void* src, size_t bytes, fmi_stream_t stream);
+int fmi_dev_d2d_async(void* dst, const void* src, size_t bytes, fmi_stream_t stream);
+int fmi_dev_memset_async(void* dst, int value, size_t bytes, fmi_stream_t stream);
+
+/* ---- streams / events (timing is taken on the stream the kernels run on) ----------------------- */
+int fmi_stream_create(fmi_stream_t* stream);
+int fmi_stream_destroy(fmi_stream_t stream);
+int fmi_stream_sync(fmi_stream_t stream);
+int fmi_event_create(fmi_event_t* event);
+int fmi_event_destroy(fmi_event_t event);
+int fmi_event_record(fmi_event_t event, fmi_stream_t stream);
+int fmi_event_sync(fmi_event_t event);
+int fmi_event_elapsed_ms(float* ms, fmi_event_t start, fmi_event_t stop);
+
+/* ---- the hot path ------------------------------------------------------------------------------ */
+/* Pairwise bucket combine: inout[i] = op(inout[i], in[i]) for i < n.
+ * Replaces one application of the raw_func built by Communicator::convert_to_raw_function
+ * (reference include/Communicator.h:180-189) at the PeerToPeer combine sites
+ * (reference src/comm/PeerToPeer.cpp:51,72,103,119,147,160,179). inout == in is allowed. */
+int fmi_dev_reduce_pair(int op, int dtype, void* inout, const void* in, size_t n, fmi_stream_t stream);
+
+/* Out-of-place pairwise combine: out[i] = op(a[i], b[i]); out may alias a or b. */
+int fmi_dev_combine(int op, int dtype, void* out, const void* a, const void* b, size_t n,
+                    fmi_stream_t stream);
+
+/* P-way reduction of P device buckets in one pass with the evaluation order of `alg`
+ * (FMI_ALG_ALLREDUCE / FMI_ALG_REDUCE / FMI_ALG_REDUCE_LTR): out = the value peer `rank` holds at the
+ * end of the reference collective (for FMI_ALG_REDUCE `rank` is the root; for ALLREDUCE it selects
+ * whose operand order is reproduced, which differs only for float MAX/MIN on signed zeros).
+ * Replaces the whole chain of f.f calls of reference PeerToPeer::allreduce_no_order / reduce_no_order /
+ * reduce_ltr (src/comm/PeerToPeer.cpp:96-130, :59-84, :44-57) for buckets that sit on one device.
+ * ins[p] = bucket of peer p (p < P); out may alias any ins[p]. P in [1, 64]; P <= 16 runs as a single
+ * fused kernel, larger P as a sequence of pairwise passes with the identical order. */
+int fmi_dev_reduce_tree(int op, int dtype, int alg, void* out, const void* const* ins, int P, int rank,
+                        size_t n, fmi_stream_t stream);
+
+/* Peer-axis inclusive scan of P device buckets: outs[k] = x0 (+) ... (+) xk with the evaluation order
+ * of `alg` (FMI_ALG_SCAN or FMI_ALG_SCAN_LTR). Replaces reference PeerToPeer::scan_no_order / scan_ltr
+ * (src/comm/PeerToPeer.cpp:154-184, :141-152) and Communicator::scan (include/Communicator.h:135-150)
+ * when the P buckets sit on one device. outs[k] may alias ins[k]. P in [1, 64] as above. */
+int fmi_dev_scan_peers(int op, int dtype, int alg, void* const* outs, const void* const* ins, int P,
+                       size_t n, fmi_stream_t stream);
+
+/* Host-resident pairwise combine through the device: pinned (or pageable) host `inout`/`in` are
+ * streamed through device staging in chunks (H2D, kernel, D2H overlapped on two streams).
+ * This is the path a recv buffer arriving over a host channel takes (reference
+ * src/comm/Direct.cpp:36-45 → PeerToPeer.cpp:119). Synchronous: returns when inout is updated. */
+int fmi_host_reduce_pair(int op, int dtype, void* inout, const void* in, size_t n);
+
+/* ---- synthetic buckets (identical on host and device: SURVEY.md §8d generator) ------------------
+ * h = splitmix64(seed ^ ((uint64)peer << 40) ^ i);  f32 = (float)((h >> 40) * 2^-24) * 2 - 1,
+ * f64 = (double)((h >> 11) * 2^-53) * 2 - 1,  i32 = (int32)(h >> 32),  i64 = (int64)h. */
+int fmi_dev_fill_synthetic(int dtype, void* buf, size_t n, uint64_t seed, uint32_t peer,
+                           fmi_stream_t stream);
+
+/* ---- schedule introspection (host-only logic, no device needed) --------------------------------
+ * Writes the symbolic combine expression peer `rank` ends with, e.g. "((x0+x1)+(x2+x3))", as the
+ * fused kernels evaluate it. Used by the parity tests to pin the order against the reference's. */
+int fmi_schedule_expr(int alg, int P, int rank, char* buf, size_t len);
+
+/* ---- tuning knobs (performance only, never semantics) ------------------------------------------ */
+typedef enum {
+    FMI_TUNE_PAIR_VARIANT = 0, /* 0 = one-shot tiles (default), 1 = grid-stride, 2 = nontemporal */
+    FMI_TUNE_PAIR_UNROLL = 1,  /* 16-B vectors per thread per operand: 1, 2, 4, 8 */
+    FMI_TUNE_BLOCK = 2,        /* threads per workgroup: 256, 512, 1024 */
+    FMI_TUNE_GRID_PER_CU = 3,  /* workgroups per CU for the grid-stride variant */
+    FMI_TUNE_HOST_CHUNK = 4    /* bytes per chunk of fmi_host_reduce_pair */
+} fmi_tune_key_t;
+int fmi_tune_set(int key, long long value);
+int fmi_tune_get(int key, long long* value);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FMI_DEV_H */

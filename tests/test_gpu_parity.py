@@ -1,0 +1,299 @@
+"""Parity of the HIP path (through the C-ABI) against the CPU oracle on the same inputs.
+
+Bar: bit-exact for every op and dtype — integer work trivially, float work because the kernels
+evaluate the reference's own bracketing. Comparisons are on raw bits (NaN payloads
+and signed zeros included). Sizes: ragged small cases the oracle finishes instantly, the edge values
+the reference's element semantics cover, and BASELINE.json's full configs C2 (256 MiB f32 pairwise sum)
+and C3 (64 MiB i64 max, 8 × 64 MiB f32 peer scan).
+"""
+import numpy as np
+import pytest
+
+import fmi_amd
+from fmi_amd import Alg, Bucket, Op, Tune
+from oracle import fmi_oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+DTYPES = [np.float32, np.float64, np.int32, np.int64]
+OPS = [Op.SUM, Op.PROD, Op.MAX, Op.MIN]
+OPNAME = {Op.SUM: "sum", Op.PROD: "prod", Op.MAX: "max", Op.MIN: "min"}
+RAGGED = [0, 1, 2, 3, 4, 5, 7, 8, 9, 15, 17, 1027, 4099, 65536 + 3]
+
+
+UINT = {4: np.uint32, 8: np.uint64}
+
+
+def assert_bit_equal(got, want, what=""):
+    """Bit-exact comparison. The one relaxation: a NaN matches any NaN. IEEE leaves the payload/sign of a
+    NaN produced by an invalid operation (inf - inf, 0 * inf) to the implementation — x86 SSE returns
+    the 'default NaN' 0xFFC00000, CDNA 0x7FC00000 — so NaN-ness, not its bits, is the contract."""
+    got, want = np.asarray(got), np.asarray(want)
+    assert got.dtype == want.dtype and got.shape == want.shape, what
+    u = UINT[got.dtype.itemsize]
+    same = got.view(u) == want.view(u)
+    if np.issubdtype(got.dtype, np.floating):
+        same |= np.isnan(got) & np.isnan(want)
+    if not same.all():
+        diff = np.nonzero(~same)[0]
+        i = diff[0]
+        raise AssertionError(f"{what}: {diff.size} mismatching elements, first at {i}: got {got[i]!r} "
+                             f"want {want[i]!r}")
+
+
+def inputs(dtype, n, peer, seed=42):
+    """Synthetic bucket, with edge values sprinkled in for the element semantics."""
+    x = orc.synthetic(dtype, n, seed=seed, peer=peer)
+    if n >= 8:
+        if np.issubdtype(dtype, np.floating):
+            edge = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, np.finfo(dtype).tiny / 4, -np.finfo(dtype).max,
+                             np.finfo(dtype).smallest_subnormal], dtype=dtype)
+        else:
+            info = np.iinfo(dtype)
+            edge = np.array([info.min, info.max, 0, -1, 1, info.min + 1, info.max - 1, 2], dtype=dtype)
+        idx = (np.arange(8) * 7919 + peer * 13) % n
+        x[idx] = np.roll(edge, peer)
+    return x
+
+
+def dev(arr):
+    return Bucket.from_numpy(arr)
+
+
+# ------------------------------------------------------------------------------------------------
+# pairwise combine — the hot path (reference include/Communicator.h:180-189)
+# ------------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("dtype", DTYPES, ids=lambda d: np.dtype(d).name)
+@pytest.mark.parametrize("op", OPS, ids=lambda o: o.name)
+def test_reduce_pair_ragged(device, op, dtype):
+    for n in RAGGED:
+        a, b = inputs(dtype, n, 0), inputs(dtype, n, 1)
+        da, db = dev(a), dev(b)
+        fmi_amd.reduce_pair(op, da, db)
+        with np.errstate(all="ignore"):
+            want = orc.pairwise(OPNAME[op], a, b)
+        assert_bit_equal(da.numpy(), want, f"{op.name} {np.dtype(dtype).name} n={n}")
+        assert_bit_equal(db.numpy(), b, "in operand must stay untouched")
+
+
+@pytest.mark.parametrize("dtype", DTYPES, ids=lambda d: np.dtype(d).name)
+def test_reduce_pair_unaligned_views(device, dtype):
+    n = 4099
+    a, b = inputs(dtype, n + 8, 0), inputs(dtype, n + 8, 1)
+    for off_a, off_b in [(1, 1), (1, 2), (3, 0), (0, 5)]:
+        da, db = dev(a), dev(b)
+        va, vb = da.view(off_a, n), db.view(off_b, n)
+        fmi_amd.reduce_pair(Op.SUM, va, vb)
+        with np.errstate(all="ignore"):
+            want = a.copy()
+            want[off_a:off_a + n] = orc.pairwise("sum", a[off_a:off_a + n], b[off_b:off_b + n])
+        assert_bit_equal(da.numpy(), want, f"offsets {off_a},{off_b}")
+
+
+def test_reduce_pair_inplace_alias(device):
+    a = inputs(np.float32, 10007, 0)
+    da = dev(a)
+    fmi_amd.reduce_pair(Op.SUM, da, da)
+    assert_bit_equal(da.numpy(), a + a)
+
+
+@pytest.mark.parametrize("variant,unroll,block", [(v, u, b) for v in (0, 1, 2) for u in (1, 2, 4, 8)
+                                                  for b in (256, 1024)])
+def test_reduce_pair_every_launch_variant(device, variant, unroll, block):
+    n = (1 << 20) + 3
+    a, b = inputs(np.float32, n, 0), inputs(np.float32, n, 1)
+    old = {k: fmi_amd.tune_get(k) for k in (Tune.PAIR_VARIANT, Tune.PAIR_UNROLL, Tune.BLOCK)}
+    try:
+        fmi_amd.tune_set(Tune.PAIR_VARIANT, variant)
+        fmi_amd.tune_set(Tune.PAIR_UNROLL, unroll)
+        fmi_amd.tune_set(Tune.BLOCK, block)
+        da, db = dev(a), dev(b)
+        fmi_amd.reduce_pair(Op.SUM, da, db)
+        assert_bit_equal(da.numpy(), a + b)
+    finally:
+        for k, v in old.items():
+            fmi_amd.tune_set(k, v)
+
+
+def test_combine_out_of_place(device):
+    a, b = inputs(np.int64, 5003, 0), inputs(np.int64, 5003, 1)
+    out = Bucket(5003, np.int64)
+    fmi_amd.combine(Op.MAX, out, dev(a), dev(b))
+    assert_bit_equal(out.numpy(), orc.op_max(a, b))
+
+
+def test_synthetic_matches_host_generator(device):
+    for dtype in DTYPES:
+        for peer in (0, 1, 7):
+            n = 100003
+            d = Bucket(n, dtype).fill_synthetic(42, peer)
+            assert_bit_equal(d.numpy(), orc.synthetic(dtype, n, seed=42, peer=peer), np.dtype(dtype).name)
+
+
+# ------------------------------------------------------------------------------------------------
+# P-way fused kernels vs the oracle's simulation of the reference collectives
+# ------------------------------------------------------------------------------------------------
+PEERS = list(range(1, 17)) + [17, 20, 33]
+
+
+def _peer_inputs(dtype, n, P, seed=7):
+    return [inputs(dtype, n, p, seed=seed) for p in range(P)]
+
+
+@pytest.mark.parametrize("P", PEERS)
+def test_allreduce_tree_all_ranks(device, P):
+    n = 1027
+    for dtype in DTYPES:
+        xs = _peer_inputs(dtype, n, P)
+        ins = [dev(x) for x in xs]
+        for op in OPS:
+            with np.errstate(all="ignore"):
+                want, _ = orc.allreduce(xs, orc.OPS[OPNAME[op]])
+            for rank in sorted({0, P // 2, P - 1}):
+                out = Bucket(n, dtype)
+                fmi_amd.reduce_tree(op, Alg.ALLREDUCE, out, ins, rank=rank)
+                assert_bit_equal(out.numpy(), want[rank], f"P={P} {op.name} {np.dtype(dtype).name} rank {rank}")
+
+
+@pytest.mark.parametrize("P", PEERS)
+def test_reduce_tree_roots(device, P):
+    n = 1029
+    for dtype in (np.float32, np.int64):
+        xs = _peer_inputs(dtype, n, P)
+        ins = [dev(x) for x in xs]
+        for op in OPS:
+            for root in sorted({0, 1 % P, P - 1}):
+                with np.errstate(all="ignore"):
+                    want, _ = orc.reduce(xs, orc.OPS[OPNAME[op]], root=root)
+                out = Bucket(n, dtype)
+                fmi_amd.reduce_tree(op, Alg.REDUCE, out, ins, rank=root)
+                assert_bit_equal(out.numpy(), want, f"P={P} {op.name} root {root}")
+
+
+@pytest.mark.parametrize("P", PEERS)
+def test_reduce_ltr(device, P):
+    n = 515
+    xs = _peer_inputs(np.float32, n, P)
+    ins = [dev(x) for x in xs]
+    for op in OPS:
+        with np.errstate(all="ignore"):
+            want, _ = orc.reduce(xs, orc.OPS[OPNAME[op]], root=0, commutative=False, associative=False)
+        out = Bucket(n, np.float32)
+        fmi_amd.reduce_tree(op, Alg.REDUCE_LTR, out, ins, rank=P - 1)
+        assert_bit_equal(out.numpy(), want, f"P={P} {op.name}")
+
+
+@pytest.mark.parametrize("P", PEERS)
+def test_scan_peers(device, P):
+    n = 1031
+    for dtype in DTYPES:
+        xs = _peer_inputs(dtype, n, P)
+        ins = [dev(x) for x in xs]
+        for op in OPS:
+            for alg, ordered in ((Alg.SCAN, False), (Alg.SCAN_LTR, True)):
+                with np.errstate(all="ignore"):
+                    want, _ = orc.scan(xs, orc.OPS[OPNAME[op]], commutative=not ordered, associative=not ordered)
+                outs = [Bucket(n, dtype) for _ in range(P)]
+                fmi_amd.scan_peers(op, alg, outs, ins)
+                for k in range(P):
+                    assert_bit_equal(outs[k].numpy(), want[k], f"P={P} {alg.name} {op.name} peer {k}")
+
+
+def test_scan_in_place(device):
+    P, n = 8, 4096
+    xs = _peer_inputs(np.float32, n, P)
+    bufs = [dev(x) for x in xs]
+    want, _ = orc.scan(xs, orc.op_sum)
+    fmi_amd.scan_peers(Op.SUM, Alg.SCAN, bufs, bufs)
+    for k in range(P):
+        assert_bit_equal(bufs[k].numpy(), want[k], f"peer {k}")
+
+
+def test_tree_unaligned_falls_back_with_same_order(device):
+    P, n = 5, 1000
+    xs = _peer_inputs(np.float32, n + 1, P)
+    big = [dev(x) for x in xs]
+    ins = [b.view(1, n) for b in big]
+    want, _ = orc.allreduce([x[1:] for x in xs], orc.op_sum)
+    out = Bucket(n, np.float32)
+    fmi_amd.reduce_tree(Op.SUM, Alg.ALLREDUCE, out, ins)
+    assert_bit_equal(out.numpy(), want[0])
+
+
+def test_signed_zero_max_follows_each_ranks_operand_order(device):
+    # Float max on ties depends on operand order; each rank's allreduce result must be its own.
+    P, n = 4, 64
+    xs = [np.full(n, (-0.0 if p % 2 else 0.0), dtype=np.float32) for p in range(P)]
+    ins = [dev(x) for x in xs]
+    want, _ = orc.allreduce(xs, orc.op_max)
+    for r in range(P):
+        out = Bucket(n, np.float32)
+        fmi_amd.reduce_tree(Op.MAX, Alg.ALLREDUCE, out, ins, rank=r)
+        assert_bit_equal(out.numpy(), want[r], f"rank {r}")
+
+
+def test_float_sum_tolerance_against_sequential_order(device):
+    """The stated float tolerance for orders that differ from the reference's (e.g. RCCL's):
+    |y - y_ref| <= (P-1) * u * sum|x_i|, u = 2^-24. Our tree result is exact;
+    a sequential fold stays inside the bound."""
+    P, n = 8, 1 << 16
+    xs = _peer_inputs(np.float32, n, P, seed=1234)
+    xs = [np.nan_to_num(x, nan=0.0, posinf=0.0, neginf=0.0) for x in xs]
+    xs = [np.where(np.abs(x) > 1e30, 0, x).astype(np.float32) for x in xs]
+    out = Bucket(n, np.float32)
+    fmi_amd.reduce_tree(Op.SUM, Alg.ALLREDUCE, out, [dev(x) for x in xs])
+    y = out.numpy()
+    seq = xs[0].copy()
+    for x in xs[1:]:
+        seq = seq + x
+    bound = (P - 1) * 2.0 ** -24 * np.sum(np.abs(np.stack(xs).astype(np.float64)), axis=0)
+    assert np.all(np.abs(y.astype(np.float64) - seq.astype(np.float64)) <= bound)
+
+
+# ------------------------------------------------------------------------------------------------
+# host-ingress pipeline (recv buffers in host memory)
+# ------------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("n", [1, 1000, (1 << 20) + 5])
+def test_host_reduce_pair(device, n):
+    old = fmi_amd.tune_get(Tune.HOST_CHUNK)
+    try:
+        fmi_amd.tune_set(Tune.HOST_CHUNK, 1 << 16)  # many chunks: exercises both pipeline slots
+        for dtype in (np.float32, np.int64):
+            a, b = inputs(dtype, n, 0), inputs(dtype, n, 1)
+            x = a.copy()
+            fmi_amd.host_reduce_pair(Op.SUM, x, b)
+            with np.errstate(all="ignore"):
+                assert_bit_equal(x, orc.pairwise("sum", a, b))
+    finally:
+        fmi_amd.tune_set(Tune.HOST_CHUNK, old)
+
+
+# ------------------------------------------------------------------------------------------------
+# BASELINE.json full-size configs
+# ------------------------------------------------------------------------------------------------
+def test_c2_256mib_f32_pairwise_sum(device):
+    n = (256 << 20) // 4
+    a = Bucket(n, np.float32).fill_synthetic(42, 0)
+    b = Bucket(n, np.float32).fill_synthetic(42, 1)
+    ha, hb = orc.synthetic(np.float32, n, 42, 0), orc.synthetic(np.float32, n, 42, 1)
+    fmi_amd.reduce_pair(Op.SUM, a, b)
+    assert_bit_equal(a.numpy(), ha + hb, "C2")
+
+
+def test_c3_64mib_i64_max(device):
+    n = (64 << 20) // 8
+    a = Bucket(n, np.int64).fill_synthetic(42, 0)
+    b = Bucket(n, np.int64).fill_synthetic(42, 1)
+    fmi_amd.reduce_pair(Op.MAX, a, b)
+    want = orc.op_max(orc.synthetic(np.int64, n, 42, 0), orc.synthetic(np.int64, n, 42, 1))
+    assert_bit_equal(a.numpy(), want, "C3 max")
+
+
+def test_c3_8peer_f32_scan_64mib(device):
+    P, n = 8, (64 << 20) // 4
+    ins = [Bucket(n, np.float32).fill_synthetic(42, p) for p in range(P)]
+    outs = [Bucket(n, np.float32) for _ in range(P)]
+    fmi_amd.scan_peers(Op.SUM, Alg.SCAN, outs, ins)
+    want, _ = orc.scan([orc.synthetic(np.float32, n, 42, p) for p in range(P)], orc.op_sum)
+    for k in range(P):
+        assert_bit_equal(outs[k].numpy(), want[k], f"C3 scan peer {k}")

@@ -1,0 +1,179 @@
+"""Pins the CPU oracle (oracle/fmi_oracle.py) before anything is checked against it:
+  * the reference's own known-answer tests (tests/golden/reference_kats.json),
+  * the evaluation order traced from the compiled reference (tests/golden/bracketing.json),
+  * the reference's side effects (sendbuf clobbering).
+CPU only."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import fmi_oracle as orc
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _fn(name):
+    i32 = np.int32
+    if name == "add":
+        return lambda a, b: (a + b).astype(i32)
+    if name == "mul":
+        return lambda a, b: (a * b).astype(i32)
+    if name == "sub":
+        return lambda a, b: (a - b).astype(i32)
+    if name == "vec_add_mul":  # tests/communicator.cpp:125-127
+        return lambda a, b: np.array([a[0] + b[0], a[1] * b[1]], dtype=i32)
+    if name == "vec_add_mul_max":  # tests/communicator.cpp:175-177 (std::max)
+        return lambda a, b: np.array([a[0] + b[0], a[1] * b[1], b[2] if a[2] < b[2] else a[2]], dtype=i32)
+    raise KeyError(name)
+
+
+def _inputs(kat):
+    P = kat["P"]
+    spec = kat["inputs"]
+    if spec == "r+1":
+        return [np.array([r + 1], dtype=np.int32) for r in range(P)]
+    if spec == "r":
+        return [np.array([r], dtype=np.int32) for r in range(P)]
+    return [np.array(v, dtype=np.int32) for v in spec]
+
+
+def _expected_all(kat):
+    P = kat["P"]
+    e = kat["expected_all"]
+    if e == "prefix_sum(r+1)":
+        return [[sum(range(1, r + 2))] for r in range(P)]
+    if e == "running_sub(r)":
+        return [[-sum(range(0, r + 1))] for r in range(P)]
+    if isinstance(e, str):
+        return [[int(e)]] * P
+    return e
+
+
+KATS = json.load(open(os.path.join(GOLDEN, "reference_kats.json")))["kats"]
+
+
+@pytest.mark.parametrize("kat", KATS, ids=[k["id"] for k in KATS])
+def test_oracle_matches_reference_kat(kat):
+    xs = _inputs(kat)
+    f = _fn(kat["fn"])
+    flags = dict(commutative=kat["commutative"], associative=kat["associative"])
+    with np.errstate(over="ignore"):
+        if kat["kind"] == "reduce":
+            res, _ = orc.reduce(xs, f, root=kat["root"], **flags)
+            assert res.tolist() == kat["expected_root"]
+        elif kat["kind"] == "allreduce":
+            res, _ = orc.allreduce(xs, f, **flags)
+            assert [r.tolist() for r in res] == _expected_all(kat)
+        else:
+            res, _ = orc.scan(xs, f, **flags)
+            assert [r.tolist() for r in res] == _expected_all(kat)
+
+
+BRACKETS = json.load(open(os.path.join(GOLDEN, "bracketing.json")))
+
+
+@pytest.mark.parametrize("P", sorted(int(p) for p in BRACKETS["allreduce_rank0"]))
+def test_oracle_bracketing_matches_reference_trace(P):
+    assert orc.expr("allreduce", P, rank=0) == BRACKETS["allreduce_rank0"][str(P)]
+    assert orc.expr("reduce", P, root=0) == BRACKETS["reduce_root0"][str(P)]
+    for r, e in BRACKETS["scan"].get(str(P), {}).items():
+        assert orc.expr("scan", P, rank=int(r)) == e
+    fold = "x0"
+    for p in range(1, P):
+        fold = f"({fold}+x{p})"
+    for r in range(P):
+        assert orc.expr("scan", P, rank=P - 1, ordered=True) == fold
+        assert orc.expr("allreduce", P, rank=r, ordered=True) == fold
+        assert orc.expr("reduce", P, root=r, ordered=True) == fold
+
+
+@pytest.mark.parametrize("P", [1, 2, 3, 4, 5, 6, 7, 8, 9, 13, 16, 17, 32])
+def test_allreduce_ranks_are_commutations_of_rank0(P):
+    # every rank's allreduce value is a commutation of rank 0's, so IEEE-commutative
+    # ops give bit-identical results on all ranks.
+    def canon(e):
+        if e.startswith("x"):
+            return e
+        depth, i = 0, 1
+        for i in range(1, len(e) - 1):
+            depth += e[i] == "("
+            depth -= e[i] == ")"
+            if depth == 0 and e[i] == "+":
+                break
+        left, right = canon(e[1:i]), canon(e[i + 1:-1])
+        return "(" + "+".join(sorted([left, right])) + ")"
+
+    exprs = [orc.expr("allreduce", P, rank=r) for r in range(P)]
+    assert len({canon(e) for e in exprs}) == 1
+
+
+def test_side_effects_match_reference():
+    # commutative allreduce/scan leave sendbuf = result; LTR allreduce leaves it.
+    xs = [np.array([r + 1.0], dtype=np.float32) for r in range(4)]
+    res, sends = orc.allreduce(xs, orc.op_sum)
+    assert all(np.array_equal(s, r) for s, r in zip(sends, res))
+    res, sends = orc.allreduce(xs, lambda a, b: a - b, commutative=False, associative=False)
+    assert all(np.array_equal(s, x) for s, x in zip(sends, xs))
+    res, sends = orc.scan(xs, orc.op_sum)
+    assert all(np.array_equal(s, r) for s, r in zip(sends, res))
+
+
+def test_p1_is_copy():
+    x = [np.arange(5, dtype=np.float32)]
+    assert np.array_equal(orc.allreduce(x, orc.op_sum)[0][0], x[0])
+    assert np.array_equal(orc.reduce(x, orc.op_sum)[0], x[0])
+    assert np.array_equal(orc.scan(x, orc.op_sum)[0][0], x[0])
+
+
+@pytest.mark.parametrize("P,root", [(4, 0), (5, 2), (8, 7), (13, 5)])
+def test_bcast_and_gather(P, root):
+    xs = [np.array([r * 10], dtype=np.int32) for r in range(P)]
+    out = orc.bcast(xs, root)
+    assert all(o.tolist() == [root * 10] for o in out)
+    g = orc.gather(xs, root)
+    assert [v.tolist() for v in g] == [[r * 10] for r in range(P)]
+
+
+def test_builtin_op_semantics_signed_zero_and_nan():
+    # std::max(a, b) = (a < b) ? b : a keeps a on ties and NaN; fmax would not.
+    a = np.array([0.0, -0.0, np.nan, 1.0], dtype=np.float32)
+    b = np.array([-0.0, 0.0, 1.0, np.nan], dtype=np.float32)
+    mx = orc.op_max(a, b)
+    mn = orc.op_min(a, b)
+    assert np.signbit(mx[0]) == False and np.signbit(mx[1]) == True  # noqa: E712
+    assert np.isnan(mx[2]) and mx[3] == 1.0
+    assert np.signbit(mn[0]) == False and np.signbit(mn[1]) == True  # noqa: E712
+    assert np.isnan(mn[2]) and mn[3] == 1.0
+
+
+def test_integer_ops_wrap():
+    a = np.array([np.iinfo(np.int32).max], dtype=np.int32)
+    b = np.array([1], dtype=np.int32)
+    assert orc.op_sum(a, b)[0] == np.iinfo(np.int32).min
+    a = np.array([np.iinfo(np.int64).max], dtype=np.int64)
+    assert orc.op_prod(a, np.array([2], dtype=np.int64))[0] == -2
+
+
+def test_synthetic_generator_properties():
+    f = orc.synthetic(np.float32, 1 << 16, seed=42, peer=0)
+    assert f.dtype == np.float32 and f.min() >= -1.0 and f.max() < 1.0
+    # values are k * 2^-23 - 1 exactly: the generator is exactly representable
+    k = (f.astype(np.float64) + 1.0) * 2.0 ** 23
+    assert np.array_equal(k, np.round(k))
+    assert not np.array_equal(f, orc.synthetic(np.float32, 1 << 16, seed=42, peer=1))
+    # counter-based: any window equals the same slice of a longer run
+    long = orc.synthetic(np.int64, 5000, seed=7, peer=3)
+    assert np.array_equal(long[1234:2234], orc.synthetic(np.int64, 1000, seed=7, peer=3, start=1234))
+    d = orc.synthetic(np.float64, 4096, seed=1234, peer=2)
+    assert d.min() >= -1.0 and d.max() < 1.0
+    i = orc.synthetic(np.int32, 4096, seed=42, peer=0)
+    assert i.dtype == np.int32 and i.min() < 0 < i.max()
+
+
+def test_splitmix64_known_values():
+    # splitmix64 published reference outputs for state 0 and 1234567 (first output of the generator
+    # whose state is incremented by the golden gamma before mixing, as here).
+    assert int(orc.splitmix64(np.array([0], dtype=np.uint64))[0]) == 0xE220A8397B1DCDAF
+    assert int(orc.splitmix64(np.array([1234567], dtype=np.uint64))[0]) == 6457827717110365317
