@@ -23,13 +23,20 @@ struct DeviceState {
     void* stage[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
     size_t stage_bytes = 0;
     hipStream_t pipe[2] = {nullptr, nullptr};
+    // scratch arena for the pairwise-pass execution of P-way programs; arena_free marks when the work
+    // that last used it has drained (the next user's stream waits on it)
+    void* arena = nullptr;
+    size_t arena_bytes = 0;
+    hipEvent_t arena_free = nullptr;
 };
 
 std::mutex g_mu;
 DeviceState g_state;  // one process drives one device (one process per GPU, as FMI runs one peer per process)
 
-std::atomic<long long> g_tune[5] = {0 /*variant: tiles*/, 4 /*unroll*/, 256 /*block*/, 8 /*grid per CU*/,
-                                    64ll << 20 /*host chunk*/};
+// Defaults from tools/tune_pair.py on MI355X (C2, 256 MiB f32): nontemporal one-shot tiles, 4 × 16 B per
+// operand per thread, 256-thread workgroups — 125 µs = 6.4 TB/s vs 142 µs for plain loads/stores.
+std::atomic<long long> g_tune[5] = {2 /*variant: nontemporal tiles*/, 4 /*unroll*/, 256 /*block*/,
+                                    8 /*grid per CU*/, 64ll << 20 /*host chunk*/};
 
 int hip_fail(const char* what, hipError_t e) {
     return fail(FMI_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
@@ -108,8 +115,9 @@ int launch_combine(int op, int dtype, void* out, const void* a, const void* b, s
 }
 
 // ----------------------------------------------------------------------------------------------------
-// P-way programs for P > 16 or unaligned buckets: the same schedule, one pairwise pass per step, temp
-// buckets recycled as soon as their value is dead (stream-ordered allocation).
+// P-way programs for P > 16 or unaligned buckets: the same schedule, one pairwise pass per step. Temp
+// buckets live in a library-owned arena; slots are assigned on the host (a value's slot is recycled
+// right after its last use) so the arena holds only the peak number of live temps.
 // ----------------------------------------------------------------------------------------------------
 int run_program_stepwise(int op, int dtype, const sched::HostProgram& prog, void* const* outs, int nouts,
                          const int* out_value, const void* const* ins, size_t n, hipStream_t s) {
@@ -122,40 +130,50 @@ int run_program_stepwise(int op, int dtype, const sched::HostProgram& prog, void
         last_use[prog.step[st].b] = st;
     }
     for (int k = 0; k < nouts; ++k) last_use[out_value[k]] = prog.nsteps;  // outputs live to the end
-    std::vector<void*> buf(nv, nullptr);
-    for (int p = 0; p < P; ++p) buf[p] = const_cast<void*>(ins[p]);
-    std::vector<void*> free_list, owned;
-    int rc = FMI_OK;
-    for (int st = 0; st < prog.nsteps && rc == FMI_OK; ++st) {
-        void* dst = nullptr;
-        if (!free_list.empty()) {
-            dst = free_list.back();
-            free_list.pop_back();
+    // host-side slot assignment
+    std::vector<int> slot(nv, -1), free_slots;
+    int nslots = 0;
+    for (int st = 0; st < prog.nsteps; ++st) {
+        int d;
+        if (!free_slots.empty()) {
+            d = free_slots.back();
+            free_slots.pop_back();
         } else {
-            const hipError_t e = hipMallocAsync(&dst, std::max<size_t>(n * esz, 16), s);
-            if (e != hipSuccess) {
-                rc = fail(FMI_ERR_ALLOC, std::string("hipMallocAsync (P-way scratch): ") + hipGetErrorString(e));
-                break;
-            }
-            owned.push_back(dst);
+            d = nslots++;
         }
-        const int v = P + st;
-        buf[v] = dst;
-        rc = launch_combine(op, dtype, dst, buf[prog.step[st].a], buf[prog.step[st].b], n, s);
-        for (int operand : {static_cast<int>(prog.step[st].a), static_cast<int>(prog.step[st].b)})
-            if (operand >= P && last_use[operand] == st && buf[operand]) {
-                free_list.push_back(buf[operand]);
-                buf[operand] = nullptr;
-            }
+        slot[P + st] = d;
+        const int a = prog.step[st].a, b = prog.step[st].b;
+        if (a >= P && last_use[a] == st) free_slots.push_back(slot[a]);
+        if (b >= P && b != a && last_use[b] == st) free_slots.push_back(slot[b]);
     }
+    const size_t stride = (std::max<size_t>(n * esz, 16) + 255) / 256 * 256;
+    const size_t need = stride * static_cast<size_t>(nslots);
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!g_state.arena_free) FMI_HIP_TRY(hipEventCreateWithFlags(&g_state.arena_free, hipEventDisableTiming));
+    if (g_state.arena_bytes < need) {
+        FMI_HIP_TRY(hipEventSynchronize(g_state.arena_free));  // previous users have drained
+        if (g_state.arena) FMI_HIP_TRY(hipFree(g_state.arena));
+        g_state.arena = nullptr;
+        g_state.arena_bytes = 0;
+        const hipError_t e = hipMalloc(&g_state.arena, need);
+        if (e != hipSuccess) return fail(FMI_ERR_ALLOC, std::string("hipMalloc (P-way scratch): ") + hipGetErrorString(e));
+        g_state.arena_bytes = need;
+    }
+    FMI_HIP_TRY(hipStreamWaitEvent(s, g_state.arena_free, 0));
+    auto addr = [&](int v) -> const void* {
+        return v < P ? ins[v] : static_cast<const char*>(g_state.arena) + stride * static_cast<size_t>(slot[v]);
+    };
+    int rc = FMI_OK;
+    for (int st = 0; st < prog.nsteps && rc == FMI_OK; ++st)
+        rc = launch_combine(op, dtype, const_cast<void*>(addr(P + st)), addr(prog.step[st].a), addr(prog.step[st].b), n, s);
     for (int k = 0; k < nouts && rc == FMI_OK; ++k) {
-        const void* src = buf[out_value[k]];
+        const void* src = addr(out_value[k]);
         if (src != outs[k] && n > 0) {
             const hipError_t e = hipMemcpyAsync(outs[k], src, n * esz, hipMemcpyDeviceToDevice, s);
             if (e != hipSuccess) rc = hip_fail("hipMemcpyAsync (P-way result)", e);
         }
     }
-    for (void* p : owned) (void)hipFreeAsync(p, s);
+    FMI_HIP_TRY(hipEventRecord(g_state.arena_free, s));
     return rc;
 }
 
@@ -231,6 +249,8 @@ int fmi_dev_finalize(void) {
             if (g_state.stage[k][j]) (void)hipFree(g_state.stage[k][j]);
         if (g_state.pipe[k]) (void)hipStreamDestroy(g_state.pipe[k]);
     }
+    if (g_state.arena) (void)hipFree(g_state.arena);
+    if (g_state.arena_free) (void)hipEventDestroy(g_state.arena_free);
     if (g_state.stream) (void)hipStreamDestroy(g_state.stream);
     g_state = DeviceState{};
     return FMI_OK;

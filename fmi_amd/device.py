@@ -52,7 +52,10 @@ NP_DTYPE = {DType.F32: np.float32, DType.F64: np.float64, DType.I32: np.int32, D
 
 
 def dtype_of(arr_or_dtype) -> DType:
-    dt = np.dtype(getattr(arr_or_dtype, "dtype", arr_or_dtype))
+    if isinstance(arr_or_dtype, np.ndarray):
+        dt = arr_or_dtype.dtype
+    else:
+        dt = np.dtype(arr_or_dtype)
     for k, v in NP_DTYPE.items():
         if np.dtype(v) == dt:
             return k

@@ -94,7 +94,8 @@ def test_reduce_pair_inplace_alias(device):
     a = inputs(np.float32, 10007, 0)
     da = dev(a)
     fmi_amd.reduce_pair(Op.SUM, da, da)
-    assert_bit_equal(da.numpy(), a + a)
+    with np.errstate(all="ignore"):
+        assert_bit_equal(da.numpy(), a + a)
 
 
 @pytest.mark.parametrize("variant,unroll,block", [(v, u, b) for v in (0, 1, 2) for u in (1, 2, 4, 8)
