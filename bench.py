@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--path", default="tree", choices=["tree", "rccl"],
                     help="N>1 exchange: tree = all-to-all + fused kernel (bit-exact), rccl = reduce-scatter")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="run the N>1 code path (RCCL exchange) even at world size 1 — plumbing check only")
     ap.add_argument("--cpu-reps", type=int, default=7)
     return ap.parse_args()
 
@@ -114,7 +116,8 @@ def main():
     import numpy as np
 
     dist = None
-    if world > 1:
+    use_dist = world > 1 or args.force_dist
+    if use_dist:
         # torch first: libfmi_dev.so then binds to the HIP runtime torch already loaded (one runtime
         # per process, shared streams/pointers with RCCL) — see DESIGN.md §Runtime.
         import torch
@@ -130,7 +133,7 @@ def main():
     n = args.bucket_mib * MIB // 4
     nbytes = n * 4
 
-    if world == 1:
+    if not use_dist:
         sets = [(Bucket(n, np.float32).fill_synthetic(42 + s, 0), Bucket(n, np.float32).fill_synthetic(42 + s, 1))
                 for s in range(args.sets)]
         fmi_amd.sync()
@@ -162,9 +165,9 @@ def main():
     else:
         from fmi_amd.collectives import ShardedAllreduce
 
-        ar = ShardedAllreduce(dist.group.WORLD, path=args.path)
+        ar = ShardedAllreduce(dist.group.WORLD, path=args.path, force_exchange=args.force_dist)
         step_ms, kernel_ms, extra = ar.bench(n, steps=args.steps, warmup=args.warmup, sets=args.sets)
-        dominant = "tree_kernel" if args.path == "tree" else "pair_tile"
+        dominant = "pair_tile"  # our local round; the exchange itself is RCCL's (config.algbw/busbw)
         algo_bytes = extra.pop("kernel_algo_bytes")
         workload = (f"C4-shaped: {2 * world}-peer float32 sum-allreduce of 256 MiB buckets, 2 peers per GPU, "
                     f"sharded over {world} GPUs")
@@ -197,7 +200,7 @@ def main():
                      "traffic_source": traffic_src},
     }
     line["config"].update(extra)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and not use_dist and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args)
     if rank == 0:
         print(json.dumps(line), flush=True)

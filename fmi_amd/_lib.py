@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import sys
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -80,6 +81,9 @@ SIGNATURES = {
 
 _lock = threading.Lock()
 _lib = None
+# Whether torch (and with it torch's bundled HIP runtime) was already loaded when libfmi_dev.so was: only
+# then do torch, RCCL and our kernels share one runtime (see fmi_amd/collectives.py).
+TORCH_LOADED_FIRST = False
 
 
 def load() -> ctypes.CDLL:
@@ -92,6 +96,8 @@ def load() -> ctypes.CDLL:
             raise FileNotFoundError(
                 f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
                 "or `make -C fmi_amd/csrc`. There is no CPU fallback for the device path.")
+        global TORCH_LOADED_FIRST
+        TORCH_LOADED_FIRST = "torch" in sys.modules
         lib = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(lib, name)

@@ -1,0 +1,207 @@
+"""Multi-GPU sharded bucket allreduce: one process per GPU, torch.distributed over RCCL/xGMI.
+
+FMI's allreduce (reference src/comm/PeerToPeer.cpp:96-130) is recursive doubling over peers that talk
+through host sockets. On one MI355X node the peers' buckets sit in HBM of different GPUs, so the
+exchange runs over xGMI instead, sharded so that all 7 links of every GPU carry traffic at once:
+
+  local rounds   every GPU first folds the peers it hosts with the pairwise kernel (with two peers per
+                 GPU this IS round 0 of recursive doubling: pairs (2g, 2g+1));
+  path "tree"    (default, bit-exact) all-to-all of bucket shards → GPU k holds shard k of every GPU's
+                 partial → ONE pass of the fused P-way kernel in allreduce_no_order order over the N
+                 partials → all-gather of the reduced shards. For N a power of two this evaluates exactly
+                 the reference's 2N-peer recursive-doubling bracketing, so every GPU ends with the
+                 reference's bits (SURVEY.md §8e "Path B").
+  path "rccl"    RCCL reduce-scatter + all-gather (SURVEY.md §8e "Path A"): same traffic, RCCL's own
+                 reduction order, float results within (P-1)·u·Σ|x| of the reference.
+
+No collective is invented: the all-to-all / reduce-scatter IS the exchange step of the reference's
+allreduce, re-cut into shards.
+
+Runtime note: torch wheels bundle their own HIP runtime. libfmi_dev.so binds to whichever
+libamdhip64.so.7 is loaded first, so torch must be imported before the library is loaded (this module
+imports torch at import time and refuses to run if the library was loaded before torch) — then torch,
+RCCL and our kernels share one runtime, one set of streams and one address space.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from . import _lib  # noqa: E402
+from .device import Alg, DType, Op  # noqa: E402
+
+_TORCH_DTYPE = {torch.float32: DType.F32, torch.float64: DType.F64, torch.int32: DType.I32, torch.int64: DType.I64}
+_REDUCE_OP = {Op.SUM: dist.ReduceOp.SUM, Op.PROD: dist.ReduceOp.PRODUCT, Op.MAX: dist.ReduceOp.MAX,
+              Op.MIN: dist.ReduceOp.MIN}
+SHARD_ALIGN = 64  # elements: keeps every shard 256-B aligned for the 16-B vector kernels
+
+
+def _dtype(t: torch.Tensor) -> DType:
+    try:
+        return _TORCH_DTYPE[t.dtype]
+    except KeyError:
+        raise TypeError(f"unsupported bucket dtype {t.dtype}") from None
+
+
+class HipEngine:
+    """Product engine: combines run as libfmi_dev.so kernels on torch CUDA tensors, on torch's current
+    stream (so they order with RCCL collectives exactly like torch's own ops)."""
+
+    def __init__(self, device_index: int):
+        if _lib._lib is not None and not _lib.TORCH_LOADED_FIRST:
+            raise RuntimeError("libfmi_dev.so was loaded before torch: two HIP runtimes would coexist; import "
+                               "fmi_amd.collectives (or torch) before using fmi_amd")
+        _lib.load()
+        _lib.call("fmi_dev_init", device_index)
+        self.device = torch.device("cuda", device_index)
+
+    @staticmethod
+    def _stream() -> int:
+        return torch.cuda.current_stream().cuda_stream
+
+    def reduce_pair(self, op: Op, inout: torch.Tensor, src: torch.Tensor) -> None:
+        assert inout.is_contiguous() and src.is_contiguous() and inout.numel() == src.numel()
+        _lib.call("fmi_dev_reduce_pair", int(op), int(_dtype(inout)), inout.data_ptr(), src.data_ptr(),
+                  inout.numel(), self._stream())
+
+    def reduce_tree(self, op: Op, alg: Alg, out: torch.Tensor, ins: Sequence[torch.Tensor], rank: int = 0) -> None:
+        import ctypes
+        ptrs = (ctypes.c_void_p * len(ins))(*[t.data_ptr() for t in ins])
+        _lib.call("fmi_dev_reduce_tree", int(op), int(_dtype(out)), int(alg), out.data_ptr(), ptrs, len(ins), rank,
+                  out.numel(), self._stream())
+
+    def fill_synthetic(self, t: torch.Tensor, seed: int, peer: int) -> None:
+        _lib.call("fmi_dev_fill_synthetic", int(_dtype(t)), t.data_ptr(), t.numel(), seed, peer, self._stream())
+
+
+class ShardedAllreduce:
+    """Allreduce of the buckets of all peers hosted by the GPUs of `group` (one process per GPU).
+
+    `allreduce(op, buckets, out)`: `buckets` are the peer buckets hosted by this GPU (peers
+    local_peers·rank … in order); every GPU's `out` receives the full reduced bucket. As in the reference
+    (src/comm/PeerToPeer.cpp:103,119) the first local bucket is overwritten with the partial result.
+    """
+
+    def __init__(self, group=None, path: str = "tree", engine=None, force_exchange: bool = False):
+        if path not in ("tree", "rccl"):
+            raise ValueError("path must be 'tree' or 'rccl'")
+        self.group = group if group is not None else dist.group.WORLD
+        self.world = dist.get_world_size(self.group)
+        self.rank = dist.get_rank(self.group)
+        self.path = path
+        self.force_exchange = force_exchange  # run the exchange even on one GPU (plumbing checks)
+        if engine is None:
+            engine = HipEngine(torch.cuda.current_device())
+        self.engine = engine
+        self._bufs = {}
+
+    def _buf(self, key, numel, like: torch.Tensor) -> torch.Tensor:
+        b = self._bufs.get(key)
+        if b is None or b.numel() != numel or b.dtype != like.dtype or b.device != like.device:
+            b = torch.empty(numel, dtype=like.dtype, device=like.device)
+            self._bufs[key] = b
+        return b
+
+    def shard_elems(self, n: int) -> int:
+        per = -(-n // self.world)
+        return -(-per // SHARD_ALIGN) * SHARD_ALIGN
+
+    def allreduce(self, op: Op, buckets: List[torch.Tensor], out: torch.Tensor) -> torch.Tensor:
+        if not buckets:
+            raise ValueError("need at least one local peer bucket")
+        x = buckets[0]
+        n = x.numel()
+        for b in buckets:
+            if b.numel() != n or b.dtype != x.dtype:
+                raise RuntimeError("Dimensions of send and receive data must match")
+        if out.numel() != n:
+            raise RuntimeError("Dimensions of send and receive data must match")
+        for b in buckets[1:]:  # local rounds of recursive doubling
+            self.engine.reduce_pair(op, x, b)
+        N = self.world
+        if N == 1 and not self.force_exchange:
+            out.copy_(x)
+            return out
+        shard = self.shard_elems(n)
+        padded = shard * N
+        if padded != n:
+            src = self._buf("pad_in", padded, x)
+            src[:n].copy_(x)
+            src[n:].zero_()
+        else:
+            src = x
+        red = self._buf("shard", shard, x)
+        if self.path == "tree":
+            staging = self._buf("staging", padded, x)
+            dist.all_to_all_single(staging, src, group=self.group)
+            parts = [staging[j * shard:(j + 1) * shard] for j in range(N)]
+            self.engine.reduce_tree(op, Alg.ALLREDUCE, red, parts, rank=0)
+        else:
+            dist.reduce_scatter_tensor(red, src, op=_REDUCE_OP[op], group=self.group)
+        gathered = out if padded == n else self._buf("pad_out", padded, x)
+        dist.all_gather_into_tensor(gathered, red, group=self.group)
+        if gathered is not out:
+            out.copy_(gathered[:n])
+        return out
+
+    # ------------------------------------------------------------------------------------------------
+    def bench(self, n: int, steps: int, warmup: int, sets: int = 2, peers_per_gpu: int = 2):
+        """Timed loop for bench.py: returns (ms_per_step max over ranks, per-step local-kernel ms, extras).
+
+        Exactly `steps` steps are timed, bracketed by barrier + device sync on both sides; the step time
+        is the max over ranks. The local pairwise kernel is also timed on the stream it runs on.
+        """
+        import time
+
+        dev = self.engine.device
+        on_gpu = dev.type == "cuda"
+
+        def sync():
+            if on_gpu:
+                torch.cuda.synchronize()
+
+        bufs = []
+        for s in range(sets):
+            pair = [torch.empty(n, dtype=torch.float32, device=dev) for _ in range(peers_per_gpu)]
+            for j, t in enumerate(pair):
+                self.engine.fill_synthetic(t, 42 + s, peers_per_gpu * self.rank + j)
+            bufs.append(pair)
+        out = torch.empty(n, dtype=torch.float32, device=dev)
+        for k in range(warmup):
+            self.allreduce(Op.SUM, bufs[k % sets], out)
+        if on_gpu:
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        local_ms = []
+        dist.barrier(group=self.group)
+        sync()
+        t0 = time.perf_counter()
+        for k in range(steps):
+            pair = bufs[k % sets]
+            if on_gpu:
+                ev[k][0].record()
+            else:
+                tl = time.perf_counter()
+            for b in pair[1:]:
+                self.engine.reduce_pair(Op.SUM, pair[0], b)
+            if on_gpu:
+                ev[k][1].record()
+            else:
+                local_ms.append((time.perf_counter() - tl) * 1e3)
+            self.allreduce(Op.SUM, [pair[0]], out)
+        sync()
+        dist.barrier(group=self.group)
+        t1 = time.perf_counter()
+        local = torch.tensor([(t1 - t0) * 1e3 / steps], dtype=torch.float64, device=dev)
+        dist.all_reduce(local, op=dist.ReduceOp.MAX, group=self.group)
+        step_ms = float(local.item())
+        kernel_ms = [a.elapsed_time(b) for a, b in ev] if on_gpu else local_ms
+        extra = {
+            "kernel_algo_bytes": 3 * n * 4,
+            "exchange": self.path,
+            "shard_elems": self.shard_elems(n),
+            "algbw_GiB_s": round((n * 4 / 2 ** 30) / (step_ms * 1e-3), 2),
+            "busbw_GiB_s": round((n * 4 / 2 ** 30) / (step_ms * 1e-3) * 2 * (self.world - 1) / self.world, 2),
+        }
+        return step_ms, kernel_ms, extra

@@ -1,0 +1,107 @@
+"""Multi-process tests (torch.distributed gloo on CPU, world size 2 and 4) of the sharded allreduce in
+fmi_amd/collectives.py — the N>1 path bench.py runs over RCCL on MI355X nodes.
+
+Checks: with two peers per process and N a power of two, path "tree" reproduces the reference's
+2N-peer recursive-doubling allreduce bit for bit on every rank (including ragged sizes that need shard
+padding); path "rccl" (reduce-scatter) stays within the stated float tolerance; integer ops are exact
+on both paths; the first local bucket is clobbered like the reference's sendbuf.
+"""
+import os
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+import torch.multiprocessing as mp  # noqa: E402
+
+from oracle import fmi_oracle as orc  # noqa: E402
+from tests import _dist_worker  # noqa: E402
+
+OPS = {0: "sum", 1: "prod", 2: "max", 3: "min"}
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(world, n, dtype, op, path, peers_per_gpu=2):
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_dist_worker.run, args=(world, _free_port(), n, dtype, op, path, peers_per_gpu, d), nprocs=world,
+                 join=True)
+        outs = [np.load(os.path.join(d, f"out{r}.npy")) for r in range(world)]
+        sends = [np.load(os.path.join(d, f"send{r}.npy")) for r in range(world)]
+    xs = [orc.synthetic(np.dtype(dtype), n, 42, p) for p in range(peers_per_gpu * world)]
+    return outs, sends, xs
+
+
+def _bits_equal(a, b):
+    u = {4: np.uint32, 8: np.uint64}[a.dtype.itemsize]
+    return np.array_equal(a.view(u), b.view(u))
+
+
+@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("n", [4096, 1000003])
+def test_tree_path_bit_exact_vs_reference_allreduce(world, n):
+    outs, sends, xs = _run(world, n, "float32", 0, "tree")
+    want, _ = orc.allreduce(xs, orc.op_sum)
+    for r in range(world):
+        # GPU r hosts peers 2r, 2r+1 and ends with the value peer 2r holds in the reference
+        assert _bits_equal(outs[r], want[2 * r]), f"rank {r}"
+        # sendbuf clobbered with the local partial (reference PeerToPeer.cpp:103,119)
+        assert _bits_equal(sends[r], xs[2 * r] + xs[2 * r + 1])
+
+
+@pytest.mark.parametrize("op", [1, 2, 3])
+def test_tree_path_other_ops_int64(op):
+    with np.errstate(over="ignore"):
+        outs, _, xs = _run(2, 2053, "int64", op, "tree")
+        want, _ = orc.allreduce(xs, orc.OPS[OPS[op]])
+    for r in range(2):
+        assert np.array_equal(outs[r], want[2 * r])
+
+
+def test_rccl_path_within_tolerance():
+    world, n = 4, 65536 + 7
+    outs, _, xs = _run(world, n, "float32", 0, "rccl")
+    want, _ = orc.allreduce(xs, orc.op_sum)
+    P = len(xs)
+    bound = (P - 1) * 2.0 ** -24 * np.sum(np.abs(np.stack(xs).astype(np.float64)), axis=0)
+    for r in range(world):
+        err = np.abs(outs[r].astype(np.float64) - want[0].astype(np.float64))
+        assert np.all(err <= bound), f"rank {r}: max err {err.max()}"
+    assert all(_bits_equal(outs[0], o) for o in outs[1:])  # every rank gets the same bits
+
+
+def test_rccl_path_exact_for_integers():
+    outs, _, xs = _run(2, 4099, "int64", 2, "rccl")
+    want, _ = orc.allreduce(xs, orc.op_max)
+    for r in range(2):
+        assert np.array_equal(outs[r], want[0])
+
+
+def test_single_peer_per_gpu():
+    world, n = 2, 1031
+    outs, sends, xs = _run(world, n, "float32", 0, "tree", peers_per_gpu=1)
+    want, _ = orc.allreduce(xs, orc.op_sum)
+    for r in range(world):
+        assert _bits_equal(outs[r], want[r])
+
+
+@pytest.mark.parametrize("path", ["tree", "rccl"])
+def test_bench_loop_runs_multi_process(path):
+    import json
+
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_dist_worker.run_bench, args=(world, _free_port(), 8192, path, d), nprocs=world, join=True)
+        res = [json.load(open(os.path.join(d, f"bench{r}.json"))) for r in range(world)]
+    # step time is the max over ranks: identical on every rank
+    assert res[0]["step_ms"] == res[1]["step_ms"] > 0
+    assert len(res[0]["kernel_ms"]) == 3
+    assert res[0]["extra"]["exchange"] == path and res[0]["extra"]["kernel_algo_bytes"] == 3 * 8192 * 4
