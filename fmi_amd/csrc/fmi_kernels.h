@@ -187,6 +187,10 @@ __global__ void __launch_bounds__(256) pair_scalar(T* out, const T* a, const T* 
 // registers. Indices into the value array are template constants (fold over index_sequence), so the
 // array is promoted to VGPRs — no scratch.
 // ---------------------------------------------------------------------------------------------------
+// Peer buckets are streamed exactly once per launch: nontemporal loads/stores (global_* nt) keep them
+// from displacing other data in L2/MALL, as for the pairwise kernel (tools/tune_pair.py: +13%).
+inline constexpr bool kFusedNT = true;
+
 struct PeerPtrs {
     const void* in[sched::kMaxFusedPeers];
     void* out[sched::kMaxFusedPeers];
@@ -211,7 +215,7 @@ __device__ __forceinline__ void run_steps(Lanes<T, W>* v, std::index_sequence<S.
 template <class T, int W, int P, size_t... I>
 __device__ __forceinline__ void load_peers(Lanes<T, W>* v, const PeerPtrs& ptrs, size_t elem,
                                            std::index_sequence<I...>) {
-    ((v[I] = load_lanes<false, T, W>(static_cast<const T*>(ptrs.in[I]) + elem)), ...);
+    ((v[I] = load_lanes<kFusedNT, T, W>(static_cast<const T*>(ptrs.in[I]) + elem)), ...);
 }
 
 template <class T, int W, int ALG, int P, size_t... R>
@@ -224,7 +228,7 @@ __device__ __forceinline__ Lanes<T, W> pick_rank(const Lanes<T, W>* v, int rank,
 template <class T, int W, int ALG, int P, size_t... R>
 __device__ __forceinline__ void store_all(const Lanes<T, W>* v, const PeerPtrs& ptrs, size_t elem,
                                           std::index_sequence<R...>) {
-    ((store_lanes<false, T, W>(static_cast<T*>(ptrs.out[R]) + elem, v[kOut<ALG, P, R>])), ...);
+    ((store_lanes<kFusedNT, T, W>(static_cast<T*>(ptrs.out[R]) + elem, v[kOut<ALG, P, R>])), ...);
 }
 
 // ALL_RANKS: honour `rank` (output = the value peer `rank` holds). Needed only where operand order can
@@ -239,7 +243,7 @@ __device__ __forceinline__ void tree_group(const PeerPtrs& ptrs, int rank, size_
         r = pick_rank<T, W, ALG, P>(v, rank, std::make_index_sequence<P>{});
     else
         r = v[kOut<ALG, P, 0>];
-    store_lanes<false, T, W>(static_cast<T*>(ptrs.out[0]) + elem, r);
+    store_lanes<kFusedNT, T, W>(static_cast<T*>(ptrs.out[0]) + elem, r);
 }
 
 template <class Op, class T, int ALG, int P, bool ALL_RANKS>

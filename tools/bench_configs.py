@@ -1,0 +1,139 @@
+"""Per-config measurements for DESIGN.md (BASELINE.json configs C2, C3, C5-shaped; tree and scan kernels).
+
+Each row: kernel time from HIP events on the launching stream (median over iterations, rotating buffer
+sets so the working set exceeds the 256 MiB Infinity Cache where the config allows), algorithmic HBM
+bytes per launch, GB/s and fraction of the 8 TB/s peak. Host-inclusive rows time fmi_host_reduce_pair
+on pinned and on pageable host buffers (PCIe-bound). Prints one JSON object per row.
+"""
+import argparse
+import ctypes
+import json
+import os
+import statistics
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import numpy as np  # noqa: E402
+
+import fmi_amd  # noqa: E402
+from fmi_amd import Alg, Bucket, Event, Op, _lib  # noqa: E402
+
+PEAK = 8000.0
+MIB = 1 << 20
+
+
+def timed(fn, iters, rotate):
+    ev = [(Event(), Event()) for _ in range(iters)]
+    for k in range(3):
+        fn(k % rotate)
+    fmi_amd.sync()
+    for k in range(iters):
+        ev[k][0].record()
+        fn(k % rotate)
+        ev[k][1].record()
+    fmi_amd.sync()
+    ms = [a.elapsed_ms(b) for a, b in ev]
+    return statistics.median(ms), min(ms)
+
+
+def row(name, algo_bytes, med_ms, min_ms, **kw):
+    gbs = algo_bytes / (med_ms * 1e-3) / 1e9
+    r = dict(config=name, algo_bytes=algo_bytes, median_us=round(med_ms * 1e3, 2), min_us=round(min_ms * 1e3, 2),
+             gb_s=round(gbs, 1), frac_of_peak=round(gbs / PEAK, 4))
+    r.update(kw)
+    print(json.dumps(r), flush=True)
+
+
+def pinned(n, dtype):
+    p = ctypes.c_void_p()
+    nbytes = n * np.dtype(dtype).itemsize
+    _lib.call("fmi_host_pin_alloc", ctypes.byref(p), nbytes)
+    buf = (ctypes.c_char * nbytes).from_address(p.value)
+    return np.frombuffer(buf, dtype=dtype, count=n), p.value
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=30)
+    ap.add_argument("--quick", action="store_true")
+    args = ap.parse_args()
+    fmi_amd.init(0)
+    it = args.iters
+
+    # C2 and its siblings: pairwise combine, every dtype/op, 256 MiB buckets, 4 rotating sets
+    for dt in (np.float32, np.float64, np.int32, np.int64):
+        n = 256 * MIB // np.dtype(dt).itemsize
+        sets = [(Bucket(n, dt).fill_synthetic(42 + s, 0), Bucket(n, dt).fill_synthetic(42 + s, 1)) for s in range(4)]
+        for op in (Op.SUM, Op.MAX) if not args.quick else (Op.SUM,):
+            med, mn = timed(lambda k: fmi_amd.reduce_pair(op, *sets[k]), it, 4)
+            row(f"pair {op.name.lower()} {np.dtype(dt).name} 256MiB", 3 * 256 * MIB, med, mn)
+        del sets
+
+    # C3a: int64 max, 64 MiB buckets; 8 rotating sets = 1.5 GiB working set (defeats the MALL)
+    n = 64 * MIB // 8
+    sets = [(Bucket(n, np.int64).fill_synthetic(42 + s, 0), Bucket(n, np.int64).fill_synthetic(42 + s, 1))
+            for s in range(8)]
+    med, mn = timed(lambda k: fmi_amd.reduce_pair(Op.MAX, *sets[k]), it, 8)
+    row("C3 pair max int64 64MiB (8 rotating sets)", 3 * 64 * MIB, med, mn)
+    med, mn = timed(lambda k: fmi_amd.reduce_pair(Op.MAX, *sets[0]), it, 1)
+    row("C3 pair max int64 64MiB (same set, MALL-resident)", 3 * 64 * MIB, med, mn, note="Infinity-Cache hits")
+    del sets
+
+    # C3b: peer-axis scan, P = 8 buckets of 64 MiB f32 → 8 outputs (2 rotating input sets = 1 GiB each)
+    P, n = 8, 64 * MIB // 4
+    ins = [[Bucket(n, np.float32).fill_synthetic(42 + s, p) for p in range(P)] for s in range(2)]
+    outs = [Bucket(n, np.float32) for _ in range(P)]
+    for alg in (Alg.SCAN, Alg.SCAN_LTR):
+        med, mn = timed(lambda k: fmi_amd.scan_peers(Op.SUM, alg, outs, ins[k]), it, 2)
+        row(f"C3 scan {alg.name.lower()} f32 P=8 x 64MiB", 2 * P * 64 * MIB, med, mn)
+    # P-way tree reductions over the same buckets (one pass: P reads + 1 write)
+    out = Bucket(n, np.float32)
+    for alg in (Alg.ALLREDUCE, Alg.REDUCE, Alg.REDUCE_LTR):
+        med, mn = timed(lambda k: fmi_amd.reduce_tree(Op.SUM, alg, out, ins[k]), it, 2)
+        row(f"tree {alg.name.lower()} f32 P=8 x 64MiB", (P + 1) * 64 * MIB, med, mn)
+    for P2 in (2, 4, 16):
+        n2 = 1024 * MIB // 4 // P2
+        ins2 = [Bucket(n2, np.float32).fill_synthetic(7, p) for p in range(P2)]
+        out2 = Bucket(n2, np.float32)
+        med, mn = timed(lambda k: fmi_amd.reduce_tree(Op.SUM, Alg.ALLREDUCE, out2, ins2), max(5, it // 2), 1)
+        row(f"tree allreduce f32 P={P2} x {1024 // P2}MiB", (P2 + 1) * n2 * 4, med, mn)
+        del ins2, out2
+    del ins, outs, out
+
+    # host-inclusive (C5-shaped, one GPU): pinned and pageable 256 MiB f32 pairs through the device
+    n = 256 * MIB // 4
+    ha, pa = pinned(n, np.float32)
+    hb, pb = pinned(n, np.float32)
+    ha[:] = 1.0
+    hb[:] = 2.0
+    for chunk in (16, 64):
+        fmi_amd.tune_set(fmi_amd.Tune.HOST_CHUNK, chunk * MIB)
+        fmi_amd.host_reduce_pair(Op.SUM, ha, hb)
+        ts = []
+        for _ in range(5):
+            t0 = time.perf_counter()
+            fmi_amd.host_reduce_pair(Op.SUM, ha, hb)
+            ts.append(time.perf_counter() - t0)
+        med = statistics.median(ts)
+        print(json.dumps(dict(config=f"host pinned pair sum f32 256MiB chunk {chunk}MiB", median_ms=round(med * 1e3, 3),
+                              bucket_gib_s=round(256 / 1024 / med, 3),
+                              pcie_gb_s=round(3 * 256 * MIB / med / 1e9, 2))), flush=True)
+    _lib.call("fmi_host_pin_free", pa)
+    _lib.call("fmi_host_pin_free", pb)
+    a = np.ones(n, np.float32)
+    b = np.full(n, 2.0, np.float32)
+    fmi_amd.tune_set(fmi_amd.Tune.HOST_CHUNK, 64 * MIB)
+    ts = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        fmi_amd.host_reduce_pair(Op.SUM, a, b)
+        ts.append(time.perf_counter() - t0)
+    med = statistics.median(ts)
+    print(json.dumps(dict(config="host pageable pair sum f32 256MiB", median_ms=round(med * 1e3, 3),
+                          bucket_gib_s=round(256 / 1024 / med, 3))), flush=True)
+
+
+if __name__ == "__main__":
+    main()
