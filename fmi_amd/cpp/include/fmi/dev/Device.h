@@ -1,0 +1,162 @@
+// FMI::Dev — C++ RAII layer over the C-ABI in include/fmi_dev.h (libfmi_dev.so, gfx950).
+//
+// Error convention: every C-ABI status != 0 becomes a std::runtime_error carrying
+// fmi_last_error(), the exception type the reference itself throws for usage errors
+// (reference include/Communicator.h:90,114,138).
+#ifndef FMI_AMD_DEV_DEVICE_H
+#define FMI_AMD_DEV_DEVICE_H
+
+#include <algorithm>
+#include <cstddef>
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <type_traits>
+#include <utility>
+#include <vector>
+
+#include "fmi_dev.h"  // C-ABI: add -I<repo>/include
+
+namespace FMI::Dev {
+
+inline void check(int status, const char* what) {
+    if (status != FMI_OK) throw std::runtime_error(std::string(what) + ": " + fmi_last_error());
+}
+
+template <class A>
+constexpr int dtype_of() {
+    if constexpr (std::is_same_v<A, float>) return FMI_F32;
+    else if constexpr (std::is_same_v<A, double>) return FMI_F64;
+    else if constexpr (std::is_same_v<A, int32_t>) return FMI_I32;
+    else if constexpr (std::is_same_v<A, int64_t>) return FMI_I64;
+    else return -1;
+}
+
+template <class A>
+constexpr bool device_type = dtype_of<A>() >= 0;
+
+// Select the device for this process (one process per GPU, as FMI runs one peer per process).
+inline void init(int device = 0) { check(fmi_dev_init(device), "fmi_dev_init"); }
+
+inline bool available() {
+    int n = 0;
+    return fmi_dev_count(&n) == FMI_OK && n > 0;
+}
+
+inline void sync() { check(fmi_dev_sync(), "fmi_dev_sync"); }
+
+// A device-resident bucket of n elements of A (owning, move-only).
+template <class A>
+class Bucket {
+    static_assert(device_type<A>, "device buckets hold float, double, int32_t or int64_t");
+
+public:
+    using value_type = A;
+    Bucket() = default;
+    explicit Bucket(std::size_t n) : n_(n) {
+        void* p = nullptr;
+        check(fmi_dev_alloc(&p, n * sizeof(A)), "fmi_dev_alloc");
+        ptr_ = static_cast<A*>(p);
+    }
+    explicit Bucket(const std::vector<A>& host) : Bucket(host.size()) { upload(host); }
+    Bucket(const Bucket&) = delete;
+    Bucket& operator=(const Bucket&) = delete;
+    Bucket(Bucket&& o) noexcept : ptr_(std::exchange(o.ptr_, nullptr)), n_(std::exchange(o.n_, 0)) {}
+    Bucket& operator=(Bucket&& o) noexcept {
+        if (this != &o) {
+            release();
+            ptr_ = std::exchange(o.ptr_, nullptr);
+            n_ = std::exchange(o.n_, 0);
+        }
+        return *this;
+    }
+    ~Bucket() { release(); }
+
+    A* data() const { return ptr_; }
+    std::size_t size() const { return n_; }
+    std::size_t size_in_bytes() const { return n_ * sizeof(A); }
+
+    void upload(const std::vector<A>& host) {
+        if (host.size() != n_) throw std::runtime_error("Bucket::upload: size mismatch");
+        check(fmi_dev_h2d_async(ptr_, host.data(), size_in_bytes(), nullptr), "fmi_dev_h2d_async");
+        check(fmi_stream_sync(nullptr), "fmi_stream_sync");
+    }
+    std::vector<A> download() const {
+        std::vector<A> host(n_);
+        check(fmi_dev_d2h_async(host.data(), ptr_, size_in_bytes(), nullptr), "fmi_dev_d2h_async");
+        check(fmi_stream_sync(nullptr), "fmi_stream_sync");
+        return host;
+    }
+    void fill_synthetic(uint64_t seed, uint32_t peer) {
+        check(fmi_dev_fill_synthetic(dtype_of<A>(), ptr_, n_, seed, peer, nullptr), "fmi_dev_fill_synthetic");
+    }
+
+private:
+    void release() noexcept {
+        if (ptr_) (void)fmi_dev_free(ptr_);
+        ptr_ = nullptr;
+        n_ = 0;
+    }
+    A* ptr_ = nullptr;
+    std::size_t n_ = 0;
+};
+
+// Untyped device scratch used by the channel algorithms for temporaries of device-resident buckets.
+class Scratch {
+public:
+    Scratch() = default;
+    Scratch(std::size_t bytes, bool on_device) : bytes_(bytes), device_(on_device) {
+        if (device_) {
+            void* p = nullptr;
+            check(fmi_dev_alloc(&p, bytes ? bytes : 1), "fmi_dev_alloc (scratch)");
+            ptr_ = static_cast<char*>(p);
+        } else {
+            ptr_ = new char[bytes ? bytes : 1];
+        }
+    }
+    Scratch(const Scratch&) = delete;
+    Scratch& operator=(const Scratch&) = delete;
+    Scratch& operator=(Scratch&& o) noexcept {
+        if (this != &o) {
+            release();
+            ptr_ = std::exchange(o.ptr_, nullptr);
+            bytes_ = o.bytes_;
+            device_ = o.device_;
+        }
+        return *this;
+    }
+    ~Scratch() { release(); }
+    char* get() const { return ptr_; }
+
+private:
+    void release() noexcept {
+        if (!ptr_) return;
+        if (device_)
+            (void)fmi_dev_free(ptr_);
+        else
+            delete[] ptr_;
+        ptr_ = nullptr;
+    }
+    char* ptr_ = nullptr;
+    std::size_t bytes_ = 0;
+    bool device_ = false;
+};
+
+// Byte copy that knows where both sides live (host-host memcpy, device-device D2D, staged otherwise).
+inline void copy_bytes(char* dst, bool dst_dev, const char* src, bool src_dev, std::size_t len) {
+    if (len == 0 || dst == src) return;
+    if (!dst_dev && !src_dev) {
+        std::copy(src, src + len, dst);
+        return;
+    }
+    int rc;
+    if (dst_dev && src_dev) rc = fmi_dev_d2d_async(dst, src, len, nullptr);
+    else if (dst_dev) rc = fmi_dev_h2d_async(dst, src, len, nullptr);
+    else rc = fmi_dev_d2h_async(dst, src, len, nullptr);
+    check(rc, "device copy");
+    check(fmi_stream_sync(nullptr), "fmi_stream_sync");
+}
+
+}  // namespace FMI::Dev
+
+#endif

@@ -1,0 +1,61 @@
+// FMI::Utils::ChannelPolicy — per-operation channel choice (mirrors reference include/utils/ChannelPolicy.h
+// and src/utils/ChannelPolicy.cpp:9-29): argmin of the model latency for Hint::fast, argmin of channel
+// price + FaaS runtime price for Hint::cheap. Channels are compared through their own
+// get_operation_latency / get_operation_price, so an RCCL channel competes on the same terms.
+// Added: channels that cannot carry the operation's buffers (host vs device) are skipped.
+#ifndef FMI_AMD_UTILS_CHANNELPOLICY_H
+#define FMI_AMD_UTILS_CHANNELPOLICY_H
+
+#include <limits>
+#include <map>
+#include <memory>
+#include <stdexcept>
+#include <string>
+
+#include "../comm/Channel.h"
+#include "Common.h"
+
+namespace FMI::Utils {
+
+class ChannelPolicy {
+public:
+    ChannelPolicy(std::map<std::string, std::shared_ptr<FMI::Comm::Channel>>& channels, peer_num num_peers,
+                  double faas_price, Hint hint)
+        : channels_(channels), num_peers_(num_peers), faas_price_(faas_price), hint_(hint) {}
+    virtual ~ChannelPolicy() = default;
+
+    virtual std::string get_channel(OperationInfo op_info) { return pick(op_info, false); }
+
+    //! Same choice for an operation on device-resident buffers.
+    virtual std::string get_device_channel(OperationInfo op_info) { return pick(op_info, true); }
+
+    void set_hint(Hint hint) { hint_ = hint; }
+
+protected:
+    std::string pick(const OperationInfo& op_info, bool on_device) {
+        std::string best;
+        double best_score = std::numeric_limits<double>::infinity();
+        for (const auto& [name, channel] : channels_) {
+            if (on_device ? !channel->supports_device_buffers() : !channel->supports_host_buffers()) continue;
+            const double latency = channel->get_operation_latency(op_info);
+            const double score = hint_ == fast ? latency : channel->get_operation_price(op_info) + latency * faas_price_;
+            if (best.empty() || score < best_score) {
+                best = name;
+                best_score = score;
+            }
+        }
+        if (best.empty())
+            throw std::runtime_error(std::string("no registered channel can carry ") + (on_device ? "device" : "host") +
+                                     " buffers");
+        return best;
+    }
+
+    std::map<std::string, std::shared_ptr<FMI::Comm::Channel>>& channels_;
+    peer_num num_peers_;
+    double faas_price_;
+    Hint hint_;
+};
+
+}  // namespace FMI::Utils
+
+#endif

@@ -1,0 +1,88 @@
+"""The C++ FMI::Communicator surface (fmi_amd/cpp/include/fmi) through its test program
+(fmi_amd/cpp/tests/test_communicator.cpp): the reference's own known-answer suites, evaluation order
+against the kernels' schedules, errors and policy (CPU); device buckets and host offload (GPU); and
+every peer's result of allreduce / reduce / scan checked bit-exactly against the oracle."""
+import os
+import subprocess
+import tempfile
+
+import numpy as np
+import pytest
+
+from oracle import fmi_oracle as orc
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EXE = os.path.join(ROOT, "build", "cpp", "test_communicator")
+
+
+@pytest.fixture(scope="module")
+def exe():
+    if not os.path.exists(EXE):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "fmi_amd", "cpp")], check=True)
+    return EXE
+
+
+def _dump(exe, kind, P, n, mode="host"):
+    with tempfile.NamedTemporaryFile(suffix=".bin", delete=False) as f:
+        path = f.name
+    try:
+        cmd = [exe, "--dump", kind, str(P), str(n), path] + ([f"--{mode}"] if mode != "host" else [])
+        subprocess.run(cmd, check=True, timeout=300)
+        raw = np.fromfile(path, dtype=np.float32)
+    finally:
+        os.unlink(path)
+    raw = raw.reshape(2, P, n)
+    return raw[0], raw[1]
+
+
+def _expected(kind, P, n):
+    xs = [orc.synthetic(np.float32, n, 42, p) for p in range(P)]
+    ordered = kind.endswith("_ltr")
+    base = kind[:-4] if ordered else kind
+    flags = dict(commutative=not ordered, associative=not ordered)
+    if base == "allreduce":
+        res, sends = orc.allreduce(xs, orc.op_sum, **flags)
+    elif base == "scan":
+        res, sends = orc.scan(xs, orc.op_sum, **flags)
+    else:
+        root_res, sends = orc.reduce(xs, orc.op_sum, root=0, **flags)
+        res = [root_res] + [None] * (P - 1)
+    return res, sends
+
+
+def _check(kind, P, n, recv, send):
+    res, sends = _expected(kind, P, n)
+    for p in range(P):
+        if res[p] is not None:
+            assert np.array_equal(recv[p].view(np.uint32), res[p].view(np.uint32)), f"{kind} P={P} peer {p}"
+        assert np.array_equal(send[p].view(np.uint32), sends[p].view(np.uint32)), f"{kind} P={P} sendbuf {p}"
+
+
+def test_cpp_suite_host(exe):
+    out = subprocess.run([exe], capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-4000:]
+    assert "0 failed checks" in out.stderr
+
+
+@pytest.mark.parametrize("kind", ["allreduce", "reduce", "scan", "allreduce_ltr", "reduce_ltr", "scan_ltr"])
+@pytest.mark.parametrize("P", [2, 3, 5, 8])
+def test_cpp_host_path_matches_oracle(exe, kind, P):
+    n = 1027
+    recv, send = _dump(exe, kind, P, n)
+    _check(kind, P, n, recv, send)
+
+
+@pytest.mark.gpu
+def test_cpp_suite_gpu(exe):
+    out = subprocess.run([exe, "--gpu"], capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-4000:]
+    assert "0 failed checks" in out.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["device", "offload"])
+@pytest.mark.parametrize("kind", ["allreduce", "reduce", "scan", "allreduce_ltr", "scan_ltr"])
+def test_cpp_device_path_matches_oracle(exe, mode, kind):
+    P, n = 8, (1 << 16) + 5
+    recv, send = _dump(exe, kind, P, n, mode)
+    _check(kind, P, n, recv, send)
