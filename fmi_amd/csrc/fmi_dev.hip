@@ -35,8 +35,8 @@ DeviceState g_state;  // one process drives one device (one process per GPU, as 
 
 // Defaults from tools/tune_pair.py on MI355X (C2, 256 MiB f32): nontemporal one-shot tiles, 4 × 16 B per
 // operand per thread, 256-thread workgroups — 125 µs = 6.4 TB/s vs 142 µs for plain loads/stores.
-std::atomic<long long> g_tune[5] = {2 /*variant: nontemporal tiles*/, 4 /*unroll*/, 256 /*block*/,
-                                    8 /*grid per CU*/, 64ll << 20 /*host chunk*/};
+std::atomic<long long> g_tune[6] = {2 /*variant: nontemporal tiles*/, 4 /*unroll*/, 256 /*block*/,
+                                    8 /*grid per CU*/, 64ll << 20 /*host chunk*/, 1 /*host zero-copy*/};
 
 int hip_fail(const char* what, hipError_t e) {
     return fail(FMI_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
@@ -58,6 +58,18 @@ int require_device() {
 hipStream_t resolve(fmi_stream_t s) { return s ? static_cast<hipStream_t>(s) : g_state.stream; }
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+// Is `p` page-locked host memory the device can address? Returns its device-side address.
+bool host_mapped(void* p, void** dev) {
+    hipPointerAttribute_t attr;
+    if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+        (void)hipGetLastError();  // pageable memory reports an error: clear it
+        return false;
+    }
+    if (attr.type != hipMemoryTypeHost || attr.devicePointer == nullptr) return false;
+    *dev = attr.devicePointer;
+    return true;
+}
 
 // ----------------------------------------------------------------------------------------------------
 // Pairwise launch policy.
@@ -470,6 +482,19 @@ int fmi_host_reduce_pair(int op, int dtype, void* inout, const void* in, size_t 
     if (n == 0) return FMI_OK;
     if (!inout || !in) return fail(FMI_ERR_INVALID, "null buffer");
     if (int rc = require_device()) return rc;
+    if (g_tune[FMI_TUNE_HOST_ZERO_COPY].load()) {
+        // Page-locked buckets: the kernel streams them straight over PCIe (reads of both operands and the
+        // write-back share the link concurrently, no staging copies, no DMA-engine serialisation).
+        void* dx = nullptr;
+        void* dy = nullptr;
+        if (host_mapped(inout, &dx) && host_mapped(const_cast<void*>(in), &dy)) {
+            hipStream_t s = g_state.stream;
+            int rc = launch_combine(op, dtype, dx, dx, dy, n, s);
+            if (rc != FMI_OK) return rc;
+            FMI_HIP_TRY(hipStreamSynchronize(s));
+            return FMI_OK;
+        }
+    }
     std::lock_guard<std::mutex> lk(g_mu);
     size_t chunk_elems = static_cast<size_t>(std::max<long long>(g_tune[FMI_TUNE_HOST_CHUNK].load(), 1 << 16)) / esz;
     chunk_elems = std::max<size_t>(16, chunk_elems / 16 * 16);
@@ -561,6 +586,9 @@ int fmi_tune_set(int key, long long value) {
         case FMI_TUNE_HOST_CHUNK:
             if (value < (1 << 16)) return fail(FMI_ERR_INVALID, "host chunk must be >= 64 KiB");
             break;
+        case FMI_TUNE_HOST_ZERO_COPY:
+            if (value != 0 && value != 1) return fail(FMI_ERR_INVALID, "host zero-copy must be 0 or 1");
+            break;
         default: return fail(FMI_ERR_INVALID, "unknown tuning key");
     }
     g_tune[key].store(value);
@@ -568,7 +596,7 @@ int fmi_tune_set(int key, long long value) {
 }
 
 int fmi_tune_get(int key, long long* value) {
-    if (!value || key < 0 || key > FMI_TUNE_HOST_CHUNK) return fail(FMI_ERR_INVALID, "bad tuning query");
+    if (!value || key < 0 || key > FMI_TUNE_HOST_ZERO_COPY) return fail(FMI_ERR_INVALID, "bad tuning query");
     *value = g_tune[key].load();
     return FMI_OK;
 }

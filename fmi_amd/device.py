@@ -46,6 +46,7 @@ class Tune(enum.IntEnum):
     BLOCK = 2
     GRID_PER_CU = 3
     HOST_CHUNK = 4
+    HOST_ZERO_COPY = 5
 
 
 NP_DTYPE = {DType.F32: np.float32, DType.F64: np.float64, DType.I32: np.int32, DType.I64: np.int64}
@@ -262,6 +263,33 @@ def host_reduce_pair(op: Op, inout: np.ndarray, src: np.ndarray) -> None:
     if not (inout.flags.c_contiguous and src.flags.c_contiguous):
         raise ValueError("host_reduce_pair: arrays must be contiguous")
     _lib.call("fmi_host_reduce_pair", int(op), int(dtype_of(inout)), inout.ctypes.data, src.ctypes.data, inout.size)
+
+
+class PinnedArray:
+    """A numpy array over page-locked host memory (fmi_host_pin_alloc) — the recv-buffer kind the
+    zero-copy host path combines in place over PCIe. Free with .free() (or on garbage collection)."""
+
+    def __init__(self, n: int, dtype):
+        self.dtype = np.dtype(dtype)
+        nbytes = max(1, int(n) * self.dtype.itemsize)
+        p = ctypes.c_void_p()
+        _lib.call("fmi_host_pin_alloc", ctypes.byref(p), nbytes)
+        self.ptr = p.value
+        raw = (ctypes.c_char * nbytes).from_address(self.ptr)
+        self.array = np.frombuffer(raw, dtype=self.dtype, count=int(n))
+
+    def free(self) -> None:
+        if self.ptr:
+            self.array = None
+            _lib.call("fmi_host_pin_free", self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            if getattr(self, "ptr", None):
+                _lib.load().fmi_host_pin_free(self.ptr)
+        except Exception:
+            pass
 
 
 def _check_peers(out: Bucket, ins: Sequence[Bucket]) -> None:

@@ -156,7 +156,9 @@ typedef enum {
     FMI_TUNE_PAIR_UNROLL = 1,  /* 16-B vectors per thread per operand: 1, 2, 4, 8 */
     FMI_TUNE_BLOCK = 2,        /* threads per workgroup: 256, 512, 1024 */
     FMI_TUNE_GRID_PER_CU = 3,  /* workgroups per CU for the grid-stride variant */
-    FMI_TUNE_HOST_CHUNK = 4    /* bytes per chunk of fmi_host_reduce_pair */
+    FMI_TUNE_HOST_CHUNK = 4,   /* bytes per chunk of fmi_host_reduce_pair's staged pipeline */
+    FMI_TUNE_HOST_ZERO_COPY = 5 /* 1: page-locked host buckets are combined in place over PCIe by the
+                                   kernel (no staging); 0: always the staged H2D/kernel/D2H pipeline */
 } fmi_tune_key_t;
 int fmi_tune_set(int key, long long value);
 int fmi_tune_get(int key, long long* value);

@@ -269,6 +269,29 @@ def test_host_reduce_pair(device, n):
         fmi_amd.tune_set(Tune.HOST_CHUNK, old)
 
 
+@pytest.mark.parametrize("zero_copy", [0, 1])
+@pytest.mark.parametrize("n", [3, 4099, (1 << 22) + 1])
+def test_host_reduce_pair_pinned(device, zero_copy, n):
+    from fmi_amd.device import PinnedArray
+
+    old = fmi_amd.tune_get(Tune.HOST_ZERO_COPY)
+    try:
+        fmi_amd.tune_set(Tune.HOST_ZERO_COPY, zero_copy)
+        for dtype, op in ((np.float32, Op.SUM), (np.int64, Op.MIN), (np.float64, Op.PROD)):
+            a, b = inputs(dtype, n, 0), inputs(dtype, n, 1)
+            pa, pb = PinnedArray(n, dtype), PinnedArray(n, dtype)
+            pa.array[:] = a
+            pb.array[:] = b
+            fmi_amd.host_reduce_pair(op, pa.array, pb.array)
+            with np.errstate(all="ignore"):
+                assert_bit_equal(pa.array.copy(), orc.pairwise(OPNAME[op], a, b), f"{op.name} zero_copy={zero_copy}")
+            assert_bit_equal(pb.array.copy(), b, "in operand untouched")
+            pa.free()
+            pb.free()
+    finally:
+        fmi_amd.tune_set(Tune.HOST_ZERO_COPY, old)
+
+
 # ------------------------------------------------------------------------------------------------
 # BASELINE.json full-size configs
 # ------------------------------------------------------------------------------------------------

@@ -71,6 +71,13 @@ def main():
             row(f"pair {op.name.lower()} {np.dtype(dt).name} 256MiB", 3 * 256 * MIB, med, mn)
         del sets
 
+    # calibration: the runtime's device-to-device copy (1 read + 1 write stream) at 256 MiB
+    src = Bucket(64 * MIB, np.float32)
+    dst = Bucket(64 * MIB, np.float32)
+    med, mn = timed(lambda k: dst.copy_from(src), it, 1)
+    row("calibration hipMemcpy D2D 256MiB", 2 * 256 * MIB, med, mn, note="runtime copy kernel, read:write 1:1")
+    del src, dst
+
     # C3a: int64 max, 64 MiB buckets; 8 rotating sets = 1.5 GiB working set (defeats the MALL)
     n = 64 * MIB // 8
     sets = [(Bucket(n, np.int64).fill_synthetic(42 + s, 0), Bucket(n, np.int64).fill_synthetic(42 + s, 1))
@@ -108,7 +115,8 @@ def main():
     hb, pb = pinned(n, np.float32)
     ha[:] = 1.0
     hb[:] = 2.0
-    for chunk in (16, 64):
+    for zero_copy, chunk in ((0, 16), (0, 64), (1, 64)):
+        fmi_amd.tune_set(fmi_amd.Tune.HOST_ZERO_COPY, zero_copy)
         fmi_amd.tune_set(fmi_amd.Tune.HOST_CHUNK, chunk * MIB)
         fmi_amd.host_reduce_pair(Op.SUM, ha, hb)
         ts = []
@@ -117,9 +125,13 @@ def main():
             fmi_amd.host_reduce_pair(Op.SUM, ha, hb)
             ts.append(time.perf_counter() - t0)
         med = statistics.median(ts)
-        print(json.dumps(dict(config=f"host pinned pair sum f32 256MiB chunk {chunk}MiB", median_ms=round(med * 1e3, 3),
+        name = "zero-copy kernel" if zero_copy else f"staged pipeline chunk {chunk}MiB"
+        print(json.dumps(dict(config=f"host pinned pair sum f32 256MiB {name}", median_ms=round(med * 1e3, 3),
                               bucket_gib_s=round(256 / 1024 / med, 3),
                               pcie_gb_s=round(3 * 256 * MIB / med / 1e9, 2))), flush=True)
+    ha_chk = ha.copy()
+    assert np.all(ha_chk == ha_chk[0]), "host pair result not uniform"
+    fmi_amd.tune_set(fmi_amd.Tune.HOST_ZERO_COPY, 1)
     _lib.call("fmi_host_pin_free", pa)
     _lib.call("fmi_host_pin_free", pb)
     a = np.ones(n, np.float32)
