@@ -20,6 +20,7 @@ FMI_ERR_HIP = -2
 FMI_ERR_NO_DEVICE = -3
 FMI_ERR_UNSUPPORTED = -4
 FMI_ERR_ALLOC = -5
+FMI_ERR_COMM = -6
 
 _STATUS_NAMES = {
     FMI_ERR_INVALID: "FMI_ERR_INVALID",
@@ -27,6 +28,7 @@ _STATUS_NAMES = {
     FMI_ERR_NO_DEVICE: "FMI_ERR_NO_DEVICE",
     FMI_ERR_UNSUPPORTED: "FMI_ERR_UNSUPPORTED",
     FMI_ERR_ALLOC: "FMI_ERR_ALLOC",
+    FMI_ERR_COMM: "FMI_ERR_COMM",
 }
 
 
@@ -73,6 +75,19 @@ SIGNATURES = {
     "fmi_dev_reduce_tree": (_i, [_i, _i, _i, _vp, _c.POINTER(_vp), _i, _i, _sz, _vp]),
     "fmi_dev_scan_peers": (_i, [_i, _i, _i, _c.POINTER(_vp), _c.POINTER(_vp), _i, _sz, _vp]),
     "fmi_host_reduce_pair": (_i, [_i, _i, _vp, _vp, _sz]),
+    "fmi_comm_unique_id": (_i, [_i, _vp, _sz]),
+    "fmi_comm_init": (_i, [_c.POINTER(_vp), _vp, _i, _i]),
+    "fmi_comm_destroy": (_i, [_vp]),
+    "fmi_comm_size": (_i, [_vp, _c.POINTER(_i), _c.POINTER(_i)]),
+    "fmi_comm_allreduce": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _sz, _vp]),
+    "fmi_comm_reduce": (_i, [_vp, _i, _i, _i, _vp, _vp, _sz, _i, _vp]),
+    "fmi_comm_scan": (_i, [_vp, _i, _i, _i, _vp, _vp, _sz, _vp]),
+    "fmi_comm_bcast": (_i, [_vp, _vp, _sz, _i, _vp]),
+    "fmi_comm_gather": (_i, [_vp, _vp, _vp, _sz, _i, _vp]),
+    "fmi_comm_scatter": (_i, [_vp, _vp, _vp, _sz, _i, _vp]),
+    "fmi_comm_send": (_i, [_vp, _vp, _sz, _i, _vp]),
+    "fmi_comm_recv": (_i, [_vp, _vp, _sz, _i, _vp]),
+    "fmi_comm_barrier": (_i, [_vp, _vp]),
     "fmi_dev_fill_synthetic": (_i, [_i, _vp, _sz, _c.c_uint64, _c.c_uint32, _vp]),
     "fmi_schedule_expr": (_i, [_i, _i, _i, _c.c_char_p, _sz]),
     "fmi_tune_set": (_i, [_i, _c.c_longlong]),

@@ -1,0 +1,98 @@
+"""Python handle over the C-ABI communicator (include/fmi_dev.h, "sharded device collectives").
+
+`Comm` wraps fmi_comm_*: sharded allreduce / reduce / scan of device buckets across ranks (one rank per
+GPU over RCCL, or ranks as threads of one process over the LOCAL transport), with the combine done by the
+fused kernels in the reference's evaluation order (reference src/comm/PeerToPeer.cpp). Buffers are
+`fmi_amd.Bucket`s or raw device pointers.
+"""
+from __future__ import annotations
+
+import ctypes
+import enum
+from typing import Optional
+
+from . import _lib
+from .device import Alg, Bucket, Op, _sptr
+
+ID_BYTES = 128
+
+
+class Transport(enum.IntEnum):
+    RCCL = 0
+    LOCAL = 1
+
+
+class Path(enum.IntEnum):
+    TREE = 0  # all-to-all + fused kernel in the reference's order + all-gather (bit-exact)
+    RCCL = 1  # RCCL reduce-scatter + all-gather (RCCL's order)
+
+
+def unique_id(transport: Transport = Transport.RCCL) -> bytes:
+    buf = ctypes.create_string_buffer(ID_BYTES)
+    _lib.call("fmi_comm_unique_id", int(transport), buf, ID_BYTES)
+    return buf.raw
+
+
+def _p(x) -> Optional[int]:
+    if x is None:
+        return None
+    return x.ptr if isinstance(x, Bucket) else int(x)
+
+
+class Comm:
+    def __init__(self, uid: bytes, nranks: int, rank: int):
+        if len(uid) != ID_BYTES:
+            raise ValueError("communicator id must be 128 bytes")
+        h = ctypes.c_void_p()
+        self._id = ctypes.create_string_buffer(uid, ID_BYTES)
+        _lib.call("fmi_comm_init", ctypes.byref(h), self._id, nranks, rank)
+        self.handle = h.value
+        self.nranks = nranks
+        self.rank = rank
+
+    def destroy(self) -> None:
+        if self.handle:
+            _lib.call("fmi_comm_destroy", self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            if getattr(self, "handle", None):
+                _lib.load().fmi_comm_destroy(self.handle)
+        except Exception:
+            pass
+
+    def allreduce(self, op: Op, send: Bucket, recv: Bucket, ordered: bool = False, path: Path = Path.TREE,
+                  stream=None) -> None:
+        alg = Alg.REDUCE_LTR if ordered else Alg.ALLREDUCE
+        _lib.call("fmi_comm_allreduce", self.handle, int(op), int(send.dtype), int(alg), int(path), _p(send), _p(recv),
+                  send.n, _sptr(stream))
+
+    def reduce(self, op: Op, send: Bucket, recv: Optional[Bucket], root: int, ordered: bool = False,
+               stream=None) -> None:
+        alg = Alg.REDUCE_LTR if ordered else Alg.REDUCE
+        _lib.call("fmi_comm_reduce", self.handle, int(op), int(send.dtype), int(alg), _p(send), _p(recv), send.n, root,
+                  _sptr(stream))
+
+    def scan(self, op: Op, send: Bucket, recv: Bucket, ordered: bool = False, stream=None) -> None:
+        alg = Alg.SCAN_LTR if ordered else Alg.SCAN
+        _lib.call("fmi_comm_scan", self.handle, int(op), int(send.dtype), int(alg), _p(send), _p(recv), send.n,
+                  _sptr(stream))
+
+    def bcast(self, buf: Bucket, root: int, stream=None) -> None:
+        _lib.call("fmi_comm_bcast", self.handle, _p(buf), buf.nbytes, root, _sptr(stream))
+
+    def gather(self, send: Bucket, recv: Optional[Bucket], root: int, stream=None) -> None:
+        _lib.call("fmi_comm_gather", self.handle, _p(send), _p(recv), send.nbytes, root, _sptr(stream))
+
+    def scatter(self, send: Optional[Bucket], recv: Bucket, root: int, stream=None) -> None:
+        _lib.call("fmi_comm_scatter", self.handle, _p(send), _p(recv), recv.nbytes, root, _sptr(stream))
+
+    def send(self, buf: Bucket, peer: int, stream=None) -> None:
+        _lib.call("fmi_comm_send", self.handle, _p(buf), buf.nbytes, peer, _sptr(stream))
+
+    def recv(self, buf: Bucket, peer: int, stream=None) -> None:
+        _lib.call("fmi_comm_recv", self.handle, _p(buf), buf.nbytes, peer, _sptr(stream))
+
+    def barrier(self, stream=None) -> None:
+        _lib.call("fmi_comm_barrier", self.handle, _sptr(stream))

@@ -1,0 +1,668 @@
+// fmi_comm.hip — sharded device collectives across GPUs (include/fmi_dev.h, "sharded device collectives").
+//
+// One rank = one FMI peer = one GPU. The reference's allreduce / reduce / scan (src/comm/PeerToPeer.cpp)
+// exchange whole buckets peer to peer; here every bucket is cut into N shards so that all of a GPU's xGMI
+// links carry traffic at once, and the combine of each shard is ONE pass of the fused P-way kernel in the
+// reference's evaluation order (fmi_schedule.h):
+//
+//   allreduce  all-to-all(shards) -> fused tree over the N partials of my shard -> all-gather
+//   reduce     all-to-all(shards) -> fused tree in reduce order for `root`       -> gather to root
+//   scan       all-to-all(shards) -> fused peer-axis scan (N prefixes of my shard) -> all-to-all back
+//
+// Transports: RCCL (librccl resolved with dlopen on first use, so processes that never use it never load
+// it) and LOCAL (ranks are threads of one process on one device; the exchanges are device-to-device
+// copies) — the latter runs the exact same schedules, which is how the multi-rank logic is tested on a
+// single MI355X.
+#include <dlfcn.h>
+#include <rccl/rccl.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <condition_variable>
+#include <cstring>
+#include <deque>
+#include <functional>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "fmi_internal.h"
+
+namespace fmi::dev {
+namespace {
+
+constexpr size_t kShardAlign = 64;  // elements: shards stay 256-B aligned for the 16-B vector kernels
+
+int hip_err(const char* what, hipError_t e) { return fail(FMI_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e)); }
+
+#define FMI_COMM_HIP(call)                                 \
+    do {                                                   \
+        const hipError_t e_ = (call);                      \
+        if (e_ != hipSuccess) return hip_err(#call, e_);   \
+    } while (0)
+#define FMI_COMM_RC(call)              \
+    do {                               \
+        const int rc_ = (call);        \
+        if (rc_ != FMI_OK) return rc_; \
+    } while (0)
+
+// ---------------------------------------------------------------------------------------------------
+// RCCL entry points (dlopen'd once)
+// ---------------------------------------------------------------------------------------------------
+struct RcclApi {
+    ncclResult_t (*GetUniqueId)(ncclUniqueId*);
+    ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int);
+    ncclResult_t (*CommDestroy)(ncclComm_t);
+    const char* (*GetErrorString)(ncclResult_t);
+    ncclResult_t (*Send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t);
+    ncclResult_t (*Recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t);
+    ncclResult_t (*GroupStart)();
+    ncclResult_t (*GroupEnd)();
+    ncclResult_t (*AllGather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t);
+    ncclResult_t (*ReduceScatter)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t);
+    ncclResult_t (*Broadcast)(const void*, void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t);
+    ncclResult_t (*AllReduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t);
+};
+
+const RcclApi* rccl_api() {
+    static std::once_flag once;
+    static RcclApi api;
+    static bool ok = false;
+    static std::string err;
+    std::call_once(once, [] {
+        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) {
+            err = std::string("cannot load librccl: ") + dlerror();
+            return;
+        }
+#define FMI_RCCL_SYM(name)                                                                  \
+    api.name = reinterpret_cast<decltype(api.name)>(dlsym(h, "nccl" #name));                \
+    if (!api.name) {                                                                        \
+        err = "librccl lacks nccl" #name;                                                   \
+        return;                                                                             \
+    }
+        FMI_RCCL_SYM(GetUniqueId)
+        FMI_RCCL_SYM(CommInitRank)
+        FMI_RCCL_SYM(CommDestroy)
+        FMI_RCCL_SYM(GetErrorString)
+        FMI_RCCL_SYM(Send)
+        FMI_RCCL_SYM(Recv)
+        FMI_RCCL_SYM(GroupStart)
+        FMI_RCCL_SYM(GroupEnd)
+        FMI_RCCL_SYM(AllGather)
+        FMI_RCCL_SYM(ReduceScatter)
+        FMI_RCCL_SYM(Broadcast)
+        FMI_RCCL_SYM(AllReduce)
+#undef FMI_RCCL_SYM
+        ok = true;
+    });
+    if (!ok) {
+        fail(FMI_ERR_COMM, err);
+        return nullptr;
+    }
+    return &api;
+}
+
+int nccl_fail(const RcclApi* api, const char* what, ncclResult_t r) {
+    return fail(FMI_ERR_COMM, std::string(what) + ": " + api->GetErrorString(r));
+}
+
+#define FMI_NCCL(api, call)                                        \
+    do {                                                           \
+        const ncclResult_t r_ = (api)->call;                       \
+        if (r_ != ncclSuccess) return nccl_fail((api), #call, r_); \
+    } while (0)
+
+// ---------------------------------------------------------------------------------------------------
+// transports
+// ---------------------------------------------------------------------------------------------------
+class Transport {
+public:
+    Transport(int n, int rank) : n_(n), rank_(rank) {}
+    virtual ~Transport() = default;
+    // recv[j*bytes ...] = rank j's send[rank*bytes ...]
+    virtual int all_to_all(const char* send, char* recv, size_t bytes, hipStream_t s) = 0;
+    // recv[j*bytes ...] = rank j's send[0 .. bytes)
+    virtual int all_gather(const char* send, char* recv, size_t bytes, hipStream_t s) = 0;
+    virtual int gather(const char* send, char* recv, size_t bytes, int root, hipStream_t s) = 0;
+    virtual int scatter(const char* send, char* recv, size_t bytes, int root, hipStream_t s) = 0;
+    virtual int bcast(char* buf, size_t bytes, int root, hipStream_t s) = 0;
+    virtual int send(const char* buf, size_t bytes, int peer, hipStream_t s) = 0;
+    virtual int recv(char* buf, size_t bytes, int peer, hipStream_t s) = 0;
+    virtual int barrier(hipStream_t s) = 0;
+    virtual int reduce_scatter(int, int, const void*, void*, size_t, hipStream_t) {
+        return fail(FMI_ERR_UNSUPPORTED, "path RCCL needs the RCCL transport");
+    }
+    int n() const { return n_; }
+    int rank() const { return rank_; }
+
+protected:
+    int n_;
+    int rank_;
+};
+
+ncclDataType_t nccl_type(int dtype) {
+    switch (dtype) {
+        case FMI_F32: return ncclFloat32;
+        case FMI_F64: return ncclFloat64;
+        case FMI_I32: return ncclInt32;
+        default: return ncclInt64;
+    }
+}
+
+ncclRedOp_t nccl_op(int op) {
+    switch (op) {
+        case FMI_OP_SUM: return ncclSum;
+        case FMI_OP_PROD: return ncclProd;
+        case FMI_OP_MAX: return ncclMax;
+        default: return ncclMin;
+    }
+}
+
+class RcclTransport final : public Transport {
+public:
+    RcclTransport(const RcclApi* api, ncclComm_t comm, int n, int rank) : Transport(n, rank), api_(api), comm_(comm) {}
+    ~RcclTransport() override { (void)api_->CommDestroy(comm_); }
+
+    int all_to_all(const char* send, char* recv, size_t bytes, hipStream_t s) override {
+        FMI_NCCL(api_, GroupStart());
+        for (int j = 0; j < n_; ++j) {
+            FMI_NCCL(api_, Send(send + j * bytes, bytes, ncclUint8, j, comm_, s));
+            FMI_NCCL(api_, Recv(recv + j * bytes, bytes, ncclUint8, j, comm_, s));
+        }
+        FMI_NCCL(api_, GroupEnd());
+        return FMI_OK;
+    }
+    int all_gather(const char* send, char* recv, size_t bytes, hipStream_t s) override {
+        FMI_NCCL(api_, AllGather(send, recv, bytes, ncclUint8, comm_, s));
+        return FMI_OK;
+    }
+    int gather(const char* send, char* recv, size_t bytes, int root, hipStream_t s) override {
+        FMI_NCCL(api_, GroupStart());
+        if (rank_ == root) {
+            for (int j = 0; j < n_; ++j) {
+                if (j == root) continue;
+                FMI_NCCL(api_, Recv(recv + j * bytes, bytes, ncclUint8, j, comm_, s));
+            }
+        } else {
+            FMI_NCCL(api_, Send(send, bytes, ncclUint8, root, comm_, s));
+        }
+        FMI_NCCL(api_, GroupEnd());
+        if (rank_ == root && bytes) FMI_COMM_HIP(hipMemcpyAsync(recv + root * bytes, send, bytes, hipMemcpyDeviceToDevice, s));
+        return FMI_OK;
+    }
+    int scatter(const char* send, char* recv, size_t bytes, int root, hipStream_t s) override {
+        FMI_NCCL(api_, GroupStart());
+        if (rank_ == root) {
+            for (int j = 0; j < n_; ++j) {
+                if (j == root) continue;
+                FMI_NCCL(api_, Send(send + j * bytes, bytes, ncclUint8, j, comm_, s));
+            }
+        } else {
+            FMI_NCCL(api_, Recv(recv, bytes, ncclUint8, root, comm_, s));
+        }
+        FMI_NCCL(api_, GroupEnd());
+        if (rank_ == root && bytes) FMI_COMM_HIP(hipMemcpyAsync(recv, send + root * bytes, bytes, hipMemcpyDeviceToDevice, s));
+        return FMI_OK;
+    }
+    int bcast(char* buf, size_t bytes, int root, hipStream_t s) override {
+        FMI_NCCL(api_, Broadcast(buf, buf, bytes, ncclUint8, root, comm_, s));
+        return FMI_OK;
+    }
+    int send(const char* buf, size_t bytes, int peer, hipStream_t s) override {
+        FMI_NCCL(api_, Send(buf, bytes, ncclUint8, peer, comm_, s));
+        return FMI_OK;
+    }
+    int recv(char* buf, size_t bytes, int peer, hipStream_t s) override {
+        FMI_NCCL(api_, Recv(buf, bytes, ncclUint8, peer, comm_, s));
+        return FMI_OK;
+    }
+    int barrier(hipStream_t s) override {
+        if (!token_) FMI_COMM_HIP(hipMalloc(&token_, sizeof(int)));
+        FMI_NCCL(api_, AllReduce(token_, token_, 1, ncclInt32, ncclSum, comm_, s));
+        FMI_COMM_HIP(hipStreamSynchronize(s));
+        return FMI_OK;
+    }
+    int reduce_scatter(int op, int dtype, const void* send, void* recv, size_t count, hipStream_t s) override {
+        FMI_NCCL(api_, ReduceScatter(send, recv, count, nccl_type(dtype), nccl_op(op), comm_, s));
+        return FMI_OK;
+    }
+
+private:
+    const RcclApi* api_;
+    ncclComm_t comm_;
+    void* token_ = nullptr;
+};
+
+// Ranks of one process on one device: a rendezvous hub per communicator id.
+struct Hub {
+    explicit Hub(int n) : n(n), ptrs(n, nullptr) {}
+    int n;
+    std::mutex mu;
+    std::condition_variable cv;
+    int arrived = 0;
+    uint64_t generation = 0;
+    std::vector<const char*> ptrs;
+    struct Msg {
+        const char* buf;
+        size_t bytes;
+        bool done;
+    };
+    std::map<std::pair<int, int>, std::deque<Msg*>> box;
+
+    void barrier() {
+        std::unique_lock<std::mutex> lk(mu);
+        const uint64_t g = generation;
+        if (++arrived == n) {
+            arrived = 0;
+            ++generation;
+            cv.notify_all();
+        } else {
+            cv.wait(lk, [&] { return generation != g; });
+        }
+    }
+};
+
+std::mutex g_hub_mu;
+std::map<uint64_t, std::weak_ptr<Hub>> g_hubs;
+std::atomic<uint64_t> g_hub_counter{1};
+constexpr char kLocalMagic[8] = {'F', 'M', 'I', 'L', 'O', 'C', 'A', 'L'};
+
+class LocalTransport final : public Transport {
+public:
+    LocalTransport(std::shared_ptr<Hub> hub, int n, int rank) : Transport(n, rank), hub_(std::move(hub)) {}
+
+    int all_to_all(const char* send, char* recv, size_t bytes, hipStream_t s) override {
+        return exchange(send, s, [&](const std::vector<const char*>& all) -> int {
+            for (int j = 0; j < n_; ++j)
+                if (bytes) FMI_COMM_HIP(hipMemcpyAsync(recv + j * bytes, all[j] + rank_ * bytes, bytes, hipMemcpyDeviceToDevice, s));
+            return FMI_OK;
+        });
+    }
+    int all_gather(const char* send, char* recv, size_t bytes, hipStream_t s) override {
+        return exchange(send, s, [&](const std::vector<const char*>& all) -> int {
+            for (int j = 0; j < n_; ++j)
+                if (bytes) FMI_COMM_HIP(hipMemcpyAsync(recv + j * bytes, all[j], bytes, hipMemcpyDeviceToDevice, s));
+            return FMI_OK;
+        });
+    }
+    int gather(const char* send, char* recv, size_t bytes, int root, hipStream_t s) override {
+        return exchange(send, s, [&](const std::vector<const char*>& all) -> int {
+            if (rank_ != root) return FMI_OK;
+            for (int j = 0; j < n_; ++j)
+                if (bytes) FMI_COMM_HIP(hipMemcpyAsync(recv + j * bytes, all[j], bytes, hipMemcpyDeviceToDevice, s));
+            return FMI_OK;
+        });
+    }
+    int scatter(const char* send, char* recv, size_t bytes, int root, hipStream_t s) override {
+        return exchange(send, s, [&](const std::vector<const char*>& all) -> int {
+            if (bytes) FMI_COMM_HIP(hipMemcpyAsync(recv, all[root] + rank_ * bytes, bytes, hipMemcpyDeviceToDevice, s));
+            return FMI_OK;
+        });
+    }
+    int bcast(char* buf, size_t bytes, int root, hipStream_t s) override {
+        return exchange(buf, s, [&](const std::vector<const char*>& all) -> int {
+            if (rank_ != root && bytes) FMI_COMM_HIP(hipMemcpyAsync(buf, all[root], bytes, hipMemcpyDeviceToDevice, s));
+            return FMI_OK;
+        });
+    }
+    int send(const char* buf, size_t bytes, int peer, hipStream_t s) override {
+        FMI_COMM_HIP(hipStreamSynchronize(s));
+        Hub::Msg msg{buf, bytes, false};
+        std::unique_lock<std::mutex> lk(hub_->mu);
+        hub_->box[{rank_, peer}].push_back(&msg);
+        hub_->cv.notify_all();
+        hub_->cv.wait(lk, [&] { return msg.done; });  // rendezvous: the receiver has copied it
+        return FMI_OK;
+    }
+    int recv(char* buf, size_t bytes, int peer, hipStream_t s) override {
+        Hub::Msg* msg = nullptr;
+        {
+            std::unique_lock<std::mutex> lk(hub_->mu);
+            auto& q = hub_->box[{peer, rank_}];
+            hub_->cv.wait(lk, [&] { return !q.empty(); });
+            msg = q.front();
+            q.pop_front();
+        }
+        int rc = FMI_OK;
+        if (msg->bytes != bytes) {
+            rc = fail(FMI_ERR_COMM, "local transport: message of " + std::to_string(msg->bytes) + " bytes, expected " +
+                                        std::to_string(bytes));
+        } else if (bytes) {
+            hipError_t e = hipMemcpyAsync(buf, msg->buf, bytes, hipMemcpyDeviceToDevice, s);
+            if (e == hipSuccess) e = hipStreamSynchronize(s);
+            if (e != hipSuccess) rc = hip_err("local transport recv", e);
+        }
+        std::lock_guard<std::mutex> lk(hub_->mu);
+        msg->done = true;
+        hub_->cv.notify_all();
+        return rc;
+    }
+    int barrier(hipStream_t s) override {
+        FMI_COMM_HIP(hipStreamSynchronize(s));
+        hub_->barrier();
+        return FMI_OK;
+    }
+
+private:
+    // Publish my buffer, wait for everyone, run `work` over all ranks' buffers, wait until everyone's
+    // copies have completed (so no rank reuses a published buffer while another still reads it).
+    int exchange(const char* mine, hipStream_t s, const std::function<int(const std::vector<const char*>&)>& work) {
+        FMI_COMM_HIP(hipStreamSynchronize(s));
+        {
+            std::lock_guard<std::mutex> lk(hub_->mu);
+            hub_->ptrs[rank_] = mine;
+        }
+        hub_->barrier();
+        std::vector<const char*> all;
+        {
+            std::lock_guard<std::mutex> lk(hub_->mu);
+            all = hub_->ptrs;
+        }
+        int rc = work(all);
+        const hipError_t e = hipStreamSynchronize(s);
+        hub_->barrier();
+        if (rc == FMI_OK && e != hipSuccess) rc = hip_err("local transport exchange", e);
+        return rc;
+    }
+
+    std::shared_ptr<Hub> hub_;
+};
+
+// ---------------------------------------------------------------------------------------------------
+// communicator
+// ---------------------------------------------------------------------------------------------------
+struct Comm {
+    std::unique_ptr<Transport> t;
+    std::mutex mu;
+    void* buf[4] = {nullptr, nullptr, nullptr, nullptr};
+    size_t cap[4] = {0, 0, 0, 0};
+
+    ~Comm() {
+        for (void* b : buf)
+            if (b) (void)hipFree(b);
+    }
+
+    // scratch slot k of at least `bytes` (grown after draining the stream that used it)
+    int scratch(int k, size_t bytes, hipStream_t s, char** out) {
+        if (cap[k] < bytes) {
+            FMI_COMM_HIP(hipStreamSynchronize(s));
+            if (buf[k]) FMI_COMM_HIP(hipFree(buf[k]));
+            buf[k] = nullptr;
+            cap[k] = 0;
+            const hipError_t e = hipMalloc(&buf[k], bytes);
+            if (e != hipSuccess) return fail(FMI_ERR_ALLOC, std::string("hipMalloc (comm scratch): ") + hipGetErrorString(e));
+            cap[k] = bytes;
+        }
+        *out = static_cast<char*>(buf[k]);
+        return FMI_OK;
+    }
+};
+
+size_t shard_elems(size_t n, int ranks) {
+    const size_t per = (n + ranks - 1) / ranks;
+    return (per + kShardAlign - 1) / kShardAlign * kShardAlign;
+}
+
+int check_common(fmi_comm_t comm, int op, int dtype) {
+    if (!comm) return fail(FMI_ERR_INVALID, "null communicator");
+    if (op < FMI_OP_SUM || op > FMI_OP_MIN) return fail(FMI_ERR_INVALID, "unknown op " + std::to_string(op));
+    if (dtype_size(dtype) == 0) return fail(FMI_ERR_INVALID, "unknown dtype " + std::to_string(dtype));
+    if (!library_stream()) return fail(FMI_ERR_NO_DEVICE, "fmi_dev_init has not been called");
+    return FMI_OK;
+}
+
+// NULL stream = the library's stream (fmi_stream_sync(NULL) then waits for the collective).
+hipStream_t resolve_stream(fmi_stream_t s) { return s ? static_cast<hipStream_t>(s) : library_stream(); }
+
+// Copy `send` (n elements) into a zero-padded staging bucket when the shard grid needs padding.
+int padded_source(Comm* c, size_t n, size_t padded, size_t esz, const void* send, hipStream_t s, const char** out) {
+    if (padded == n) {
+        *out = static_cast<const char*>(send);
+        return FMI_OK;
+    }
+    char* pad = nullptr;
+    FMI_COMM_RC(c->scratch(0, padded * esz, s, &pad));
+    FMI_COMM_HIP(hipMemcpyAsync(pad, send, n * esz, hipMemcpyDeviceToDevice, s));
+    FMI_COMM_HIP(hipMemsetAsync(pad + n * esz, 0, (padded - n) * esz, s));
+    *out = pad;
+    return FMI_OK;
+}
+
+}  // namespace
+}  // namespace fmi::dev
+
+using namespace fmi::dev;
+
+extern "C" {
+
+int fmi_comm_unique_id(int transport, void* id, size_t len) {
+    if (!id || len < FMI_COMM_ID_BYTES) return fail(FMI_ERR_INVALID, "id buffer must hold FMI_COMM_ID_BYTES");
+    std::memset(id, 0, FMI_COMM_ID_BYTES);
+    if (transport == FMI_TRANSPORT_LOCAL) {
+        const uint64_t key = (static_cast<uint64_t>(getpid()) << 32) ^ g_hub_counter.fetch_add(1);
+        std::memcpy(id, kLocalMagic, 8);
+        std::memcpy(static_cast<char*>(id) + 8, &key, 8);
+        return FMI_OK;
+    }
+    if (transport != FMI_TRANSPORT_RCCL) return fail(FMI_ERR_INVALID, "unknown transport");
+    const RcclApi* api = rccl_api();
+    if (!api) return FMI_ERR_COMM;
+    ncclUniqueId uid;
+    FMI_NCCL(api, GetUniqueId(&uid));
+    static_assert(sizeof(ncclUniqueId) == FMI_COMM_ID_BYTES, "RCCL unique id size");
+    std::memcpy(id, &uid, FMI_COMM_ID_BYTES);
+    return FMI_OK;
+}
+
+int fmi_comm_init(fmi_comm_t* comm, const void* id, int nranks, int rank) {
+    if (!comm || !id) return fail(FMI_ERR_INVALID, "null argument");
+    if (nranks < 1 || rank < 0 || rank >= nranks) return fail(FMI_ERR_INVALID, "rank out of range");
+    auto c = std::make_unique<Comm>();
+    if (std::memcmp(id, kLocalMagic, 8) == 0) {
+        uint64_t key;
+        std::memcpy(&key, static_cast<const char*>(id) + 8, 8);
+        std::shared_ptr<Hub> hub;
+        {
+            std::lock_guard<std::mutex> lk(g_hub_mu);
+            hub = g_hubs[key].lock();
+            if (!hub) {
+                hub = std::make_shared<Hub>(nranks);
+                g_hubs[key] = hub;
+            }
+        }
+        if (hub->n != nranks) return fail(FMI_ERR_INVALID, "local communicator joined with a different size");
+        c->t = std::make_unique<LocalTransport>(hub, nranks, rank);
+    } else {
+        const RcclApi* api = rccl_api();
+        if (!api) return FMI_ERR_COMM;
+        ncclUniqueId uid;
+        std::memcpy(&uid, id, FMI_COMM_ID_BYTES);
+        ncclComm_t nc = nullptr;
+        FMI_NCCL(api, CommInitRank(&nc, nranks, uid, rank));
+        c->t = std::make_unique<RcclTransport>(api, nc, nranks, rank);
+    }
+    *comm = c.release();
+    return FMI_OK;
+}
+
+int fmi_comm_destroy(fmi_comm_t comm) {
+    delete static_cast<Comm*>(comm);
+    return FMI_OK;
+}
+
+int fmi_comm_size(fmi_comm_t comm, int* nranks, int* rank) {
+    if (!comm || !nranks || !rank) return fail(FMI_ERR_INVALID, "null argument");
+    Comm* c = static_cast<Comm*>(comm);
+    *nranks = c->t->n();
+    *rank = c->t->rank();
+    return FMI_OK;
+}
+
+int fmi_comm_allreduce(fmi_comm_t comm, int op, int dtype, int alg, int path, const void* send, void* recv, size_t n,
+                       fmi_stream_t stream) {
+    FMI_COMM_RC(check_common(comm, op, dtype));
+    if (alg != FMI_ALG_ALLREDUCE && alg != FMI_ALG_REDUCE_LTR)
+        return fail(FMI_ERR_INVALID, "allreduce: alg must be ALLREDUCE or REDUCE_LTR");
+    if (path != FMI_PATH_TREE && path != FMI_PATH_RCCL) return fail(FMI_ERR_INVALID, "unknown path");
+    if (path == FMI_PATH_RCCL && alg != FMI_ALG_ALLREDUCE)
+        return fail(FMI_ERR_INVALID, "ordered (LTR) allreduce needs the tree path");
+    if (n == 0) return FMI_OK;
+    if (!send || !recv) return fail(FMI_ERR_INVALID, "null bucket");
+    Comm* c = static_cast<Comm*>(comm);
+    std::lock_guard<std::mutex> lk(c->mu);
+    hipStream_t s = resolve_stream(stream);
+    const int N = c->t->n();
+    const size_t esz = dtype_size(dtype);
+    if (N == 1) {  // reference P = 1: a copy
+        if (send != recv) FMI_COMM_HIP(hipMemcpyAsync(recv, send, n * esz, hipMemcpyDeviceToDevice, s));
+        return FMI_OK;
+    }
+    const size_t shard = shard_elems(n, N);
+    const size_t padded = shard * N;
+    const char* src = nullptr;
+    FMI_COMM_RC(padded_source(c, n, padded, esz, send, s, &src));
+    char* red = nullptr;
+    FMI_COMM_RC(c->scratch(2, shard * esz, s, &red));
+    if (path == FMI_PATH_TREE) {
+        char* staging = nullptr;
+        FMI_COMM_RC(c->scratch(1, padded * esz, s, &staging));
+        FMI_COMM_RC(c->t->all_to_all(src, staging, shard * esz, s));
+        std::vector<const void*> parts(N);
+        for (int j = 0; j < N; ++j) parts[j] = staging + j * shard * esz;
+        FMI_COMM_RC(fmi_dev_reduce_tree(op, dtype, alg, red, parts.data(), N, 0, shard, s));
+    } else {
+        FMI_COMM_RC(c->t->reduce_scatter(op, dtype, src, red, shard, s));
+    }
+    if (padded == n) return c->t->all_gather(red, static_cast<char*>(recv), shard * esz, s);
+    char* out = nullptr;
+    FMI_COMM_RC(c->scratch(3, padded * esz, s, &out));
+    FMI_COMM_RC(c->t->all_gather(red, out, shard * esz, s));
+    FMI_COMM_HIP(hipMemcpyAsync(recv, out, n * esz, hipMemcpyDeviceToDevice, s));
+    return FMI_OK;
+}
+
+int fmi_comm_reduce(fmi_comm_t comm, int op, int dtype, int alg, const void* send, void* recv, size_t n, int root,
+                    fmi_stream_t stream) {
+    FMI_COMM_RC(check_common(comm, op, dtype));
+    if (alg != FMI_ALG_REDUCE && alg != FMI_ALG_REDUCE_LTR)
+        return fail(FMI_ERR_INVALID, "reduce: alg must be REDUCE or REDUCE_LTR");
+    Comm* c = static_cast<Comm*>(comm);
+    const int N = c->t->n();
+    if (root < 0 || root >= N) return fail(FMI_ERR_INVALID, "root out of range");
+    if (n == 0) return FMI_OK;
+    if (!send || (c->t->rank() == root && !recv)) return fail(FMI_ERR_INVALID, "null bucket");
+    std::lock_guard<std::mutex> lk(c->mu);
+    hipStream_t s = resolve_stream(stream);
+    const size_t esz = dtype_size(dtype);
+    if (N == 1) {
+        if (send != recv) FMI_COMM_HIP(hipMemcpyAsync(recv, send, n * esz, hipMemcpyDeviceToDevice, s));
+        return FMI_OK;
+    }
+    const size_t shard = shard_elems(n, N);
+    const size_t padded = shard * N;
+    const char* src = nullptr;
+    FMI_COMM_RC(padded_source(c, n, padded, esz, send, s, &src));
+    char* staging = nullptr;
+    char* red = nullptr;
+    FMI_COMM_RC(c->scratch(1, padded * esz, s, &staging));
+    FMI_COMM_RC(c->scratch(2, shard * esz, s, &red));
+    FMI_COMM_RC(c->t->all_to_all(src, staging, shard * esz, s));
+    std::vector<const void*> parts(N);
+    for (int j = 0; j < N; ++j) parts[j] = staging + j * shard * esz;
+    FMI_COMM_RC(fmi_dev_reduce_tree(op, dtype, alg, red, parts.data(), N, root, shard, s));
+    const bool is_root = c->t->rank() == root;
+    if (padded == n) return c->t->gather(red, is_root ? static_cast<char*>(recv) : nullptr, shard * esz, root, s);
+    char* out = nullptr;
+    FMI_COMM_RC(c->scratch(3, padded * esz, s, &out));
+    FMI_COMM_RC(c->t->gather(red, out, shard * esz, root, s));
+    if (is_root) FMI_COMM_HIP(hipMemcpyAsync(recv, out, n * esz, hipMemcpyDeviceToDevice, s));
+    return FMI_OK;
+}
+
+int fmi_comm_scan(fmi_comm_t comm, int op, int dtype, int alg, const void* send, void* recv, size_t n,
+                  fmi_stream_t stream) {
+    FMI_COMM_RC(check_common(comm, op, dtype));
+    if (alg != FMI_ALG_SCAN && alg != FMI_ALG_SCAN_LTR) return fail(FMI_ERR_INVALID, "scan: alg must be SCAN or SCAN_LTR");
+    if (n == 0) return FMI_OK;
+    if (!send || !recv) return fail(FMI_ERR_INVALID, "null bucket");
+    Comm* c = static_cast<Comm*>(comm);
+    std::lock_guard<std::mutex> lk(c->mu);
+    hipStream_t s = resolve_stream(stream);
+    const int N = c->t->n();
+    const size_t esz = dtype_size(dtype);
+    if (N == 1) {
+        if (send != recv) FMI_COMM_HIP(hipMemcpyAsync(recv, send, n * esz, hipMemcpyDeviceToDevice, s));
+        return FMI_OK;
+    }
+    const size_t shard = shard_elems(n, N);
+    const size_t padded = shard * N;
+    const char* src = nullptr;
+    FMI_COMM_RC(padded_source(c, n, padded, esz, send, s, &src));
+    char* staging = nullptr;
+    char* prefix = nullptr;
+    FMI_COMM_RC(c->scratch(1, padded * esz, s, &staging));
+    FMI_COMM_RC(c->scratch(2, padded * esz, s, &prefix));
+    FMI_COMM_RC(c->t->all_to_all(src, staging, shard * esz, s));
+    std::vector<const void*> ins(N);
+    std::vector<void*> outs(N);
+    for (int j = 0; j < N; ++j) {
+        ins[j] = staging + j * shard * esz;
+        outs[j] = prefix + j * shard * esz;  // prefix of rank j over my shard
+    }
+    FMI_COMM_RC(fmi_dev_scan_peers(op, dtype, alg, outs.data(), ins.data(), N, shard, s));
+    // rank k gathers its prefix shard j from rank j: an all-to-all back
+    if (padded == n) return c->t->all_to_all(prefix, static_cast<char*>(recv), shard * esz, s);
+    char* out = nullptr;
+    FMI_COMM_RC(c->scratch(3, padded * esz, s, &out));
+    FMI_COMM_RC(c->t->all_to_all(prefix, out, shard * esz, s));
+    FMI_COMM_HIP(hipMemcpyAsync(recv, out, n * esz, hipMemcpyDeviceToDevice, s));
+    return FMI_OK;
+}
+
+#define FMI_COMM_PRELUDE()                                                        \
+    if (!comm) return fail(FMI_ERR_INVALID, "null communicator");                 \
+    if (!library_stream()) return fail(FMI_ERR_NO_DEVICE, "fmi_dev_init has not been called"); \
+    Comm* c = static_cast<Comm*>(comm);                                           \
+    std::lock_guard<std::mutex> lk(c->mu);                                        \
+    hipStream_t s = resolve_stream(stream);
+
+int fmi_comm_bcast(fmi_comm_t comm, void* buf, size_t bytes, int root, fmi_stream_t stream) {
+    FMI_COMM_PRELUDE();
+    if (root < 0 || root >= c->t->n()) return fail(FMI_ERR_INVALID, "root out of range");
+    return c->t->bcast(static_cast<char*>(buf), bytes, root, s);
+}
+
+int fmi_comm_gather(fmi_comm_t comm, const void* send, void* recv, size_t bytes, int root, fmi_stream_t stream) {
+    FMI_COMM_PRELUDE();
+    if (root < 0 || root >= c->t->n()) return fail(FMI_ERR_INVALID, "root out of range");
+    return c->t->gather(static_cast<const char*>(send), static_cast<char*>(recv), bytes, root, s);
+}
+
+int fmi_comm_scatter(fmi_comm_t comm, const void* send, void* recv, size_t bytes, int root, fmi_stream_t stream) {
+    FMI_COMM_PRELUDE();
+    if (root < 0 || root >= c->t->n()) return fail(FMI_ERR_INVALID, "root out of range");
+    return c->t->scatter(static_cast<const char*>(send), static_cast<char*>(recv), bytes, root, s);
+}
+
+int fmi_comm_send(fmi_comm_t comm, const void* buf, size_t bytes, int peer, fmi_stream_t stream) {
+    FMI_COMM_PRELUDE();
+    if (peer < 0 || peer >= c->t->n()) return fail(FMI_ERR_INVALID, "peer out of range");
+    return c->t->send(static_cast<const char*>(buf), bytes, peer, s);
+}
+
+int fmi_comm_recv(fmi_comm_t comm, void* buf, size_t bytes, int peer, fmi_stream_t stream) {
+    FMI_COMM_PRELUDE();
+    if (peer < 0 || peer >= c->t->n()) return fail(FMI_ERR_INVALID, "peer out of range");
+    return c->t->recv(static_cast<char*>(buf), bytes, peer, s);
+}
+
+int fmi_comm_barrier(fmi_comm_t comm, fmi_stream_t stream) {
+    FMI_COMM_PRELUDE();
+    return c->t->barrier(s);
+}
+
+}  // extern "C"

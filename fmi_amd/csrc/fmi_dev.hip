@@ -211,6 +211,8 @@ int fail(int code, const std::string& msg) {
     return code;
 }
 
+hipStream_t library_stream() { return g_state.stream; }
+
 }  // namespace fmi::dev
 
 using namespace fmi::dev;

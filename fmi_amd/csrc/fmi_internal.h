@@ -15,6 +15,9 @@ namespace fmi::dev {
 // Records a failure message for fmi_last_error() and returns `code`.
 int fail(int code, const std::string& msg);
 
+// The library's default stream (what a NULL fmi_stream_t means); nullptr before fmi_dev_init.
+hipStream_t library_stream();
+
 // Invoke f.template operator()<Op, T>() for a runtime (op, dtype); returns FMI_ERR_INVALID if unknown.
 template <class F>
 int with_op_dtype(int op, int dtype, F&& f) {

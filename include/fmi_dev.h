@@ -46,7 +46,8 @@ typedef enum {
     FMI_ERR_HIP = -2,         /* a HIP runtime call failed; message names the call */
     FMI_ERR_NO_DEVICE = -3,   /* no gfx950 device visible / fmi_dev_init not called */
     FMI_ERR_UNSUPPORTED = -4, /* combination not implemented */
-    FMI_ERR_ALLOC = -5        /* device or pinned allocation failed */
+    FMI_ERR_ALLOC = -5,       /* device or pinned allocation failed */
+    FMI_ERR_COMM = -6         /* a communicator / transport (RCCL) call failed */
 } fmi_status_t;
 
 /* ---- op / dtype / algorithm descriptors -------------------------------------------------------- */
@@ -138,6 +139,51 @@ int fmi_dev_scan_peers(int op, int dtype, int alg, void* const* outs, const void
  * This is the path a recv buffer arriving over a host channel takes (reference
  * src/comm/Direct.cpp:36-45 → PeerToPeer.cpp:119). Synchronous: returns when inout is updated. */
 int fmi_host_reduce_pair(int op, int dtype, void* inout, const void* in, size_t n);
+
+/* ---- sharded device collectives across GPUs (one process per GPU, RCCL over xGMI) ----------------
+ * The reference's collectives exchange whole buckets peer to peer over host sockets
+ * (src/comm/PeerToPeer.cpp). Between MI355X GPUs the same collectives run sharded, so every GPU's 7
+ * xGMI links carry traffic at once, with the combine done by the fused kernels above in the reference's
+ * order:
+ *   allreduce (path TREE): all-to-all of N shards -> fused P-way kernel over the N partials of this
+ *       GPU's shard (allreduce_no_order / reduce_ltr order) -> all-gather. Bit-identical to the
+ *       reference's N-peer allreduce (rank 0's operand order for float max/min ties).
+ *   allreduce (path RCCL): RCCL reduce-scatter + all-gather (RCCL's order; within (N-1)*u*sum|x|).
+ *   reduce: all-to-all -> fused kernel in reduce_no_order / reduce_ltr order for `root` -> gather.
+ *   scan:   all-to-all -> fused peer-axis scan -> all-to-all back.
+ * One rank = one peer = one GPU. Transports: FMI_TRANSPORT_RCCL (librccl, loaded on first use; with
+ * torch imported first it is torch's copy) and FMI_TRANSPORT_LOCAL (ranks are threads of ONE process
+ * sharing one device: the same schedules over device-to-device copies — used to test the multi-rank
+ * schedules on a single GPU and to serve several peers co-resident on one GPU).
+ * All calls enqueue on `stream` (NULL = library stream); results are valid after fmi_stream_sync.
+ * Buckets are device pointers; `send` is never modified; recv may alias send. */
+#define FMI_COMM_ID_BYTES 128
+typedef void* fmi_comm_t;
+typedef enum { FMI_TRANSPORT_RCCL = 0, FMI_TRANSPORT_LOCAL = 1 } fmi_transport_t;
+typedef enum { FMI_PATH_TREE = 0, FMI_PATH_RCCL = 1 } fmi_path_t;
+
+/* A fresh communicator id (FMI_COMM_ID_BYTES) made by one rank and handed to the others by any host
+ * channel (FMI: Communicator::bcast over the host channel, reference include/Communicator.h:43-47). */
+int fmi_comm_unique_id(int transport, void* id, size_t len);
+int fmi_comm_init(fmi_comm_t* comm, const void* id, int nranks, int rank);
+int fmi_comm_destroy(fmi_comm_t comm);
+int fmi_comm_size(fmi_comm_t comm, int* nranks, int* rank);
+/* alg: FMI_ALG_ALLREDUCE (commutative+associative) or FMI_ALG_REDUCE_LTR (ordered) */
+int fmi_comm_allreduce(fmi_comm_t comm, int op, int dtype, int alg, int path, const void* send, void* recv, size_t n,
+                       fmi_stream_t stream);
+/* alg: FMI_ALG_REDUCE or FMI_ALG_REDUCE_LTR; recv is used on root only (may be NULL elsewhere) */
+int fmi_comm_reduce(fmi_comm_t comm, int op, int dtype, int alg, const void* send, void* recv, size_t n, int root,
+                    fmi_stream_t stream);
+/* alg: FMI_ALG_SCAN or FMI_ALG_SCAN_LTR; rank k receives x0 (+) ... (+) xk */
+int fmi_comm_scan(fmi_comm_t comm, int op, int dtype, int alg, const void* send, void* recv, size_t n,
+                  fmi_stream_t stream);
+int fmi_comm_bcast(fmi_comm_t comm, void* buf, size_t bytes, int root, fmi_stream_t stream);
+/* recv holds nranks * bytes on root (rank order); scatter sends root's nranks * bytes */
+int fmi_comm_gather(fmi_comm_t comm, const void* send, void* recv, size_t bytes, int root, fmi_stream_t stream);
+int fmi_comm_scatter(fmi_comm_t comm, const void* send, void* recv, size_t bytes, int root, fmi_stream_t stream);
+int fmi_comm_send(fmi_comm_t comm, const void* buf, size_t bytes, int peer, fmi_stream_t stream);
+int fmi_comm_recv(fmi_comm_t comm, void* buf, size_t bytes, int peer, fmi_stream_t stream);
+int fmi_comm_barrier(fmi_comm_t comm, fmi_stream_t stream);
 
 /* ---- synthetic buckets (identical on host and device: SURVEY.md §8d generator) ------------------
  * h = splitmix64(seed ^ ((uint64)peer << 40) ^ i);  f32 = (float)((h >> 40) * 2^-24) * 2 - 1,

@@ -66,6 +66,27 @@ def test_argument_validation_is_host_side():
     assert lib.fmi_host_reduce_pair(0, 0, None, None, 0) == 0  # empty bucket is a no-op
 
 
+def test_comm_host_side_without_device():
+    """Communicator ids and LOCAL-transport joins are host logic; collectives refuse without a device."""
+    from fmi_amd.comm import Comm, Transport, unique_id
+
+    a, b = unique_id(Transport.LOCAL), unique_id(Transport.LOCAL)
+    assert len(a) == 128 and a != b and a[:8] == b"FMILOCAL"
+    c0, c1 = Comm(a, 2, 0), Comm(a, 2, 1)
+    lib = _lib.load()
+    c = ctypes.c_int(-1)
+    lib.fmi_dev_count(ctypes.byref(c))
+    if c.value == 0:
+        assert lib.fmi_comm_barrier(ctypes.c_void_p(c0.handle), None) == _lib.FMI_ERR_NO_DEVICE
+    assert lib.fmi_comm_allreduce(ctypes.c_void_p(c0.handle), 9, 0, 0, 0, None, None, 8, None) == _lib.FMI_ERR_INVALID
+    with pytest.raises(fmi_amd.FmiError):
+        Comm(a, 3, 0)  # joining a 2-rank communicator as a 3-rank one
+    with pytest.raises(fmi_amd.FmiError):
+        Comm(a, 2, 2)  # rank out of range
+    c0.destroy()
+    c1.destroy()
+
+
 def test_tuning_knobs_validate():
     fmi_amd.tune_set(fmi_amd.Tune.PAIR_UNROLL, 8)
     assert fmi_amd.tune_get(fmi_amd.Tune.PAIR_UNROLL) == 8

@@ -1,0 +1,184 @@
+"""The C-ABI communicator (fmi_comm_*) — sharded allreduce / reduce / scan across ranks — run with the
+LOCAL transport: N ranks are threads of this process on the one MI355X, exchanging through device copies.
+The schedules (shard layout, padding, all-to-all, fused kernel in the reference's order, all-gather /
+gather / all-to-all back) are exactly those the RCCL transport runs across GPUs; the result of every rank
+is compared bit-exactly with the oracle's simulation of the reference collective over the same buckets.
+"""
+import threading
+
+import numpy as np
+import pytest
+
+import fmi_amd
+from fmi_amd import Bucket, Op
+from fmi_amd.comm import Comm, Path, Transport, unique_id
+from oracle import fmi_oracle as orc
+from tests.test_gpu_parity import OPNAME, assert_bit_equal, inputs
+
+pytestmark = pytest.mark.gpu
+
+
+def run_ranks(N, body):
+    uid = unique_id(Transport.LOCAL)
+    errors = [None] * N
+    results = [None] * N
+
+    def worker(r):
+        try:
+            c = Comm(uid, N, r)
+            results[r] = body(c, r)
+            c.destroy()
+        except BaseException as e:  # noqa: BLE001 - re-raised below
+            errors[r] = e
+
+    threads = [threading.Thread(target=worker, args=(r,)) for r in range(N)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=300)
+    for e in errors:
+        if e is not None:
+            raise e
+    return results
+
+
+@pytest.mark.parametrize("N", [2, 3, 4, 5, 8])
+@pytest.mark.parametrize("n", [1, 1027, 3 * 65536 + 5])
+def test_comm_allreduce_tree_bit_exact(device, N, n):
+    for dtype, op in ((np.float32, Op.SUM), (np.int64, Op.PROD), (np.float64, Op.MAX), (np.int32, Op.MIN)):
+        xs = [inputs(dtype, n, r, seed=11) for r in range(N)]
+
+        def body(c, r):
+            s, out = Bucket.from_numpy(xs[r]), Bucket(n, dtype)
+            c.allreduce(op, s, out)
+            fmi_amd.sync()
+            return out.numpy(), s.numpy()
+
+        res = run_ranks(N, body)
+        with np.errstate(all="ignore"):
+            want, _ = orc.allreduce(xs, orc.OPS[OPNAME[op]])
+        for r in range(N):
+            # every rank receives the shard reductions computed in rank 0's operand order
+            assert_bit_equal(res[r][0], want[0], f"N={N} n={n} {op.name} rank {r}")
+            assert_bit_equal(res[r][1], xs[r], "send bucket untouched")
+
+
+@pytest.mark.parametrize("N", [2, 5, 8])
+def test_comm_allreduce_ordered(device, N):
+    n = 4099
+    xs = [inputs(np.float32, n, r, seed=3) for r in range(N)]
+
+    def body(c, r):
+        s, out = Bucket.from_numpy(xs[r]), Bucket(n, np.float32)
+        c.allreduce(Op.SUM, s, out, ordered=True)
+        fmi_amd.sync()
+        return out.numpy()
+
+    res = run_ranks(N, body)
+    want, _ = orc.allreduce(xs, orc.op_sum, commutative=False, associative=False)
+    for r in range(N):
+        assert_bit_equal(res[r], want[r], f"rank {r}")
+
+
+@pytest.mark.parametrize("N", [2, 3, 4, 7, 8])
+def test_comm_reduce_every_root(device, N):
+    n = 2053
+    for ordered in (False, True):
+        xs = [inputs(np.float32, n, r, seed=5) for r in range(N)]
+        for root in range(N):
+            def body(c, r):
+                s = Bucket.from_numpy(xs[r])
+                out = Bucket(n, np.float32) if r == root else None
+                c.reduce(Op.SUM, s, out, root, ordered=ordered)
+                fmi_amd.sync()
+                return out.numpy() if out is not None else None
+
+            res = run_ranks(N, body)
+            want, _ = orc.reduce(xs, orc.op_sum, root=root, commutative=not ordered, associative=not ordered)
+            assert_bit_equal(res[root], want, f"N={N} root {root} ordered={ordered}")
+
+
+@pytest.mark.parametrize("N", [2, 3, 5, 8])
+def test_comm_scan(device, N):
+    n = 65536 + 129
+    for ordered in (False, True):
+        for dtype, op in ((np.float32, Op.SUM), (np.int64, Op.MAX)):
+            xs = [inputs(dtype, n, r, seed=9) for r in range(N)]
+
+            def body(c, r):
+                s, out = Bucket.from_numpy(xs[r]), Bucket(n, dtype)
+                c.scan(op, s, out, ordered=ordered)
+                fmi_amd.sync()
+                return out.numpy()
+
+            res = run_ranks(N, body)
+            with np.errstate(all="ignore"):
+                want, _ = orc.scan(xs, orc.OPS[OPNAME[op]], commutative=not ordered, associative=not ordered)
+            for r in range(N):
+                assert_bit_equal(res[r], want[r], f"N={N} {op.name} ordered={ordered} rank {r}")
+
+
+def test_comm_point_to_point_and_data_movement(device):
+    N, n = 4, 1000
+
+    def body(c, r):
+        out = {}
+        b = Bucket.from_numpy(np.full(n, r, dtype=np.int64))
+        c.bcast(b, 2)
+        out["bcast"] = b.numpy()
+        mine = Bucket.from_numpy(np.arange(n, dtype=np.int64) + 1000 * r)
+        allb = Bucket(N * n, np.int64) if r == 1 else None
+        c.gather(mine, allb, 1)
+        out["gather"] = allb.numpy() if allb is not None else None
+        src = Bucket.from_numpy(np.arange(N * n, dtype=np.int64)) if r == 3 else None
+        piece = Bucket(n, np.int64)
+        c.scatter(src, piece, 3)
+        out["scatter"] = piece.numpy()
+        ring = Bucket.from_numpy(np.full(n, r, dtype=np.int64))
+        got = Bucket(n, np.int64)
+        if r % 2 == 0:
+            c.send(ring, (r + 1) % N)
+            c.recv(got, (r - 1) % N)
+        else:
+            c.recv(got, (r - 1) % N)
+            c.send(ring, (r + 1) % N)
+        out["ring"] = got.numpy()
+        c.barrier()
+        fmi_amd.sync()
+        return out
+
+    res = run_ranks(N, body)
+    for r in range(N):
+        assert np.all(res[r]["bcast"] == 2)
+        assert np.array_equal(res[r]["scatter"], np.arange(r * n, (r + 1) * n))
+        assert np.all(res[r]["ring"] == (r - 1) % N)
+    assert np.array_equal(res[1]["gather"], np.concatenate([np.arange(n) + 1000 * j for j in range(N)]))
+
+
+def test_comm_rccl_path_needs_rccl_transport(device):
+    def body(c, r):
+        s, out = Bucket(64, np.float32), Bucket(64, np.float32)
+        with pytest.raises(fmi_amd.FmiError):
+            c.allreduce(Op.SUM, s, out, path=Path.RCCL)
+        return True
+
+    assert all(run_ranks(2, body))
+
+
+def test_comm_rccl_transport_single_rank(device):
+    """RCCL transport plumbing on one GPU (world size 1): id, init, every collective degenerates to a copy."""
+    uid = unique_id(Transport.RCCL)
+    c = Comm(uid, 1, 0)
+    x = inputs(np.float32, 4099, 0)
+    s, out = Bucket.from_numpy(x), Bucket(4099, np.float32)
+    for path in (Path.TREE, Path.RCCL):
+        c.allreduce(Op.SUM, s, out, path=path)
+        fmi_amd.sync()
+        assert_bit_equal(out.numpy(), x)
+    c.scan(Op.SUM, s, out)
+    c.reduce(Op.SUM, s, out, 0)
+    c.bcast(out, 0)
+    c.barrier()
+    fmi_amd.sync()
+    assert_bit_equal(out.numpy(), x)
+    c.destroy()
