@@ -112,7 +112,7 @@ public:
     }
 
     double get_latency(Utils::peer_num producer, Utils::peer_num consumer, std::size_t size_in_bytes) override {
-        return overhead_ + producer * consumer * (static_cast<double>(size_in_bytes) / 1e6) / bandwidth_;
+        return overhead_ + producer * consumer * (static_cast<double>(size_in_bytes) / 1e6) / bandwidth_ * 1e3;  // ms
     }
     double get_price(Utils::peer_num, Utils::peer_num, std::size_t) override { return 0.; }
 

@@ -61,9 +61,10 @@ public:
         mailbox_->take(peer, peer_id, buf.buf, buf.len, timeout_);
     }
 
-    // memcpy-speed model in ms (same shape as Direct's: overhead + size / bandwidth)
+    // memcpy-speed model in ms (same shape as Direct's: overhead + size / bandwidth); every bundled channel
+    // models in ms so ChannelPolicy compares like with like
     double get_latency(Utils::peer_num producer, Utils::peer_num consumer, std::size_t size_in_bytes) override {
-        return overhead_ + producer * consumer * (static_cast<double>(size_in_bytes) / 1e6) / bandwidth_;
+        return overhead_ + producer * consumer * (static_cast<double>(size_in_bytes) / 1e6) / bandwidth_ * 1e3;
     }
     double get_price(Utils::peer_num, Utils::peer_num, std::size_t) override { return 0.; }
 

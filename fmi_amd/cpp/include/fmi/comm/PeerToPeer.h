@@ -160,7 +160,14 @@ public:
         const double P = num_peers;
         const double up = std::ceil(std::log2(P));
         const double down = std::floor(std::log2(P));
-        auto hop = [&](std::size_t bytes) { return get_latency(1, 1, bytes); };
+        // device buckets cross PCIe twice per message (D2H before the send, H2D after the receive)
+        const double stage_ms = info.on_device ? 2 * 0.02 : 0.;
+        const double stage_gb_s = 25.;
+        auto hop = [&](std::size_t bytes) {
+            double t = get_latency(1, 1, bytes);
+            if (info.on_device) t += stage_ms + 2 * static_cast<double>(bytes) / 1e9 / stage_gb_s * 1e3;
+            return t;
+        };
         auto tree_growing = [&](std::size_t bytes) {  // gather/scatter: buffers grow per round
             double t = 0.;
             for (int i = 1; i <= static_cast<int>(down); ++i) t += hop(i * bytes);

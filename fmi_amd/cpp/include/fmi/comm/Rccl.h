@@ -1,0 +1,161 @@
+// FMI::Comm::Rccl — a Channel for buckets resident in MI355X HBM, one peer per GPU, over RCCL / xGMI
+// (SURVEY.md §8f rank 2). It plugs in through the reference's own extension point,
+// Communicator::register_channel (reference include/Communicator.h:153), and competes in ChannelPolicy
+// (reference src/utils/ChannelPolicy.cpp:9-29) through its latency/price model; for device buckets it
+// beats any host-staged channel, so the policy routes them here.
+//
+// The collectives are the C-ABI's sharded schedules (fmi_comm_*): all-to-all of shards, one pass of the
+// fused kernel in the reference's order, all-gather / gather / all-to-all back — so every result has the
+// reference's bracketing (float max/min ties: rank 0's operand order on every rank).
+// Side effects mirrored from the reference: commutative allreduce and scan leave sendbuf = result
+// (reference src/comm/PeerToPeer.cpp:129,183), reduce leaves the root's sendbuf = result (:80); the
+// non-root partials of the reference's reduce are intermediate values and are not reproduced.
+#ifndef FMI_AMD_COMM_RCCL_H
+#define FMI_AMD_COMM_RCCL_H
+
+#include <array>
+#include <cmath>
+#include <memory>
+#include <stdexcept>
+#include <string>
+
+#include "Channel.h"
+
+namespace FMI::Comm {
+
+class Rccl : public Channel {
+public:
+    //! Join a communicator: peer 0 creates the id, `bootstrap` (any host channel of the same peers)
+    //! broadcasts it, every peer initialises its rank. transport: FMI_TRANSPORT_RCCL (one process per GPU)
+    //! or FMI_TRANSPORT_LOCAL (peers are threads of one process sharing one GPU).
+    static std::shared_ptr<Rccl> connect(Channel& bootstrap, Utils::peer_num peer, Utils::peer_num num_peers,
+                                         int transport = FMI_TRANSPORT_RCCL, double link_gb_s = 300.) {
+        std::array<char, FMI_COMM_ID_BYTES> id{};
+        if (peer == 0) Dev::check(fmi_comm_unique_id(transport, id.data(), id.size()), "fmi_comm_unique_id");
+        bootstrap.bcast({id.data(), id.size()}, 0);
+        fmi_comm_t comm = nullptr;
+        Dev::check(fmi_comm_init(&comm, id.data(), static_cast<int>(num_peers), static_cast<int>(peer)), "fmi_comm_init");
+        auto ch = std::shared_ptr<Rccl>(new Rccl(comm, link_gb_s));
+        ch->set_peer_id(peer);
+        ch->set_num_peers(num_peers);
+        return ch;
+    }
+
+    ~Rccl() override { finalize(); }
+
+    bool supports_host_buffers() const override { return false; }
+
+    void send(channel_data buf, Utils::peer_num dest) override {
+        device_only(buf);
+        run(fmi_comm_send(comm_, buf.buf, buf.len, static_cast<int>(dest), nullptr), "fmi_comm_send");
+    }
+    void recv(channel_data buf, Utils::peer_num src) override {
+        device_only(buf);
+        run(fmi_comm_recv(comm_, buf.buf, buf.len, static_cast<int>(src), nullptr), "fmi_comm_recv");
+    }
+    void bcast(channel_data buf, Utils::peer_num root) override {
+        device_only(buf);
+        run(fmi_comm_bcast(comm_, buf.buf, buf.len, static_cast<int>(root), nullptr), "fmi_comm_bcast");
+    }
+    void barrier() override { run(fmi_comm_barrier(comm_, nullptr), "fmi_comm_barrier"); }
+
+    void gather(channel_data sendbuf, channel_data recvbuf, Utils::peer_num root) override {
+        device_only(sendbuf);
+        run(fmi_comm_gather(comm_, sendbuf.buf, peer_id == root ? recvbuf.buf : nullptr, sendbuf.len,
+                            static_cast<int>(root), nullptr),
+            "fmi_comm_gather");
+    }
+    void scatter(channel_data sendbuf, channel_data recvbuf, Utils::peer_num root) override {
+        device_only(recvbuf);
+        run(fmi_comm_scatter(comm_, peer_id == root ? sendbuf.buf : nullptr, recvbuf.buf, recvbuf.len,
+                             static_cast<int>(root), nullptr),
+            "fmi_comm_scatter");
+    }
+
+    void reduce(channel_data sendbuf, channel_data recvbuf, Utils::peer_num root, raw_function f) override {
+        const device_op& d = device_of(f, sendbuf);
+        const int alg = ordered(f) ? FMI_ALG_REDUCE_LTR : FMI_ALG_REDUCE;
+        const bool is_root = peer_id == root;
+        run(fmi_comm_reduce(comm_, d.op, d.dtype, alg, sendbuf.buf, is_root ? recvbuf.buf : nullptr, d.count,
+                            static_cast<int>(root), nullptr),
+            "fmi_comm_reduce");
+        if (is_root && !ordered(f)) mirror(sendbuf, recvbuf);
+    }
+
+    void allreduce(channel_data sendbuf, channel_data recvbuf, raw_function f) override {
+        const device_op& d = device_of(f, sendbuf);
+        const int alg = ordered(f) ? FMI_ALG_REDUCE_LTR : FMI_ALG_ALLREDUCE;
+        run(fmi_comm_allreduce(comm_, d.op, d.dtype, alg, path_, sendbuf.buf, recvbuf.buf, d.count, nullptr),
+            "fmi_comm_allreduce");
+        if (!ordered(f)) mirror(sendbuf, recvbuf);
+    }
+
+    void scan(channel_data sendbuf, channel_data recvbuf, raw_function f) override {
+        const device_op& d = device_of(f, sendbuf);
+        const int alg = ordered(f) ? FMI_ALG_SCAN_LTR : FMI_ALG_SCAN;
+        run(fmi_comm_scan(comm_, d.op, d.dtype, alg, sendbuf.buf, recvbuf.buf, d.count, nullptr), "fmi_comm_scan");
+        if (!ordered(f)) mirror(sendbuf, recvbuf);
+    }
+
+    //! FMI_PATH_TREE (default, reference order) or FMI_PATH_RCCL (reduce-scatter, RCCL's order).
+    void set_path(int path) { path_ = path; }
+
+    void finalize() override {
+        if (comm_) (void)fmi_comm_destroy(comm_);
+        comm_ = nullptr;
+    }
+
+    // xGMI model in ms: latency + bytes over the per-GPU link bandwidth; sharded collectives move
+    // 2 (N-1)/N of the bucket per GPU (reduce-scatter + all-gather), point-to-point moves it once.
+    double get_latency(Utils::peer_num producer, Utils::peer_num consumer, std::size_t size_in_bytes) override {
+        return 0.01 + producer * consumer * (static_cast<double>(size_in_bytes) / 1e9) / link_gb_s_ * 1e3;
+    }
+    double get_price(Utils::peer_num, Utils::peer_num, std::size_t) override { return 0.; }
+    double get_operation_latency(Utils::OperationInfo info) override {
+        const double P = num_peers;
+        const double frac = P > 1 ? (P - 1) / P : 0.;
+        const std::size_t bytes = info.data_size;
+        switch (info.op) {
+            case Utils::send: return get_latency(1, 1, bytes);
+            case Utils::barrier: return 0.02;
+            case Utils::bcast:
+            case Utils::gather:
+            case Utils::scatter: return 0.01 + frac * get_latency(1, 1, bytes);
+            case Utils::reduce:
+            case Utils::allreduce:
+            case Utils::scan: return 0.02 + 2 * frac * get_latency(1, 1, bytes);
+        }
+        throw std::runtime_error("Operation not implemented");
+    }
+    double get_operation_price(Utils::OperationInfo) override { return 0.; }
+
+private:
+    Rccl(fmi_comm_t comm, double link_gb_s) : comm_(comm), link_gb_s_(link_gb_s) {}
+
+    static bool ordered(const raw_function& f) { return !(f.commutative && f.associative); }
+
+    static void device_only(const channel_data& b) {
+        if (!b.on_device && b.len) throw std::runtime_error("Rccl channel carries device buckets only");
+    }
+    static const device_op& device_of(const raw_function& f, const channel_data& b) {
+        device_only(b);
+        if (!f.device.valid())
+            throw std::runtime_error("Rccl channel needs a built-in reduction op (Function<T>(Utils::Op::...))");
+        return f.device;
+    }
+    static void run(int status, const char* what) {
+        Dev::check(status, what);
+        Dev::check(fmi_stream_sync(nullptr), "fmi_stream_sync");  // FMI collectives are blocking
+    }
+    static void mirror(const channel_data& sendbuf, const channel_data& recvbuf) {
+        if (sendbuf.buf != recvbuf.buf) Dev::copy_bytes(sendbuf.buf, true, recvbuf.buf, true, sendbuf.len);
+    }
+
+    fmi_comm_t comm_ = nullptr;
+    double link_gb_s_;
+    int path_ = FMI_PATH_TREE;
+};
+
+}  // namespace FMI::Comm
+
+#endif

@@ -6,5 +6,6 @@
 #include "comm/LocalSocket.h"
 #include "comm/Loopback.h"
 #include "comm/PeerToPeer.h"
+#include "comm/Rccl.h"
 
 #endif

@@ -27,7 +27,10 @@ public:
     virtual std::string get_channel(OperationInfo op_info) { return pick(op_info, false); }
 
     //! Same choice for an operation on device-resident buffers.
-    virtual std::string get_device_channel(OperationInfo op_info) { return pick(op_info, true); }
+    virtual std::string get_device_channel(OperationInfo op_info) {
+        op_info.on_device = true;
+        return pick(op_info, true);
+    }
 
     void set_hint(Hint hint) { hint_ = hint; }
 

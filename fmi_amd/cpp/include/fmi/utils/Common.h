@@ -27,6 +27,7 @@ struct OperationInfo {
     Operation op;
     std::size_t data_size;
     bool left_to_right = false;
+    bool on_device = false;  // extension: the buffers live in GPU memory (channel models add staging)
 };
 
 }  // namespace FMI::Utils

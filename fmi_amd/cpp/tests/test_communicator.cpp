@@ -605,6 +605,84 @@ GPU_TEST(host_offload_matches_host_path) {
     for (int p = 0; p < 4; ++p) CHECK(std::memcmp(off[p].data(), host[p].data(), n * 4) == 0);
 }
 
+// The Rccl channel over the LOCAL transport (peers = threads sharing the GPU): bootstrapped through the
+// Loopback host channel, selected by the policy for device buckets, results equal to the host path.
+GPU_TEST(rccl_channel_collectives_local_transport) {
+    Dev::init(0);
+    for (peer_num P : {2u, 3u, 4u, 8u}) {
+        const std::size_t n = 300007;
+        std::vector<std::vector<float>> host_ar(P), dev_ar(P), dev_send(P), host_sc(P), dev_sc(P);
+        std::vector<float> host_red, dev_red;
+        std::vector<std::string> picked(P);
+        with_peers(P, [&](Communicator& c, peer_num p) {
+            Data<std::vector<float>> a(synth_f32(n, 5, p)), r(n);
+            c.allreduce(a, r, Function<std::vector<float>>(Op::sum));
+            host_ar[p] = r.get();
+            Data<std::vector<float>> s(synth_f32(n, 5, p)), sr(n);
+            c.scan(s, sr, Function<std::vector<float>>(Op::sum));
+            host_sc[p] = sr.get();
+            Data<std::vector<float>> d(synth_f32(n, 5, p)), dr(n);
+            c.reduce(d, dr, 1 % P, Function<std::vector<float>>(Op::sum));
+            if (p == 1 % P) host_red = dr.get();
+        });
+        auto mailbox = std::make_shared<FMI::Comm::Mailbox>();
+        std::vector<std::thread> ts;
+        std::vector<std::string> errors(P);
+        for (peer_num p = 0; p < P; ++p)
+            ts.emplace_back([&, p] {
+                try {
+                    Communicator c(p, P, "", "rccl-test");
+                    auto loop = std::make_shared<FMI::Comm::Loopback>(mailbox, std::chrono::seconds(60));
+                    c.register_channel("Loopback", loop);
+                    c.register_channel("Rccl", FMI::Comm::Rccl::connect(*loop, p, P, FMI_TRANSPORT_LOCAL));
+                    Data<Dev::Bucket<float>> a(synth_f32(n, 5, p)), r(n);
+                    c.allreduce(a, r, Function<Dev::Bucket<float>>(Op::sum));
+                    dev_ar[p] = r.get();
+                    dev_send[p] = a.get();
+                    Data<Dev::Bucket<float>> s(synth_f32(n, 5, p)), sr(n);
+                    c.scan(s, sr, Function<Dev::Bucket<float>>(Op::sum));
+                    dev_sc[p] = sr.get();
+                    Data<Dev::Bucket<float>> d(synth_f32(n, 5, p)), dr(n);
+                    c.reduce(d, dr, 1 % P, Function<Dev::Bucket<float>>(Op::sum));
+                    if (p == 1 % P) dev_red = dr.get();
+                    Data<Dev::Bucket<int64_t>> b(std::vector<int64_t>{static_cast<int64_t>(p), 9});
+                    c.bcast(b, P - 1);
+                    if (b.get()[0] != static_cast<int64_t>(P - 1)) throw std::runtime_error("bcast over Rccl");
+                    c.barrier();
+                } catch (const std::exception& e) {
+                    errors[p] = e.what();
+                }
+            });
+        for (auto& t : ts) t.join();
+        for (peer_num p = 0; p < P; ++p) {
+            if (!errors[p].empty()) {
+                ++g_failures;
+                std::fprintf(stderr, "  peer %u threw: %s\n", p, errors[p].c_str());
+                continue;
+            }
+            CHECK(std::memcmp(host_ar[p].data(), dev_ar[p].data(), n * 4) == 0);
+            CHECK(std::memcmp(dev_send[p].data(), dev_ar[p].data(), n * 4) == 0);  // sendbuf = result
+            CHECK(std::memcmp(host_sc[p].data(), dev_sc[p].data(), n * 4) == 0);
+        }
+        CHECK(host_red.size() == n && dev_red.size() == n && std::memcmp(host_red.data(), dev_red.data(), n * 4) == 0);
+    }
+}
+
+GPU_TEST(policy_routes_device_buckets_to_rccl) {
+    Dev::init(0);
+    std::map<std::string, std::shared_ptr<FMI::Comm::Channel>> chans;
+    auto mailbox = std::make_shared<FMI::Comm::Mailbox>();
+    auto loop = std::make_shared<FMI::Comm::Loopback>(mailbox);
+    loop->set_num_peers(1);
+    chans["Loopback"] = loop;
+    chans["Rccl"] = FMI::Comm::Rccl::connect(*loop, 0, 1, FMI_TRANSPORT_LOCAL);
+    FMI::Utils::ChannelPolicy policy(chans, 1, 0.0000166667 / 8, FMI::Utils::cheap);
+    for (std::size_t bytes : {std::size_t(1) << 10, std::size_t(1) << 20, std::size_t(256) << 20}) {
+        CHECK(policy.get_device_channel({FMI::Utils::allreduce, bytes}) == "Rccl");
+        CHECK(policy.get_channel({FMI::Utils::allreduce, bytes}) == "Loopback");  // host buffers never go to Rccl
+    }
+}
+
 GPU_TEST(device_buckets_need_builtin_op) {
     Dev::init(0);
     with_peers(1, [](Communicator& c, peer_num) {
