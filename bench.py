@@ -46,6 +46,9 @@ def parse():
     ap.add_argument("--sets", type=int, default=4, help="rotating bucket sets (defeats the 256 MiB MALL)")
     ap.add_argument("--path", default="tree", choices=["tree", "rccl"],
                     help="N>1 exchange: tree = all-to-all + fused kernel (bit-exact), rccl = reduce-scatter")
+    ap.add_argument("--backend", default="fmi", choices=["fmi", "torch"],
+                    help="N>1 exchange driver: fmi = the C-ABI communicator fmi_comm_* (RCCL transport), "
+                         "torch = torch.distributed collectives + our kernels on torch's stream")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--force-dist", action="store_true",
                     help="run the N>1 code path (RCCL exchange) even at world size 1 — plumbing check only")
@@ -163,10 +166,20 @@ def main():
         parallelism = "single GPU (2 peers resident)"
         extra = {}
     else:
-        from fmi_amd.collectives import ShardedAllreduce
+        from fmi_amd.collectives import CommAllreduce, ShardedAllreduce
 
-        ar = ShardedAllreduce(dist.group.WORLD, path=args.path, force_exchange=args.force_dist)
+        ar = None
+        backend = args.backend
+        if backend == "fmi":
+            try:  # the product C-ABI communicator (fmi_comm_*, RCCL transport)
+                ar = CommAllreduce(dist.group.WORLD, path=args.path)
+            except Exception as e:  # setup only: every rank fails alike, before any timed work
+                print(f"fmi_comm setup failed ({e}); using the torch.distributed exchange", file=sys.stderr)
+                backend = "torch"
+        if ar is None:
+            ar = ShardedAllreduce(dist.group.WORLD, path=args.path, force_exchange=args.force_dist)
         step_ms, kernel_ms, extra = ar.bench(n, steps=args.steps, warmup=args.warmup, sets=args.sets)
+        extra["backend"] = backend
         dominant = "pair_tile"  # our local round; the exchange itself is RCCL's (config.algbw/busbw)
         algo_bytes = extra.pop("kernel_algo_bytes")
         workload = (f"C4-shaped: {2 * world}-peer float32 sum-allreduce of 256 MiB buckets, 2 peers per GPU, "

@@ -148,6 +148,9 @@ class ShardedAllreduce:
 
     # ------------------------------------------------------------------------------------------------
     def bench(self, n: int, steps: int, warmup: int, sets: int = 2, peers_per_gpu: int = 2):
+        return self._bench(n, steps, warmup, sets, peers_per_gpu)
+
+    def _bench(self, n: int, steps: int, warmup: int, sets: int = 2, peers_per_gpu: int = 2):
         """Timed loop for bench.py: returns (ms_per_step max over ranks, per-step local-kernel ms, extras).
 
         Exactly `steps` steps are timed, bracketed by barrier + device sync on both sides; the step time
@@ -201,6 +204,75 @@ class ShardedAllreduce:
             "kernel_algo_bytes": 3 * n * 4,
             "exchange": self.path,
             "shard_elems": self.shard_elems(n),
+            "algbw_GiB_s": round((n * 4 / 2 ** 30) / (step_ms * 1e-3), 2),
+            "busbw_GiB_s": round((n * 4 / 2 ** 30) / (step_ms * 1e-3) * 2 * (self.world - 1) / self.world, 2),
+        }
+        return step_ms, kernel_ms, extra
+
+
+class CommAllreduce:
+    """The same 2-peers-per-GPU sharded allreduce through the product C-ABI (fmi_comm_*, RCCL transport):
+    pairwise kernel for the local round, then fmi_comm_allreduce (all-to-all of shards + fused kernel in
+    the reference's order + all-gather, or RCCL reduce-scatter + all-gather) — everything on the
+    library's stream. torch.distributed only bootstraps: it broadcasts the 128-byte communicator id and
+    provides the bracketing barriers of the timed region."""
+
+    def __init__(self, group=None, path: str = "tree"):
+        from .comm import Comm, Path, Transport, unique_id
+
+        self.group = group if group is not None else dist.group.WORLD
+        self.world = dist.get_world_size(self.group)
+        self.rank = dist.get_rank(self.group)
+        self.path = path
+        self._path = Path.TREE if path == "tree" else Path.RCCL
+        _lib.load()
+        _lib.call("fmi_dev_init", torch.cuda.current_device())
+        box = [unique_id(Transport.RCCL) if self.rank == 0 else None]
+        dist.broadcast_object_list(box, src=0, group=self.group)
+        self.comm = Comm(box[0], self.world, self.rank)
+
+    def bench(self, n: int, steps: int, warmup: int, sets: int = 2, peers_per_gpu: int = 2):
+        import time
+
+        import numpy as np
+
+        from . import device as fdev
+
+        bufs = [[fdev.Bucket(n, np.float32).fill_synthetic(42 + s, peers_per_gpu * self.rank + j)
+                 for j in range(peers_per_gpu)] for s in range(sets)]
+        out = fdev.Bucket(n, np.float32)
+
+        def step(k, ev=None):
+            pair = bufs[k % sets]
+            if ev:
+                ev[0].record()
+            for b in pair[1:]:
+                fdev.reduce_pair(Op.SUM, pair[0], b)
+            if ev:
+                ev[1].record()
+            self.comm.allreduce(Op.SUM, pair[0], out, path=self._path)
+
+        for k in range(warmup):
+            step(k)
+        fdev.sync()
+        evs = [(fdev.Event(), fdev.Event()) for _ in range(steps)]
+        dist.barrier(group=self.group)
+        fdev.sync()
+        t0 = time.perf_counter()
+        for k in range(steps):
+            step(k, evs[k])
+        fdev.sync()
+        dist.barrier(group=self.group)
+        t1 = time.perf_counter()
+        local = torch.tensor([(t1 - t0) * 1e3 / steps], dtype=torch.float64, device=torch.cuda.current_device())
+        dist.all_reduce(local, op=dist.ReduceOp.MAX, group=self.group)
+        step_ms = float(local.item())
+        kernel_ms = [a.elapsed_ms(b) for a, b in evs]
+        per = -(-n // self.world)
+        extra = {
+            "kernel_algo_bytes": 3 * n * 4,
+            "exchange": f"fmi_comm/{self.path}",
+            "shard_elems": -(-per // SHARD_ALIGN) * SHARD_ALIGN,
             "algbw_GiB_s": round((n * 4 / 2 ** 30) / (step_ms * 1e-3), 2),
             "busbw_GiB_s": round((n * 4 / 2 ** 30) / (step_ms * 1e-3) * 2 * (self.world - 1) / self.world, 2),
         }
