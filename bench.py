@@ -148,23 +148,35 @@ def main():
         for k in range(args.warmup):
             step(k)
         fmi_amd.sync()
-        starts = [Event() for _ in range(args.steps)]
-        stops = [Event() for _ in range(args.steps)]
+        # Timed region: exactly K back-to-back launches on the library stream, bracketed by device syncs;
+        # two HIP events on that stream bracket them (no markers between launches).
+        ev0, ev1 = Event(), Event()
         t0 = time.perf_counter()
+        ev0.record()
         for k in range(args.steps):
-            starts[k].record()
             step(k)
-            stops[k].record()
+        ev1.record()
         fmi_amd.sync()
         t1 = time.perf_counter()
-        kernel_ms = [starts[k].elapsed_ms(stops[k]) for k in range(args.steps)]
-        wall_ms = (t1 - t0) * 1e3 / args.steps
-        step_ms = wall_ms
+        step_ms = (t1 - t0) * 1e3 / args.steps
+        # mean launch duration over the timed region (includes the ~1-2 us dispatch gaps between launches)
+        kernel_ms = [ev0.elapsed_ms(ev1) / args.steps]
+        # diagnostic, untimed: per-launch event pairs give the launch duration without the gaps
+        probe = min(args.steps, 32)
+        pairs = [(Event(), Event()) for _ in range(probe)]
+        for k in range(probe):
+            pairs[k][0].record()
+            step(k)
+            pairs[k][1].record()
+        fmi_amd.sync()
+        isolated_us = 1e3 * sum(a.elapsed_ms(b) for a, b in pairs) / probe
         dominant = "pair_tile"
         algo_bytes = 3 * nbytes
         workload = "C2: 1-GPU pairwise float32 sum-reduce of two 256 MiB device-resident peer buckets"
         parallelism = "single GPU (2 peers resident)"
         extra = {}
+        roofline_extra = {"kernel_avg_us_isolated": round(isolated_us, 2),
+                          "kernel_avg_source": "HIP events bracketing the K timed launches on the library stream"}
     else:
         from fmi_amd.collectives import CommAllreduce, ShardedAllreduce
 
@@ -180,6 +192,7 @@ def main():
             ar = ShardedAllreduce(dist.group.WORLD, path=args.path, force_exchange=args.force_dist)
         step_ms, kernel_ms, extra = ar.bench(n, steps=args.steps, warmup=args.warmup, sets=args.sets)
         extra["backend"] = backend
+        roofline_extra = {"kernel_avg_source": "HIP event pair around the local pairwise round of each step"}
         dominant = "pair_tile"  # our local round; the exchange itself is RCCL's (config.algbw/busbw)
         algo_bytes = extra.pop("kernel_algo_bytes")
         workload = (f"C4-shaped: {2 * world}-peer float32 sum-allreduce of 256 MiB buckets, 2 peers per GPU, "
@@ -213,6 +226,7 @@ def main():
                      "traffic_source": traffic_src},
     }
     line["config"].update(extra)
+    line["roofline"].update(roofline_extra)
     if rank == 0 and not use_dist and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args)
     if rank == 0:

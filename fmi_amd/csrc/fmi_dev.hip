@@ -74,7 +74,7 @@ bool host_mapped(void* p, void** dev) {
 // ----------------------------------------------------------------------------------------------------
 // Pairwise launch policy.
 // ----------------------------------------------------------------------------------------------------
-template <class Op, class T, bool NT>
+template <class Op, class T, int NT>
 int launch_pair_vec(T* out, const T* a, const T* b, size_t n, hipStream_t s) {
     const long long variant = g_tune[FMI_TUNE_PAIR_VARIANT].load();
     const long long unroll = g_tune[FMI_TUNE_PAIR_UNROLL].load();
@@ -115,8 +115,12 @@ int launch_combine(int op, int dtype, void* out, const void* a, const void* b, s
         const T* x = static_cast<const T*>(a);
         const T* y = static_cast<const T*>(b);
         if (aligned16(o) && aligned16(x) && aligned16(y)) {
-            if (g_tune[FMI_TUNE_PAIR_VARIANT].load() == 2) return launch_pair_vec<Op, T, true>(o, x, y, n, s);
-            return launch_pair_vec<Op, T, false>(o, x, y, n, s);
+            switch (g_tune[FMI_TUNE_PAIR_VARIANT].load()) {
+                case 2: return launch_pair_vec<Op, T, 3>(o, x, y, n, s);  // nt loads + nt stores
+                case 3: return launch_pair_vec<Op, T, 1>(o, x, y, n, s);  // nt loads only
+                case 4: return launch_pair_vec<Op, T, 2>(o, x, y, n, s);  // nt stores only
+                default: return launch_pair_vec<Op, T, 0>(o, x, y, n, s);
+            }
         }
         const unsigned grid = static_cast<unsigned>(std::min<size_t>(grid_for(n, 256), 65536));
         pair_scalar<Op, T><<<grid, 256, 0, s>>>(o, x, y, n);
@@ -573,7 +577,7 @@ int fmi_schedule_expr(int alg, int P, int rank, char* buf, size_t len) {
 int fmi_tune_set(int key, long long value) {
     switch (key) {
         case FMI_TUNE_PAIR_VARIANT:
-            if (value < 0 || value > 2) return fail(FMI_ERR_INVALID, "variant must be 0, 1 or 2");
+            if (value < 0 || value > 4) return fail(FMI_ERR_INVALID, "variant must be in [0, 4]");
             break;
         case FMI_TUNE_PAIR_UNROLL:
             if (value != 1 && value != 2 && value != 4 && value != 8) return fail(FMI_ERR_INVALID, "unroll must be 1, 2, 4 or 8");

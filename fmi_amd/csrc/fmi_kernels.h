@@ -115,9 +115,12 @@ __device__ __forceinline__ Lanes<T, W> combine(const Lanes<T, W>& a, const Lanes
 // b*U*B + u*B + t (u < U), so each of the U wave-instructions is one contiguous 1-KiB access and each
 // thread keeps 2U independent 16-B loads in flight before its first add.
 // ---------------------------------------------------------------------------------------------------
-template <class Op, class T, int U, bool NT>
+// NT: cache policy bitmask — bit 0 nontemporal loads, bit 1 nontemporal stores.
+template <class Op, class T, int U, int NT>
 __device__ __forceinline__ void pair_tile_body(T* out, const T* a, const T* b, size_t nvec, size_t tile) {
     constexpr int W = kVecLanes<T>;
+    constexpr bool NTL = (NT & 1) != 0;
+    constexpr bool NTS = (NT & 2) != 0;
     using L = Lanes<T, W>;
     const size_t B = blockDim.x;
     const size_t base = tile * U * B + threadIdx.x;
@@ -125,24 +128,24 @@ __device__ __forceinline__ void pair_tile_body(T* out, const T* a, const T* b, s
     if (tile * U * B + U * B <= nvec) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            va[u] = load_lanes<NT, T, W>(a + (base + u * B) * W);
-            vb[u] = load_lanes<NT, T, W>(b + (base + u * B) * W);
+            va[u] = load_lanes<NTL, T, W>(a + (base + u * B) * W);
+            vb[u] = load_lanes<NTL, T, W>(b + (base + u * B) * W);
         }
 #pragma unroll
-        for (int u = 0; u < U; ++u) store_lanes<NT, T, W>(out + (base + u * B) * W, combine<Op, T, W>(va[u], vb[u]));
+        for (int u = 0; u < U; ++u) store_lanes<NTS, T, W>(out + (base + u * B) * W, combine<Op, T, W>(va[u], vb[u]));
     } else {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const size_t i = base + u * B;
             if (i < nvec) {
-                va[u] = load_lanes<NT, T, W>(a + i * W);
-                vb[u] = load_lanes<NT, T, W>(b + i * W);
+                va[u] = load_lanes<NTL, T, W>(a + i * W);
+                vb[u] = load_lanes<NTL, T, W>(b + i * W);
             }
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const size_t i = base + u * B;
-            if (i < nvec) store_lanes<NT, T, W>(out + i * W, combine<Op, T, W>(va[u], vb[u]));
+            if (i < nvec) store_lanes<NTS, T, W>(out + i * W, combine<Op, T, W>(va[u], vb[u]));
         }
     }
 }
@@ -158,7 +161,7 @@ __device__ __forceinline__ void pair_tail(T* out, const T* a, const T* b, size_t
 }
 
 // One-shot grid: one tile per workgroup. Pointers must be 16-B aligned.
-template <class Op, class T, int U, bool NT>
+template <class Op, class T, int U, int NT>
 __global__ void __launch_bounds__(1024) pair_tile(T* out, const T* a, const T* b, size_t n) {
     const size_t nvec = n / kVecLanes<T>;
     pair_tile_body<Op, T, U, NT>(out, a, b, nvec, blockIdx.x);
@@ -166,7 +169,7 @@ __global__ void __launch_bounds__(1024) pair_tile(T* out, const T* a, const T* b
 }
 
 // Grid-stride: a fixed grid (k workgroups per CU) walks the tiles. Pointers must be 16-B aligned.
-template <class Op, class T, int U, bool NT>
+template <class Op, class T, int U, int NT>
 __global__ void __launch_bounds__(1024) pair_stride(T* out, const T* a, const T* b, size_t n) {
     const size_t nvec = n / kVecLanes<T>;
     const size_t ntiles = (nvec + static_cast<size_t>(U) * blockDim.x - 1) / (static_cast<size_t>(U) * blockDim.x);

@@ -198,7 +198,8 @@ int fmi_schedule_expr(int alg, int P, int rank, char* buf, size_t len);
 
 /* ---- tuning knobs (performance only, never semantics) ------------------------------------------ */
 typedef enum {
-    FMI_TUNE_PAIR_VARIANT = 0, /* 0 = one-shot tiles, 1 = grid-stride, 2 = nontemporal tiles (default) */
+    FMI_TUNE_PAIR_VARIANT = 0, /* 0 = one-shot tiles, 1 = grid-stride, 2 = nontemporal tiles (default),
+                                  3 = tiles with nontemporal loads only, 4 = nontemporal stores only */
     FMI_TUNE_PAIR_UNROLL = 1,  /* 16-B vectors per thread per operand: 1, 2, 4, 8 */
     FMI_TUNE_BLOCK = 2,        /* threads per workgroup: 256, 512, 1024 */
     FMI_TUNE_GRID_PER_CU = 3,  /* workgroups per CU for the grid-stride variant */

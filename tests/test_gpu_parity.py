@@ -98,7 +98,7 @@ def test_reduce_pair_inplace_alias(device):
         assert_bit_equal(da.numpy(), a + a)
 
 
-@pytest.mark.parametrize("variant,unroll,block", [(v, u, b) for v in (0, 1, 2) for u in (1, 2, 4, 8)
+@pytest.mark.parametrize("variant,unroll,block", [(v, u, b) for v in (0, 1, 2, 3, 4) for u in (1, 2, 4, 8)
                                                   for b in (256, 1024)])
 def test_reduce_pair_every_launch_variant(device, variant, unroll, block):
     n = (1 << 20) + 3

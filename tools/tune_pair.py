@@ -28,7 +28,7 @@ def main():
     n = args.mib * (1 << 20) // np.dtype(dt).itemsize
     sets = [(Bucket(n, dt).fill_synthetic(42 + s, 0), Bucket(n, dt).fill_synthetic(42 + s, 1)) for s in range(4)]
     variants = []
-    for v, u, b in itertools.product((0, 2), (1, 2, 4, 8), (256, 512, 1024)):
+    for v, u, b in itertools.product((0, 2, 3, 4), (1, 2, 4, 8), (256, 512, 1024)):
         variants.append(dict(variant=v, unroll=u, block=b, grid_per_cu=0))
     for u, b, g in itertools.product((2, 4, 8), (256, 512), (2, 4, 8, 16)):
         variants.append(dict(variant=1, unroll=u, block=b, grid_per_cu=g))
