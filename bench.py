@@ -50,6 +50,7 @@ def parse():
                     help="N>1 exchange driver: fmi = the C-ABI communicator fmi_comm_* (RCCL transport), "
                          "torch = torch.distributed collectives + our kernels on torch's stream")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-diagnostics", action="store_true", help="skip the untimed N>1 phase breakdown")
     ap.add_argument("--force-dist", action="store_true",
                     help="run the N>1 code path (RCCL exchange) even at world size 1 — plumbing check only")
     ap.add_argument("--cpu-reps", type=int, default=7)
@@ -192,6 +193,26 @@ def main():
             ar = ShardedAllreduce(dist.group.WORLD, path=args.path, force_exchange=args.force_dist)
         step_ms, kernel_ms, extra = ar.bench(n, steps=args.steps, warmup=args.warmup, sets=args.sets)
         extra["backend"] = backend
+        if not args.no_diagnostics:
+            # untimed diagnostics for the next optimisation round: the other exchange path's step time and
+            # the per-phase breakdown of the sharded allreduce (each max over ranks)
+            from fmi_amd.collectives import phase_breakdown
+
+            other = "rccl" if args.path == "tree" else "tree"
+            if isinstance(ar, CommAllreduce):
+                from fmi_amd.comm import Path
+
+                saved = ar._path
+                ar._path = Path.RCCL if other == "rccl" else Path.TREE
+                alt_ms, _, _ = ar.bench(n, steps=max(10, args.steps // 4), warmup=3, sets=min(2, args.sets))
+                ar._path = saved
+            else:
+                saved = ar.path
+                ar.path = other
+                alt_ms, _, _ = ar.bench(n, steps=max(10, args.steps // 4), warmup=3, sets=min(2, args.sets))
+                ar.path = saved
+            extra["diagnostics"] = {f"ms_per_step_path_{other}": round(alt_ms, 5),
+                                    "phase_ms": phase_breakdown(n, dist.group.WORLD)}
         roofline_extra = {"kernel_avg_source": "HIP event pair around the local pairwise round of each step"}
         dominant = "pair_tile"  # our local round; the exchange itself is RCCL's (config.algbw/busbw)
         algo_bytes = extra.pop("kernel_algo_bytes")

@@ -277,3 +277,48 @@ class CommAllreduce:
             "busbw_GiB_s": round((n * 4 / 2 ** 30) / (step_ms * 1e-3) * 2 * (self.world - 1) / self.world, 2),
         }
         return step_ms, kernel_ms, extra
+
+
+def phase_breakdown(n: int, group=None, iters: int = 5) -> dict:
+    """Untimed diagnostic for bench.py at N > 1: mean duration (ms, max over ranks) of each phase of the
+    sharded allreduce of an n-element f32 bucket, measured with events on torch's stream — the local
+    pairwise round, the all-to-all, the fused shard kernel, the all-gather, and RCCL's reduce-scatter
+    (the alternative to all-to-all + kernel)."""
+    group = group if group is not None else dist.group.WORLD
+    world = dist.get_world_size(group)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    eng = HipEngine(dev.index)
+    per = -(-n // world)
+    shard = -(-per // SHARD_ALIGN) * SHARD_ALIGN
+    padded = shard * world
+    a = torch.empty(padded, dtype=torch.float32, device=dev)
+    b = torch.empty(padded, dtype=torch.float32, device=dev)
+    eng.fill_synthetic(a, 7, 0)
+    eng.fill_synthetic(b, 7, 1)
+    staging = torch.empty(padded, dtype=torch.float32, device=dev)
+    red = torch.empty(shard, dtype=torch.float32, device=dev)
+    out = torch.empty(padded, dtype=torch.float32, device=dev)
+    parts = [staging[j * shard:(j + 1) * shard] for j in range(world)]
+
+    phases = {
+        "local_pair": lambda: eng.reduce_pair(Op.SUM, a, b),
+        "all_to_all": lambda: dist.all_to_all_single(staging, a, group=group),
+        "shard_tree_kernel": lambda: eng.reduce_tree(Op.SUM, Alg.ALLREDUCE, red, parts, rank=0),
+        "all_gather": lambda: dist.all_gather_into_tensor(out, red, group=group),
+        "reduce_scatter": lambda: dist.reduce_scatter_tensor(red, a, group=group),
+    }
+    result = {}
+    for name, fn in phases.items():
+        fn()
+        torch.cuda.synchronize()
+        dist.barrier(group=group)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(iters):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        t = torch.tensor([e0.elapsed_time(e1) / iters], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+        result[name] = round(float(t.item()), 4)
+    return result
