@@ -81,10 +81,14 @@ def splitmix64(x: np.ndarray) -> np.ndarray:
 
 def synthetic(dtype, n: int, seed: int, peer: int, start: int = 0) -> np.ndarray:
     """Counter-based bucket: element i of peer `peer` (identical to fmi_dev_fill_synthetic)."""
+    return synthetic_at(dtype, np.arange(start, start + n, dtype=np.uint64), seed, peer)
+
+
+def synthetic_at(dtype, idx: np.ndarray, seed: int, peer: int) -> np.ndarray:
+    """The synthetic bucket's elements at arbitrary indices (sampled checks of full-size buckets)."""
     dtype = np.dtype(dtype)
     key = np.uint64((seed ^ (peer << 40)) & 0xFFFFFFFFFFFFFFFF)
-    i = np.arange(start, start + n, dtype=np.uint64)
-    h = splitmix64(key ^ i)
+    h = splitmix64(key ^ np.asarray(idx, dtype=np.uint64))
     if dtype == np.float32:
         u = (h >> np.uint64(40)).astype(np.float32) * np.float32(2.0 ** -24)
         return u * np.float32(2.0) - np.float32(1.0)

@@ -182,3 +182,35 @@ def test_comm_rccl_transport_single_rank(device):
     fmi_amd.sync()
     assert_bit_equal(out.numpy(), x)
     c.destroy()
+
+
+def test_c4_8peer_1gib_allreduce_full_size(device):
+    """BASELINE config C4 at full size: 8 peers x 1 GiB f32, sharded allreduce (LOCAL transport on one
+    GPU; the RCCL transport runs the same schedule across 8 GPUs). Every rank's 1 GiB result must equal,
+    bit for bit, the single-pass fused kernel over the same 8 buckets in allreduce_no_order order, and
+    the oracle's simulation of the reference collective on 2^16 sampled indices."""
+    from fmi_amd import Alg
+
+    N, n = 8, (1 << 30) // 4
+    ins = [Bucket(n, np.float32).fill_synthetic(42, r) for r in range(N)]
+    ref = Bucket(n, np.float32)
+    fmi_amd.reduce_tree(Op.SUM, Alg.ALLREDUCE, ref, ins)
+    fmi_amd.sync()
+    want_full = ref.numpy()
+    ref.free()
+
+    def body(c, r):
+        out = Bucket(n, np.float32)
+        c.allreduce(Op.SUM, ins[r], out)
+        fmi_amd.sync()
+        got = out.numpy()
+        out.free()
+        return bool(np.array_equal(got.view(np.uint32), want_full.view(np.uint32)))
+
+    assert all(run_ranks(N, body))
+    idx = np.sort(np.random.default_rng(0).choice(n, size=1 << 16, replace=False)).astype(np.uint64)
+    xs = [orc.synthetic_at(np.float32, idx, 42, r) for r in range(N)]
+    want, _ = orc.allreduce(xs, orc.op_sum)
+    assert_bit_equal(want_full[idx.astype(np.int64)], want[0], "sampled oracle check")
+    for b in ins:
+        b.free()
