@@ -19,6 +19,7 @@
 
 #include <atomic>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <functional>
@@ -64,6 +65,8 @@ struct RcclApi {
     ncclResult_t (*ReduceScatter)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t);
     ncclResult_t (*Broadcast)(const void*, void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t);
     ncclResult_t (*AllReduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t);
+    // RCCL's native all-to-all (optional symbol; grouped send/recv otherwise)
+    ncclResult_t (*AllToAll)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t);
 };
 
 const RcclApi* rccl_api() {
@@ -97,6 +100,8 @@ const RcclApi* rccl_api() {
         FMI_RCCL_SYM(Broadcast)
         FMI_RCCL_SYM(AllReduce)
 #undef FMI_RCCL_SYM
+        api.AllToAll = reinterpret_cast<decltype(api.AllToAll)>(dlsym(h, "ncclAllToAll"));
+        if (const char* g = std::getenv("FMI_A2A_GROUPED"); g && g[0] == '1') api.AllToAll = nullptr;
         ok = true;
     });
     if (!ok) {
@@ -168,6 +173,10 @@ public:
     ~RcclTransport() override { (void)api_->CommDestroy(comm_); }
 
     int all_to_all(const char* send, char* recv, size_t bytes, hipStream_t s) override {
+        if (api_->AllToAll) {
+            FMI_NCCL(api_, AllToAll(send, recv, bytes, ncclUint8, comm_, s));
+            return FMI_OK;
+        }
         FMI_NCCL(api_, GroupStart());
         for (int j = 0; j < n_; ++j) {
             FMI_NCCL(api_, Send(send + j * bytes, bytes, ncclUint8, j, comm_, s));
