@@ -213,6 +213,12 @@ def main():
                 ar.path = saved
             extra["diagnostics"] = {f"ms_per_step_path_{other}": round(alt_ms, 5),
                                     "phase_ms": phase_breakdown(n, dist.group.WORLD)}
+            if isinstance(ar, CommAllreduce):
+                # config C5: 1 GiB host (pinned) bucket per rank, H2D + allreduce + D2H pipelined
+                try:
+                    extra["diagnostics"]["c5_host_allreduce_1GiB"] = ar.host_bench(GIB // 4)
+                except Exception as e:  # diagnostic only; never fails the bench line
+                    extra["diagnostics"]["c5_host_allreduce_1GiB"] = f"failed: {e}"
         roofline_extra = {"kernel_avg_source": "HIP event pair around the local pairwise round of each step"}
         dominant = "pair_tile"  # our local round; the exchange itself is RCCL's (config.algbw/busbw)
         algo_bytes = extra.pop("kernel_algo_bytes")

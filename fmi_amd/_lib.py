@@ -80,6 +80,7 @@ SIGNATURES = {
     "fmi_comm_destroy": (_i, [_vp]),
     "fmi_comm_size": (_i, [_vp, _c.POINTER(_i), _c.POINTER(_i)]),
     "fmi_comm_allreduce": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _sz, _vp]),
+    "fmi_comm_allreduce_host": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _sz, _sz]),
     "fmi_comm_reduce": (_i, [_vp, _i, _i, _i, _vp, _vp, _sz, _i, _vp]),
     "fmi_comm_scan": (_i, [_vp, _i, _i, _i, _vp, _vp, _sz, _vp]),
     "fmi_comm_bcast": (_i, [_vp, _vp, _sz, _i, _vp]),

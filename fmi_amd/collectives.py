@@ -278,6 +278,40 @@ class CommAllreduce:
         }
         return step_ms, kernel_ms, extra
 
+    def host_bench(self, n: int, iters: int = 3, chunk: int = 64 << 18) -> dict:
+        """Config C5 (untimed diagnostic): fmi_comm_allreduce_host of an n-element f32 bucket in page-locked
+        host memory on every rank — H2D, sharded allreduce and D2H pipelined in `chunk`-element pieces.
+        Returns the median wall time (max over ranks) and the per-rank host-bucket rate. 64 MiB chunks: with
+        torch's bundled HIP runtime, 16 MiB chunks measured 2x slower (49 vs 23.4 ms per GiB round trip)."""
+        import statistics
+        import time
+
+        import numpy as np
+
+        from .device import PinnedArray
+
+        send, recv = PinnedArray(n, np.float32), PinnedArray(n, np.float32)
+        try:
+            send.array[:] = np.float32(self.rank + 1)
+            times = []
+            for k in range(iters + 1):
+                dist.barrier(group=self.group)
+                t0 = time.perf_counter()
+                self.comm.allreduce_host(Op.SUM, send.array, recv.array, path=self._path, chunk=chunk)
+                dist.barrier(group=self.group)
+                if k:
+                    times.append(time.perf_counter() - t0)
+            local = torch.tensor([statistics.median(times) * 1e3], dtype=torch.float64,
+                                 device=torch.cuda.current_device())
+            dist.all_reduce(local, op=dist.ReduceOp.MAX, group=self.group)
+            ms = float(local.item())
+            ok = bool(np.all(recv.array == np.float32(self.world * (self.world + 1) // 2)))
+        finally:
+            send.free()
+            recv.free()
+        return {"bucket_mib": n * 4 // (1 << 20), "chunk_mib": chunk * 4 / (1 << 20), "ms": round(ms, 3),
+                "per_rank_GiB_s": round(n * 4 / 2 ** 30 / (ms * 1e-3), 2), "result_ok": ok}
+
 
 def phase_breakdown(n: int, group=None, iters: int = 5) -> dict:
     """Untimed diagnostic for bench.py at N > 1: mean duration (ms, max over ranks) of each phase of the

@@ -12,7 +12,9 @@ import enum
 from typing import Optional
 
 from . import _lib
-from .device import Alg, Bucket, Op, _sptr
+import numpy as np
+
+from .device import Alg, Bucket, Op, _sptr, dtype_of
 
 ID_BYTES = 128
 
@@ -67,6 +69,19 @@ class Comm:
         alg = Alg.REDUCE_LTR if ordered else Alg.ALLREDUCE
         _lib.call("fmi_comm_allreduce", self.handle, int(op), int(send.dtype), int(alg), int(path), _p(send), _p(recv),
                   send.n, _sptr(stream))
+
+    def allreduce_host(self, op: Op, send: np.ndarray, recv: np.ndarray, ordered: bool = False,
+                       path: Path = Path.TREE, chunk: int = 0) -> None:
+        """Allreduce of HOST arrays (channel recv buffers, config C5), streamed through the GPU in
+        `chunk`-element pieces (0 = FMI_TUNE_HOST_CHUNK). Page-locked arrays (PinnedArray.array) take the
+        DMA path. Blocking: `recv` holds the result on return."""
+        if send.dtype != recv.dtype or send.size != recv.size:
+            raise ValueError("allreduce_host: arrays must share dtype and size")
+        if not (send.flags.c_contiguous and recv.flags.c_contiguous):
+            raise ValueError("allreduce_host: arrays must be contiguous")
+        alg = Alg.REDUCE_LTR if ordered else Alg.ALLREDUCE
+        _lib.call("fmi_comm_allreduce_host", self.handle, int(op), int(dtype_of(send)), int(alg), int(path),
+                  send.ctypes.data, recv.ctypes.data, send.size, int(chunk))
 
     def reduce(self, op: Op, send: Bucket, recv: Optional[Bucket], root: int, ordered: bool = False,
                stream=None) -> None:

@@ -22,6 +22,7 @@
 #include <memory>
 #include <stdexcept>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "comm/Channel.h"
@@ -104,8 +105,9 @@ public:
         if (peer_id == root && sendbuf.size_in_bytes() != recvbuf.size_in_bytes())
             throw std::runtime_error("Dimensions of send and receive data must match");
         const bool ltr = !(f.commutative && f.associative);
-        auto ch = channel_for({Utils::reduce, sendbuf.size_in_bytes(), ltr}, on_device(sendbuf));
-        ch->reduce(view(sendbuf), view(recvbuf), root, convert_to_raw_function(f, sendbuf.size_in_bytes()));
+        raw_function raw = convert_to_raw_function(f, sendbuf.size_in_bytes());
+        auto ch = channel_for({Utils::reduce, sendbuf.size_in_bytes(), ltr, false, !raw.device.valid()}, on_device(sendbuf));
+        ch->reduce(view(sendbuf), view(recvbuf), root, std::move(raw));
     }
 
     template <typename T>
@@ -113,8 +115,10 @@ public:
         if (sendbuf.size_in_bytes() != recvbuf.size_in_bytes())
             throw std::runtime_error("Dimensions of send and receive data must match");
         const bool ltr = !(f.commutative && f.associative);
-        auto ch = channel_for({Utils::allreduce, sendbuf.size_in_bytes(), ltr}, on_device(sendbuf));
-        ch->allreduce(view(sendbuf), view(recvbuf), convert_to_raw_function(f, sendbuf.size_in_bytes()));
+        raw_function raw = convert_to_raw_function(f, sendbuf.size_in_bytes());
+        auto ch = channel_for({Utils::allreduce, sendbuf.size_in_bytes(), ltr, false, !raw.device.valid()},
+                              on_device(sendbuf));
+        ch->allreduce(view(sendbuf), view(recvbuf), std::move(raw));
     }
 
     //! Inclusive prefix across peers: peer k receives x0 f ... f xk.
@@ -123,8 +127,9 @@ public:
         if (sendbuf.size_in_bytes() != recvbuf.size_in_bytes())
             throw std::runtime_error("Dimensions of send and receive data must match");
         // the reference does not pass left_to_right here (include/Communicator.h:140)
-        auto ch = channel_for({Utils::scan, sendbuf.size_in_bytes()}, on_device(sendbuf));
-        ch->scan(view(sendbuf), view(recvbuf), convert_to_raw_function(f, sendbuf.size_in_bytes()));
+        raw_function raw = convert_to_raw_function(f, sendbuf.size_in_bytes());
+        auto ch = channel_for({Utils::scan, sendbuf.size_in_bytes(), false, false, !raw.device.valid()}, on_device(sendbuf));
+        ch->scan(view(sendbuf), view(recvbuf), std::move(raw));
     }
 
     //! Add a channel under `name` (reference src/Communicator.cpp:24-29).

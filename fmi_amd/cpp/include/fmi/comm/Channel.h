@@ -107,6 +107,9 @@ public:
     //! policy uses it to keep device buckets off channels that cannot).
     virtual bool supports_device_buffers() const { return true; }
     virtual bool supports_host_buffers() const { return true; }
+    //! Whether reductions may be opaque user functions (raw_function::f); device collectives need a
+    //! built-in op (raw_function::device).
+    virtual bool supports_user_functions() const { return true; }
 
     virtual double get_latency(Utils::peer_num producer, Utils::peer_num consumer, std::size_t size_in_bytes) = 0;
     virtual double get_price(Utils::peer_num producer, Utils::peer_num consumer, std::size_t size_in_bytes) = 0;

@@ -10,6 +10,12 @@
 // Side effects mirrored from the reference: commutative allreduce and scan leave sendbuf = result
 // (reference src/comm/PeerToPeer.cpp:129,183), reduce leaves the root's sendbuf = result (:80); the
 // non-root partials of the reference's reduce are intermediate values and are not reproduced.
+//
+// Host ingress (config C5), opt-in with set_host_ingress(): the channel then also
+// carries host buckets — the recv buffers FMI's transports fill (reference src/comm/Direct.cpp:36-45).
+// allreduce streams them through the GPU with fmi_comm_allreduce_host (H2D, sharded allreduce and D2H of
+// successive chunks overlapped); every other collective stages the host bucket through HBM. The model
+// charges the PCIe crossing, so ChannelPolicy keeps small host operations on the host channels.
 #ifndef FMI_AMD_COMM_RCCL_H
 #define FMI_AMD_COMM_RCCL_H
 
@@ -43,57 +49,83 @@ public:
 
     ~Rccl() override { finalize(); }
 
-    bool supports_host_buffers() const override { return false; }
+    bool supports_host_buffers() const override { return host_ingress_; }
+    bool supports_user_functions() const override { return false; }
+
+    //! Accept host buckets too (staged through HBM; allreduce pipelined). pcie_gb_s prices the crossing.
+    void set_host_ingress(bool on, double pcie_gb_s = 50.) {
+        host_ingress_ = on;
+        pcie_gb_s_ = pcie_gb_s;
+    }
 
     void send(channel_data buf, Utils::peer_num dest) override {
-        device_only(buf);
-        run(fmi_comm_send(comm_, buf.buf, buf.len, static_cast<int>(dest), nullptr), "fmi_comm_send");
+        Staged b(this, buf, true);
+        run(fmi_comm_send(comm_, b.ptr(), buf.len, static_cast<int>(dest), nullptr), "fmi_comm_send");
     }
     void recv(channel_data buf, Utils::peer_num src) override {
-        device_only(buf);
-        run(fmi_comm_recv(comm_, buf.buf, buf.len, static_cast<int>(src), nullptr), "fmi_comm_recv");
+        Staged b(this, buf, false);
+        run(fmi_comm_recv(comm_, b.ptr(), buf.len, static_cast<int>(src), nullptr), "fmi_comm_recv");
+        b.store();
     }
     void bcast(channel_data buf, Utils::peer_num root) override {
-        device_only(buf);
-        run(fmi_comm_bcast(comm_, buf.buf, buf.len, static_cast<int>(root), nullptr), "fmi_comm_bcast");
+        Staged b(this, buf, peer_id == root);
+        run(fmi_comm_bcast(comm_, b.ptr(), buf.len, static_cast<int>(root), nullptr), "fmi_comm_bcast");
+        if (peer_id != root) b.store();
     }
     void barrier() override { run(fmi_comm_barrier(comm_, nullptr), "fmi_comm_barrier"); }
 
     void gather(channel_data sendbuf, channel_data recvbuf, Utils::peer_num root) override {
-        device_only(sendbuf);
-        run(fmi_comm_gather(comm_, sendbuf.buf, peer_id == root ? recvbuf.buf : nullptr, sendbuf.len,
-                            static_cast<int>(root), nullptr),
+        const bool is_root = peer_id == root;
+        Staged s(this, sendbuf, true);
+        Staged r(this, is_root ? recvbuf : channel_data{nullptr, 0, true}, false);
+        run(fmi_comm_gather(comm_, s.ptr(), is_root ? r.ptr() : nullptr, sendbuf.len, static_cast<int>(root), nullptr),
             "fmi_comm_gather");
+        if (is_root) r.store();
     }
     void scatter(channel_data sendbuf, channel_data recvbuf, Utils::peer_num root) override {
-        device_only(recvbuf);
-        run(fmi_comm_scatter(comm_, peer_id == root ? sendbuf.buf : nullptr, recvbuf.buf, recvbuf.len,
-                             static_cast<int>(root), nullptr),
+        const bool is_root = peer_id == root;
+        Staged s(this, is_root ? sendbuf : channel_data{nullptr, 0, true}, true);
+        Staged r(this, recvbuf, false);
+        run(fmi_comm_scatter(comm_, is_root ? s.ptr() : nullptr, r.ptr(), recvbuf.len, static_cast<int>(root), nullptr),
             "fmi_comm_scatter");
+        r.store();
     }
 
     void reduce(channel_data sendbuf, channel_data recvbuf, Utils::peer_num root, raw_function f) override {
         const device_op& d = device_of(f, sendbuf);
         const int alg = ordered(f) ? FMI_ALG_REDUCE_LTR : FMI_ALG_REDUCE;
         const bool is_root = peer_id == root;
-        run(fmi_comm_reduce(comm_, d.op, d.dtype, alg, sendbuf.buf, is_root ? recvbuf.buf : nullptr, d.count,
+        Staged s(this, sendbuf, true);
+        Staged r(this, is_root ? recvbuf : channel_data{nullptr, 0, true}, false);
+        run(fmi_comm_reduce(comm_, d.op, d.dtype, alg, s.ptr(), is_root ? r.ptr() : nullptr, d.count,
                             static_cast<int>(root), nullptr),
             "fmi_comm_reduce");
-        if (is_root && !ordered(f)) mirror(sendbuf, recvbuf);
+        if (!is_root) return;
+        r.store();
+        if (!ordered(f)) mirror(sendbuf, recvbuf);
     }
 
     void allreduce(channel_data sendbuf, channel_data recvbuf, raw_function f) override {
         const device_op& d = device_of(f, sendbuf);
+        carries(recvbuf);
         const int alg = ordered(f) ? FMI_ALG_REDUCE_LTR : FMI_ALG_ALLREDUCE;
-        run(fmi_comm_allreduce(comm_, d.op, d.dtype, alg, path_, sendbuf.buf, recvbuf.buf, d.count, nullptr),
-            "fmi_comm_allreduce");
+        if (!sendbuf.on_device || !recvbuf.on_device) {  // host ingress: pipelined through the GPU
+            Dev::check(fmi_comm_allreduce_host(comm_, d.op, d.dtype, alg, path_, sendbuf.buf, recvbuf.buf, d.count, 0),
+                       "fmi_comm_allreduce_host");
+        } else {
+            run(fmi_comm_allreduce(comm_, d.op, d.dtype, alg, path_, sendbuf.buf, recvbuf.buf, d.count, nullptr),
+                "fmi_comm_allreduce");
+        }
         if (!ordered(f)) mirror(sendbuf, recvbuf);
     }
 
     void scan(channel_data sendbuf, channel_data recvbuf, raw_function f) override {
         const device_op& d = device_of(f, sendbuf);
         const int alg = ordered(f) ? FMI_ALG_SCAN_LTR : FMI_ALG_SCAN;
-        run(fmi_comm_scan(comm_, d.op, d.dtype, alg, sendbuf.buf, recvbuf.buf, d.count, nullptr), "fmi_comm_scan");
+        Staged s(this, sendbuf, true);
+        Staged r(this, recvbuf, false);
+        run(fmi_comm_scan(comm_, d.op, d.dtype, alg, s.ptr(), r.ptr(), d.count, nullptr), "fmi_comm_scan");
+        r.store();
         if (!ordered(f)) mirror(sendbuf, recvbuf);
     }
 
@@ -115,15 +147,20 @@ public:
         const double P = num_peers;
         const double frac = P > 1 ? (P - 1) / P : 0.;
         const std::size_t bytes = info.data_size;
+        // host buckets cross PCIe once each way (overlapped with the exchange for allreduce)
+        const double pcie = info.on_device || info.op == Utils::barrier
+                                ? 0.
+                                : (info.op == Utils::allreduce ? 1. : 2.) * static_cast<double>(bytes) / 1e9 /
+                                      pcie_gb_s_ * 1e3;
         switch (info.op) {
-            case Utils::send: return get_latency(1, 1, bytes);
+            case Utils::send: return pcie + get_latency(1, 1, bytes);
             case Utils::barrier: return 0.02;
             case Utils::bcast:
             case Utils::gather:
-            case Utils::scatter: return 0.01 + frac * get_latency(1, 1, bytes);
+            case Utils::scatter: return pcie + 0.01 + frac * get_latency(1, 1, bytes);
             case Utils::reduce:
             case Utils::allreduce:
-            case Utils::scan: return 0.02 + 2 * frac * get_latency(1, 1, bytes);
+            case Utils::scan: return pcie + 0.02 + 2 * frac * get_latency(1, 1, bytes);
         }
         throw std::runtime_error("Operation not implemented");
     }
@@ -134,11 +171,12 @@ private:
 
     static bool ordered(const raw_function& f) { return !(f.commutative && f.associative); }
 
-    static void device_only(const channel_data& b) {
-        if (!b.on_device && b.len) throw std::runtime_error("Rccl channel carries device buckets only");
+    void carries(const channel_data& b) const {
+        if (!b.on_device && b.len && !host_ingress_)
+            throw std::runtime_error("Rccl channel carries device buckets only (see set_host_ingress)");
     }
-    static const device_op& device_of(const raw_function& f, const channel_data& b) {
-        device_only(b);
+    const device_op& device_of(const raw_function& f, const channel_data& b) const {
+        carries(b);
         if (!f.device.valid())
             throw std::runtime_error("Rccl channel needs a built-in reduction op (Function<T>(Utils::Op::...))");
         return f.device;
@@ -148,12 +186,36 @@ private:
         Dev::check(fmi_stream_sync(nullptr), "fmi_stream_sync");  // FMI collectives are blocking
     }
     static void mirror(const channel_data& sendbuf, const channel_data& recvbuf) {
-        if (sendbuf.buf != recvbuf.buf) Dev::copy_bytes(sendbuf.buf, true, recvbuf.buf, true, sendbuf.len);
+        if (sendbuf.buf != recvbuf.buf)
+            Dev::copy_bytes(sendbuf.buf, sendbuf.on_device, recvbuf.buf, recvbuf.on_device, sendbuf.len);
     }
+
+    // A device view of a channel buffer: the buffer itself when it lives in HBM, else an HBM copy of the
+    // host bucket (loaded on construction if `load`, written back by store()).
+    class Staged {
+    public:
+        Staged(const Rccl* ch, const channel_data& b, bool load) : user_(b), host_(!b.on_device && b.buf) {
+            ch->carries(b);
+            if (!host_) return;
+            scratch_ = Dev::Scratch(b.len, true);
+            if (load) Dev::copy_bytes(scratch_.get(), true, b.buf, false, b.len);
+        }
+        char* ptr() const { return host_ ? scratch_.get() : user_.buf; }
+        void store() const {
+            if (host_) Dev::copy_bytes(user_.buf, false, scratch_.get(), true, user_.len);
+        }
+
+    private:
+        channel_data user_;
+        bool host_;
+        Dev::Scratch scratch_;
+    };
 
     fmi_comm_t comm_ = nullptr;
     double link_gb_s_;
     int path_ = FMI_PATH_TREE;
+    bool host_ingress_ = false;
+    double pcie_gb_s_ = 50.;
 };
 
 }  // namespace FMI::Comm

@@ -2,7 +2,8 @@
 // and src/utils/ChannelPolicy.cpp:9-29): argmin of the model latency for Hint::fast, argmin of channel
 // price + FaaS runtime price for Hint::cheap. Channels are compared through their own
 // get_operation_latency / get_operation_price, so an RCCL channel competes on the same terms.
-// Added: channels that cannot carry the operation's buffers (host vs device) are skipped.
+// Added: channels that cannot carry the operation's buffers (host vs device), or cannot run an opaque user
+// reduction function, are skipped.
 #ifndef FMI_AMD_UTILS_CHANNELPOLICY_H
 #define FMI_AMD_UTILS_CHANNELPOLICY_H
 
@@ -40,6 +41,7 @@ protected:
         double best_score = std::numeric_limits<double>::infinity();
         for (const auto& [name, channel] : channels_) {
             if (on_device ? !channel->supports_device_buffers() : !channel->supports_host_buffers()) continue;
+            if (op_info.user_function && !channel->supports_user_functions()) continue;
             const double latency = channel->get_operation_latency(op_info);
             const double score = hint_ == fast ? latency : channel->get_operation_price(op_info) + latency * faas_price_;
             if (best.empty() || score < best_score) {

@@ -28,6 +28,7 @@ struct OperationInfo {
     std::size_t data_size;
     bool left_to_right = false;
     bool on_device = false;  // extension: the buffers live in GPU memory (channel models add staging)
+    bool user_function = false;  // extension: the reduction is an opaque user function (no built-in op)
 };
 
 }  // namespace FMI::Utils

@@ -683,6 +683,96 @@ GPU_TEST(policy_routes_device_buckets_to_rccl) {
     }
 }
 
+// Host buckets over the Rccl channel (host ingress, config C5 shape): with only Rccl registered, every
+// collective of host vectors runs through the GPU (allreduce pipelined, the rest staged) and must equal
+// the host-channel results bit for bit; sendbuf side effects as in the reference.
+GPU_TEST(rccl_channel_host_ingress_local_transport) {
+    Dev::init(0);
+    for (peer_num P : {2u, 3u, 8u}) {
+        const std::size_t n = 200003;
+        std::vector<std::vector<float>> host_ar(P), host_sc(P), dev_ar(P), dev_send(P), dev_sc(P);
+        std::vector<float> host_red, dev_red;
+        with_peers(P, [&](Communicator& c, peer_num p) {
+            Data<std::vector<float>> a(synth_f32(n, 8, p)), r(n);
+            c.allreduce(a, r, Function<std::vector<float>>(Op::sum));
+            host_ar[p] = r.get();
+            Data<std::vector<float>> s(synth_f32(n, 8, p)), sr(n);
+            c.scan(s, sr, Function<std::vector<float>>(Op::sum));
+            host_sc[p] = sr.get();
+            Data<std::vector<float>> d(synth_f32(n, 8, p)), dr(n);
+            c.reduce(d, dr, P - 1, Function<std::vector<float>>(Op::sum));
+            if (p == P - 1) host_red = dr.get();
+        });
+        auto mailbox = std::make_shared<FMI::Comm::Mailbox>();
+        std::vector<std::thread> ts;
+        std::vector<std::string> errors(P);
+        for (peer_num p = 0; p < P; ++p)
+            ts.emplace_back([&, p] {
+                try {
+                    Communicator c(p, P, "", "rccl-host");
+                    FMI::Comm::Loopback boot(mailbox, std::chrono::seconds(60));
+                    boot.set_peer_id(p);
+                    boot.set_num_peers(P);
+                    auto rccl = FMI::Comm::Rccl::connect(boot, p, P, FMI_TRANSPORT_LOCAL);
+                    rccl->set_host_ingress(true);
+                    c.register_channel("Rccl", rccl);
+                    Data<std::vector<float>> a(synth_f32(n, 8, p)), r(n);
+                    c.allreduce(a, r, Function<std::vector<float>>(Op::sum));
+                    dev_ar[p] = r.get();
+                    dev_send[p] = a.get();
+                    Data<std::vector<float>> s(synth_f32(n, 8, p)), sr(n);
+                    c.scan(s, sr, Function<std::vector<float>>(Op::sum));
+                    dev_sc[p] = sr.get();
+                    Data<std::vector<float>> d(synth_f32(n, 8, p)), dr(n);
+                    c.reduce(d, dr, P - 1, Function<std::vector<float>>(Op::sum));
+                    if (p == P - 1) dev_red = dr.get();
+                    Data<std::vector<int64_t>> b(std::vector<int64_t>{static_cast<int64_t>(p), 9});
+                    c.bcast(b, P - 1);
+                    if (b.get()[0] != static_cast<int64_t>(P - 1)) throw std::runtime_error("host bcast over Rccl");
+                    Data<std::vector<int32_t>> g(std::vector<int32_t>{static_cast<int32_t>(p)}), all(P);
+                    c.gather(g, all, 0);
+                    if (p == 0)
+                        for (peer_num j = 0; j < P; ++j)
+                            if (all.get()[j] != static_cast<int32_t>(j)) throw std::runtime_error("host gather over Rccl");
+                    c.barrier();
+                } catch (const std::exception& e) {
+                    errors[p] = e.what();
+                }
+            });
+        for (auto& t : ts) t.join();
+        for (peer_num p = 0; p < P; ++p) {
+            if (!errors[p].empty()) {
+                ++g_failures;
+                std::fprintf(stderr, "  peer %u threw: %s\n", p, errors[p].c_str());
+                continue;
+            }
+            CHECK(std::memcmp(host_ar[p].data(), dev_ar[p].data(), n * 4) == 0);
+            CHECK(std::memcmp(dev_send[p].data(), dev_ar[p].data(), n * 4) == 0);  // sendbuf = result
+            CHECK(std::memcmp(host_sc[p].data(), dev_sc[p].data(), n * 4) == 0);
+        }
+        CHECK(host_red.size() == n && dev_red.size() == n && std::memcmp(host_red.data(), dev_red.data(), n * 4) == 0);
+    }
+}
+
+GPU_TEST(policy_host_ingress_keeps_user_functions_and_small_buckets_on_host) {
+    Dev::init(0);
+    std::map<std::string, std::shared_ptr<FMI::Comm::Channel>> chans;
+    auto mailbox = std::make_shared<FMI::Comm::Mailbox>();
+    auto loop = std::make_shared<FMI::Comm::Loopback>(mailbox);
+    loop->set_num_peers(1);
+    chans["Loopback"] = loop;
+    auto rccl = FMI::Comm::Rccl::connect(*loop, 0, 1, FMI_TRANSPORT_LOCAL);
+    rccl->set_host_ingress(true);
+    chans["Rccl"] = rccl;
+    FMI::Utils::ChannelPolicy policy(chans, 1, 0.0000166667 / 8, FMI::Utils::fast);
+    for (std::size_t bytes : {std::size_t(1) << 10, std::size_t(256) << 20}) {
+        FMI::Utils::OperationInfo user{FMI::Utils::allreduce, bytes, false, false, true};
+        CHECK(policy.get_channel(user) == "Loopback");  // Rccl cannot run an opaque user function
+    }
+    CHECK(policy.get_channel({FMI::Utils::send, 64}) == "Loopback");  // PCIe crossing outweighs it
+    CHECK(policy.get_device_channel({FMI::Utils::allreduce, std::size_t(1) << 20}) == "Rccl");
+}
+
 GPU_TEST(device_buckets_need_builtin_op) {
     Dev::init(0);
     with_peers(1, [](Communicator& c, peer_num) {

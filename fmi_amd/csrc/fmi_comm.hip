@@ -17,6 +17,7 @@
 #include <rccl/rccl.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
 #include <condition_variable>
 #include <cstdlib>
@@ -384,13 +385,42 @@ private:
 // ---------------------------------------------------------------------------------------------------
 // communicator
 // ---------------------------------------------------------------------------------------------------
+// Streams and events of the host-ingress pipeline (fmi_comm_allreduce_host), created on first use.
+struct HostPipe {
+    hipStream_t cs = nullptr;   // the chunk's sharded allreduce
+    hipStream_t h2d = nullptr;  // host -> device loads
+    hipStream_t d2h = nullptr;  // device -> host results
+    hipEvent_t loaded[2] = {}, reduced[2] = {}, drained[2] = {};
+    bool ready = false;
+
+    int init() {
+        if (ready) return FMI_OK;
+        for (hipStream_t* st : {&cs, &h2d, &d2h}) FMI_COMM_HIP(hipStreamCreateWithFlags(st, hipStreamNonBlocking));
+        for (int k = 0; k < 2; ++k)
+            for (hipEvent_t* ev : {&loaded[k], &reduced[k], &drained[k]})
+                FMI_COMM_HIP(hipEventCreateWithFlags(ev, hipEventDisableTiming));
+        ready = true;
+        return FMI_OK;
+    }
+    ~HostPipe() {
+        for (hipStream_t st : {cs, h2d, d2h})
+            if (st) (void)hipStreamDestroy(st);
+        for (int k = 0; k < 2; ++k)
+            for (hipEvent_t ev : {loaded[k], reduced[k], drained[k]})
+                if (ev) (void)hipEventDestroy(ev);
+    }
+};
+
 struct Comm {
+    static constexpr int kSlots = 8;  // 0-3: collective scratch; 4-7: host-pipeline chunk slots
     std::unique_ptr<Transport> t;
     std::mutex mu;
-    void* buf[4] = {nullptr, nullptr, nullptr, nullptr};
-    size_t cap[4] = {0, 0, 0, 0};
+    void* buf[kSlots] = {};
+    size_t cap[kSlots] = {};
+    HostPipe pipe;
 
     ~Comm() {
+        if (pipe.cs) (void)hipStreamSynchronize(pipe.cs);
         for (void* b : buf)
             if (b) (void)hipFree(b);
     }
@@ -438,6 +468,48 @@ int padded_source(Comm* c, size_t n, size_t padded, size_t esz, const void* send
     FMI_COMM_HIP(hipMemcpyAsync(pad, send, n * esz, hipMemcpyDeviceToDevice, s));
     FMI_COMM_HIP(hipMemsetAsync(pad + n * esz, 0, (padded - n) * esz, s));
     *out = pad;
+    return FMI_OK;
+}
+
+// The sharded allreduce of one device bucket on stream s (caller holds c->mu; arguments validated).
+int allreduce_device(Comm* c, int op, int dtype, int alg, int path, const void* send, void* recv, size_t n,
+                     hipStream_t s) {
+    const int N = c->t->n();
+    const size_t esz = dtype_size(dtype);
+    if (N == 1) {  // reference P = 1: a copy
+        if (send != recv) FMI_COMM_HIP(hipMemcpyAsync(recv, send, n * esz, hipMemcpyDeviceToDevice, s));
+        return FMI_OK;
+    }
+    const size_t shard = shard_elems(n, N);
+    const size_t padded = shard * N;
+    const char* src = nullptr;
+    FMI_COMM_RC(padded_source(c, n, padded, esz, send, s, &src));
+    char* red = nullptr;
+    FMI_COMM_RC(c->scratch(2, shard * esz, s, &red));
+    if (path == FMI_PATH_TREE) {
+        char* staging = nullptr;
+        FMI_COMM_RC(c->scratch(1, padded * esz, s, &staging));
+        FMI_COMM_RC(c->t->all_to_all(src, staging, shard * esz, s));
+        std::vector<const void*> parts(N);
+        for (int j = 0; j < N; ++j) parts[j] = staging + j * shard * esz;
+        FMI_COMM_RC(fmi_dev_reduce_tree(op, dtype, alg, red, parts.data(), N, 0, shard, s));
+    } else {
+        FMI_COMM_RC(c->t->reduce_scatter(op, dtype, src, red, shard, s));
+    }
+    if (padded == n) return c->t->all_gather(red, static_cast<char*>(recv), shard * esz, s);
+    char* out = nullptr;
+    FMI_COMM_RC(c->scratch(3, padded * esz, s, &out));
+    FMI_COMM_RC(c->t->all_gather(red, out, shard * esz, s));
+    FMI_COMM_HIP(hipMemcpyAsync(recv, out, n * esz, hipMemcpyDeviceToDevice, s));
+    return FMI_OK;
+}
+
+int check_allreduce_args(int alg, int path) {
+    if (alg != FMI_ALG_ALLREDUCE && alg != FMI_ALG_REDUCE_LTR)
+        return fail(FMI_ERR_INVALID, "allreduce: alg must be ALLREDUCE or REDUCE_LTR");
+    if (path != FMI_PATH_TREE && path != FMI_PATH_RCCL) return fail(FMI_ERR_INVALID, "unknown path");
+    if (path == FMI_PATH_RCCL && alg != FMI_ALG_ALLREDUCE)
+        return fail(FMI_ERR_INVALID, "ordered (LTR) allreduce needs the tree path");
     return FMI_OK;
 }
 
@@ -514,43 +586,66 @@ int fmi_comm_size(fmi_comm_t comm, int* nranks, int* rank) {
 int fmi_comm_allreduce(fmi_comm_t comm, int op, int dtype, int alg, int path, const void* send, void* recv, size_t n,
                        fmi_stream_t stream) {
     FMI_COMM_RC(check_common(comm, op, dtype));
-    if (alg != FMI_ALG_ALLREDUCE && alg != FMI_ALG_REDUCE_LTR)
-        return fail(FMI_ERR_INVALID, "allreduce: alg must be ALLREDUCE or REDUCE_LTR");
-    if (path != FMI_PATH_TREE && path != FMI_PATH_RCCL) return fail(FMI_ERR_INVALID, "unknown path");
-    if (path == FMI_PATH_RCCL && alg != FMI_ALG_ALLREDUCE)
-        return fail(FMI_ERR_INVALID, "ordered (LTR) allreduce needs the tree path");
+    FMI_COMM_RC(check_allreduce_args(alg, path));
     if (n == 0) return FMI_OK;
     if (!send || !recv) return fail(FMI_ERR_INVALID, "null bucket");
     Comm* c = static_cast<Comm*>(comm);
     std::lock_guard<std::mutex> lk(c->mu);
-    hipStream_t s = resolve_stream(stream);
-    const int N = c->t->n();
+    return allreduce_device(c, op, dtype, alg, path, send, recv, n, resolve_stream(stream));
+}
+
+// Three-stage pipeline over two chunk slots: while chunk k is allreduced on pipe.cs, chunk k+1 loads on
+// pipe.h2d and chunk k-1 drains on pipe.d2h. Slot reuse is ordered by events: a load into slot j waits
+// until the allreduce that read it has finished (reduced), an allreduce into slot j waits until the
+// previous result in it has drained to the host.
+int fmi_comm_allreduce_host(fmi_comm_t comm, int op, int dtype, int alg, int path, const void* send, void* recv,
+                            size_t n, size_t chunk) {
+    FMI_COMM_RC(check_common(comm, op, dtype));
+    FMI_COMM_RC(check_allreduce_args(alg, path));
+    if (n == 0) return FMI_OK;
+    if (!send || !recv) return fail(FMI_ERR_INVALID, "null bucket");
+    Comm* c = static_cast<Comm*>(comm);
+    std::lock_guard<std::mutex> lk(c->mu);
+    HostPipe& p = c->pipe;
+    FMI_COMM_RC(p.init());
     const size_t esz = dtype_size(dtype);
-    if (N == 1) {  // reference P = 1: a copy
-        if (send != recv) FMI_COMM_HIP(hipMemcpyAsync(recv, send, n * esz, hipMemcpyDeviceToDevice, s));
+    if (chunk == 0) {
+        long long bytes = 0;
+        (void)fmi_tune_get(FMI_TUNE_HOST_CHUNK, &bytes);
+        chunk = std::max<size_t>(static_cast<size_t>(bytes) / esz, kShardAlign);
+    }
+    chunk = std::min(chunk, n);
+    const size_t nchunks = (n + chunk - 1) / chunk;
+    char* in[2] = {};
+    char* out[2] = {};
+    for (int j = 0; j < 2; ++j) {
+        FMI_COMM_RC(c->scratch(4 + j, chunk * esz, p.cs, &in[j]));
+        FMI_COMM_RC(c->scratch(6 + j, chunk * esz, p.cs, &out[j]));
+    }
+    const char* src = static_cast<const char*>(send);
+    char* dst = static_cast<char*>(recv);
+    auto span = [&](size_t k) { return std::min(chunk, n - k * chunk); };
+    auto load = [&](size_t k) -> int {
+        const int j = static_cast<int>(k & 1);
+        if (k >= 2) FMI_COMM_HIP(hipStreamWaitEvent(p.h2d, p.reduced[j], 0));
+        FMI_COMM_HIP(hipMemcpyAsync(in[j], src + k * chunk * esz, span(k) * esz, hipMemcpyDefault, p.h2d));
+        FMI_COMM_HIP(hipEventRecord(p.loaded[j], p.h2d));
         return FMI_OK;
+    };
+    FMI_COMM_RC(load(0));
+    for (size_t k = 0; k < nchunks; ++k) {
+        if (k + 1 < nchunks) FMI_COMM_RC(load(k + 1));
+        const int j = static_cast<int>(k & 1);
+        FMI_COMM_HIP(hipStreamWaitEvent(p.cs, p.loaded[j], 0));
+        if (k >= 2) FMI_COMM_HIP(hipStreamWaitEvent(p.cs, p.drained[j], 0));
+        FMI_COMM_RC(allreduce_device(c, op, dtype, alg, path, in[j], out[j], span(k), p.cs));
+        FMI_COMM_HIP(hipEventRecord(p.reduced[j], p.cs));
+        FMI_COMM_HIP(hipStreamWaitEvent(p.d2h, p.reduced[j], 0));
+        FMI_COMM_HIP(hipMemcpyAsync(dst + k * chunk * esz, out[j], span(k) * esz, hipMemcpyDefault, p.d2h));
+        FMI_COMM_HIP(hipEventRecord(p.drained[j], p.d2h));
     }
-    const size_t shard = shard_elems(n, N);
-    const size_t padded = shard * N;
-    const char* src = nullptr;
-    FMI_COMM_RC(padded_source(c, n, padded, esz, send, s, &src));
-    char* red = nullptr;
-    FMI_COMM_RC(c->scratch(2, shard * esz, s, &red));
-    if (path == FMI_PATH_TREE) {
-        char* staging = nullptr;
-        FMI_COMM_RC(c->scratch(1, padded * esz, s, &staging));
-        FMI_COMM_RC(c->t->all_to_all(src, staging, shard * esz, s));
-        std::vector<const void*> parts(N);
-        for (int j = 0; j < N; ++j) parts[j] = staging + j * shard * esz;
-        FMI_COMM_RC(fmi_dev_reduce_tree(op, dtype, alg, red, parts.data(), N, 0, shard, s));
-    } else {
-        FMI_COMM_RC(c->t->reduce_scatter(op, dtype, src, red, shard, s));
-    }
-    if (padded == n) return c->t->all_gather(red, static_cast<char*>(recv), shard * esz, s);
-    char* out = nullptr;
-    FMI_COMM_RC(c->scratch(3, padded * esz, s, &out));
-    FMI_COMM_RC(c->t->all_gather(red, out, shard * esz, s));
-    FMI_COMM_HIP(hipMemcpyAsync(recv, out, n * esz, hipMemcpyDeviceToDevice, s));
+    FMI_COMM_HIP(hipStreamSynchronize(p.d2h));
+    FMI_COMM_HIP(hipStreamSynchronize(p.cs));
     return FMI_OK;
 }
 

@@ -171,6 +171,15 @@ int fmi_comm_size(fmi_comm_t comm, int* nranks, int* rank);
 /* alg: FMI_ALG_ALLREDUCE (commutative+associative) or FMI_ALG_REDUCE_LTR (ordered) */
 int fmi_comm_allreduce(fmi_comm_t comm, int op, int dtype, int alg, int path, const void* send, void* recv, size_t n,
                        fmi_stream_t stream);
+/* Host-ingress allreduce (BASELINE config C5): `send` / `recv` are HOST buckets, i.e. the channel recv
+ * buffers FMI's transports deliver into (reference src/comm/Direct.cpp:36-45, PeerToPeer.cpp:110-129).
+ * The bucket streams through the GPU in chunks of `chunk` elements (0 = FMI_TUNE_HOST_CHUNK bytes):
+ * H2D of chunk k+1, the sharded allreduce of chunk k and D2H of chunk k-1 overlap on three streams.
+ * Every rank must pass the same n and chunk. Page-locked buckets (fmi_host_pin_alloc) move at PCIe DMA
+ * rate; pageable ones work but copy synchronously. Element-wise results are identical to
+ * fmi_comm_allreduce over the whole bucket. Blocking: returns when `recv` holds the result. */
+int fmi_comm_allreduce_host(fmi_comm_t comm, int op, int dtype, int alg, int path, const void* send, void* recv,
+                            size_t n, size_t chunk);
 /* alg: FMI_ALG_REDUCE or FMI_ALG_REDUCE_LTR; recv is used on root only (may be NULL elsewhere) */
 int fmi_comm_reduce(fmi_comm_t comm, int op, int dtype, int alg, const void* send, void* recv, size_t n, int root,
                     fmi_stream_t stream);

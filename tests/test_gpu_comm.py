@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 
 import fmi_amd
-from fmi_amd import Bucket, Op
+from fmi_amd import Bucket, Op, PinnedArray
 from fmi_amd.comm import Comm, Path, Transport, unique_id
 from oracle import fmi_oracle as orc
 from tests.test_gpu_parity import OPNAME, assert_bit_equal, inputs
@@ -116,6 +116,55 @@ def test_comm_scan(device, N):
                 want, _ = orc.scan(xs, orc.OPS[OPNAME[op]], commutative=not ordered, associative=not ordered)
             for r in range(N):
                 assert_bit_equal(res[r], want[r], f"N={N} {op.name} ordered={ordered} rank {r}")
+
+
+def _host_allreduce(c, r, x, op, ordered, pinned, chunk):
+    n, dtype = x.size, x.dtype
+    if pinned:
+        s, out = PinnedArray(n, dtype), PinnedArray(n, dtype)
+        s.array[:] = x
+        c.allreduce_host(op, s.array, out.array, ordered=ordered, chunk=chunk)
+        res = out.array.copy(), s.array.copy()
+        s.free()
+        out.free()
+        return res
+    s, out = x.copy(), np.zeros(n, dtype)
+    c.allreduce_host(op, s, out, ordered=ordered, chunk=chunk)
+    return out, s
+
+
+@pytest.mark.parametrize("N", [1, 2, 3, 8])
+@pytest.mark.parametrize("pinned", [True, False])
+def test_comm_allreduce_host_pipeline(device, N, pinned):
+    """Host-ingress allreduce (config C5 shape): host buckets stream through the GPU in chunks (ragged last
+    chunk, padded shards, slot reuse over > 2 chunks); every rank's host result equals the oracle's."""
+    n, chunk = 3 * 4099 + 17, 4099
+    for dtype, op, ordered in ((np.float32, Op.SUM, False), (np.int64, Op.MAX, False), (np.float64, Op.PROD, False),
+                               (np.float32, Op.SUM, True)):
+        xs = [inputs(dtype, n, r, seed=13) for r in range(N)]
+        res = run_ranks(N, lambda c, r: _host_allreduce(c, r, xs[r], op, ordered, pinned, chunk))
+        with np.errstate(all="ignore"):
+            want, _ = orc.allreduce(xs, orc.OPS[OPNAME[op]], commutative=not ordered, associative=not ordered)
+        for r in range(N):
+            assert_bit_equal(res[r][0], want[r] if ordered else want[0], f"N={N} {op.name} ordered={ordered} rank {r}")
+            assert_bit_equal(res[r][1], xs[r], "send bucket untouched")
+
+
+def test_comm_allreduce_host_default_chunk_matches_device(device):
+    """Default chunking (FMI_TUNE_HOST_CHUNK) over a 40 MiB bucket per rank: bit-identical to the device
+    allreduce of the whole bucket."""
+    N, n = 4, 10 * (1 << 20) + 3
+    xs = [inputs(np.float32, n, r, seed=21) for r in range(N)]
+
+    def body(c, r):
+        got, _ = _host_allreduce(c, r, xs[r], Op.SUM, False, True, 0)
+        s, out = Bucket.from_numpy(xs[r]), Bucket(n, np.float32)
+        c.allreduce(Op.SUM, s, out)
+        fmi_amd.sync()
+        return got, out.numpy()
+
+    for r, (got, dev) in enumerate(run_ranks(N, body)):
+        assert_bit_equal(got, dev, f"rank {r}")
 
 
 def test_comm_point_to_point_and_data_movement(device):

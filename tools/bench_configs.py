@@ -58,9 +58,17 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=30)
     ap.add_argument("--quick", action="store_true")
+    ap.add_argument("--c5-only", action="store_true", help="only the host-ingress allreduce rows")
+    ap.add_argument("--torch-runtime", action="store_true",
+                    help="import torch first, so the library binds to torch's bundled HIP runtime")
     args = ap.parse_args()
+    if args.torch_runtime:
+        import torch  # noqa: F401
     fmi_amd.init(0)
     it = args.iters
+    if args.c5_only:
+        host_allreduce_rows()
+        return
 
     # C2 and its siblings: pairwise combine, every dtype/op, 256 MiB buckets, 4 rotating sets
     for dt in (np.float32, np.float64, np.int32, np.int64):
@@ -145,6 +153,55 @@ def main():
     med = statistics.median(ts)
     print(json.dumps(dict(config="host pageable pair sum f32 256MiB", median_ms=round(med * 1e3, 3),
                           bucket_gib_s=round(256 / 1024 / med, 3))), flush=True)
+    host_allreduce_rows()
+
+
+def host_allreduce_rows():
+    """Config C5 shape: fmi_comm_allreduce_host over page-locked host buckets (H2D, sharded allreduce, D2H
+    pipelined in chunks). N ranks are threads of this process on the one GPU (LOCAL transport), so all of
+    them share one PCIe link: N = 1 is the per-GPU PCIe-bound rate of the 8-GPU node, N = 8 shows the
+    schedule with 8 ranks behind one link."""
+    import threading
+
+    from fmi_amd.comm import Comm, Transport, unique_id
+
+    for N, mib, chunks in ((1, 1024, (16, 64, 128)), (8, 128, (16, 64))):
+        n = mib * MIB // 4
+        bufs = [(fmi_amd.PinnedArray(n, np.float32), fmi_amd.PinnedArray(n, np.float32)) for _ in range(N)]
+        for r, (s, _) in enumerate(bufs):
+            s.array[:] = np.float32(r + 1)
+        for chunk in chunks:
+            uid = unique_id(Transport.LOCAL)
+            times = [None] * N
+
+            def worker(r):
+                c = Comm(uid, N, r)
+                s, o = bufs[r]
+                ts = []
+                for k in range(4):
+                    c.barrier()
+                    t0 = time.perf_counter()
+                    c.allreduce_host(Op.SUM, s.array, o.array, chunk=chunk * MIB // 4)
+                    c.barrier()
+                    ts.append(time.perf_counter() - t0)
+                times[r] = statistics.median(ts[1:])
+                c.destroy()
+
+            th = [threading.Thread(target=worker, args=(r,)) for r in range(N)]
+            for t in th:
+                t.start()
+            for t in th:
+                t.join()
+            med = max(times)
+            want = np.float32(N * (N + 1) // 2)
+            assert all(np.all(o.array == want) for _, o in bufs), "host allreduce result"
+            print(json.dumps(dict(config=f"C5 host allreduce f32 N={N} x {mib}MiB pinned, chunk {chunk}MiB",
+                                  ranks_share_one_gpu=N > 1, median_ms=round(med * 1e3, 3),
+                                  per_rank_gib_s=round(mib / 1024 / med, 3),
+                                  pcie_gb_s_all_ranks=round(2 * N * mib * MIB / med / 1e9, 2))), flush=True)
+        for s, o in bufs:
+            s.free()
+            o.free()
 
 
 if __name__ == "__main__":
