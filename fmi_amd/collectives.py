@@ -281,8 +281,8 @@ class CommAllreduce:
     def host_bench(self, n: int, iters: int = 3, chunk: int = 64 << 18) -> dict:
         """Config C5 (untimed diagnostic): fmi_comm_allreduce_host of an n-element f32 bucket in page-locked
         host memory on every rank — H2D, sharded allreduce and D2H pipelined in `chunk`-element pieces.
-        Returns the median wall time (max over ranks) and the per-rank host-bucket rate. 64 MiB chunks: with
-        torch's bundled HIP runtime, 16 MiB chunks measured 2x slower (49 vs 23.4 ms per GiB round trip)."""
+        Returns the median wall time (max over ranks) and the per-rank host-bucket rate. 64 MiB chunks: 16 MiB
+        chunks measured up to 2x slower on some boxes."""
         import statistics
         import time
 
