@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--backend", default="fmi", choices=["fmi", "torch"],
                     help="N>1 exchange driver: fmi = the C-ABI communicator fmi_comm_* (RCCL transport), "
                          "torch = torch.distributed collectives + our kernels on torch's stream")
+    ap.add_argument("--overlap-steps", action="store_true",
+                    help="N>1, fmi backend: run step k+1's local round on a second stream during step k's exchange")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-diagnostics", action="store_true", help="skip the untimed N>1 phase breakdown")
     ap.add_argument("--force-dist", action="store_true",
@@ -191,7 +193,11 @@ def main():
                 backend = "torch"
         if ar is None:
             ar = ShardedAllreduce(dist.group.WORLD, path=args.path, force_exchange=args.force_dist)
-        step_ms, kernel_ms, extra = ar.bench(n, steps=args.steps, warmup=args.warmup, sets=args.sets)
+        if isinstance(ar, CommAllreduce):
+            step_ms, kernel_ms, extra = ar.bench(n, steps=args.steps, warmup=args.warmup, sets=args.sets,
+                                                 overlap=args.overlap_steps)
+        else:
+            step_ms, kernel_ms, extra = ar.bench(n, steps=args.steps, warmup=args.warmup, sets=args.sets)
         extra["backend"] = backend
         if not args.no_diagnostics:
             # untimed diagnostics for the next optimisation round: the other exchange path's step time and
@@ -214,6 +220,11 @@ def main():
             extra["diagnostics"] = {f"ms_per_step_path_{other}": round(alt_ms, 5),
                                     "phase_ms": phase_breakdown(n, dist.group.WORLD)}
             if isinstance(ar, CommAllreduce):
+                # the other step schedule: local round of step k+1 overlapped with step k's exchange, or not
+                ov_ms, _, _ = ar.bench(n, steps=max(10, args.steps // 4), warmup=3, sets=args.sets,
+                                       overlap=not args.overlap_steps)
+                key = "ms_per_step_no_overlap" if args.overlap_steps else "ms_per_step_overlap_steps"
+                extra["diagnostics"][key] = round(ov_ms, 5)
                 # config C5: 1 GiB host (pinned) bucket per rank, H2D + allreduce + D2H pipelined
                 try:
                     extra["diagnostics"]["c5_host_allreduce_1GiB"] = ar.host_bench(GIB // 4)

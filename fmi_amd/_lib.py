@@ -68,6 +68,7 @@ SIGNATURES = {
     "fmi_event_create": (_i, [_c.POINTER(_vp)]),
     "fmi_event_destroy": (_i, [_vp]),
     "fmi_event_record": (_i, [_vp, _vp]),
+    "fmi_stream_wait_event": (_i, [_vp, _vp]),
     "fmi_event_sync": (_i, [_vp]),
     "fmi_event_elapsed_ms": (_i, [_c.POINTER(_c.c_float), _vp, _vp]),
     "fmi_dev_reduce_pair": (_i, [_i, _i, _vp, _vp, _sz, _vp]),

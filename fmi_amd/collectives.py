@@ -231,7 +231,11 @@ class CommAllreduce:
         dist.broadcast_object_list(box, src=0, group=self.group)
         self.comm = Comm(box[0], self.world, self.rank)
 
-    def bench(self, n: int, steps: int, warmup: int, sets: int = 2, peers_per_gpu: int = 2):
+    def bench(self, n: int, steps: int, warmup: int, sets: int = 2, peers_per_gpu: int = 2,
+              overlap: bool = False):
+        """overlap=True: the local round of step k+1 runs on a second stream while step k's exchange is
+        in flight (steps are independent: each reduces its own buffer set). Events order the reuse of a
+        set: its local round waits until the exchange that last read it has finished."""
         import time
 
         import numpy as np
@@ -241,16 +245,27 @@ class CommAllreduce:
         bufs = [[fdev.Bucket(n, np.float32).fill_synthetic(42 + s, peers_per_gpu * self.rank + j)
                  for j in range(peers_per_gpu)] for s in range(sets)]
         out = fdev.Bucket(n, np.float32)
+        side = fdev.Stream() if overlap else None
+        ready = [fdev.Event() for _ in range(sets)]
+        freed = [fdev.Event() for _ in range(sets)]
 
         def step(k, ev=None):
-            pair = bufs[k % sets]
+            s = k % sets
+            pair = bufs[s]
+            if overlap:
+                freed[s].wait_on(side)
             if ev:
-                ev[0].record()
+                ev[0].record(side)
             for b in pair[1:]:
-                fdev.reduce_pair(Op.SUM, pair[0], b)
+                fdev.reduce_pair(Op.SUM, pair[0], b, stream=side)
             if ev:
-                ev[1].record()
+                ev[1].record(side)
+            if overlap:
+                ready[s].record(side)
+                ready[s].wait_on(None)
             self.comm.allreduce(Op.SUM, pair[0], out, path=self._path)
+            if overlap:
+                freed[s].record(None)
 
         for k in range(warmup):
             step(k)
@@ -276,6 +291,11 @@ class CommAllreduce:
             "algbw_GiB_s": round((n * 4 / 2 ** 30) / (step_ms * 1e-3), 2),
             "busbw_GiB_s": round((n * 4 / 2 ** 30) / (step_ms * 1e-3) * 2 * (self.world - 1) / self.world, 2),
         }
+        if overlap:
+            extra["overlap_steps"] = True
+            side.destroy()
+        for e in ready + freed:
+            e.destroy()
         return step_ms, kernel_ms, extra
 
     def host_bench(self, n: int, iters: int = 3, chunk: int = 64 << 18) -> dict:
@@ -316,8 +336,8 @@ class CommAllreduce:
 def phase_breakdown(n: int, group=None, iters: int = 5) -> dict:
     """Untimed diagnostic for bench.py at N > 1: mean duration (ms, max over ranks) of each phase of the
     sharded allreduce of an n-element f32 bucket, measured with events on torch's stream — the local
-    pairwise round, the all-to-all, the fused shard kernel, the all-gather, and RCCL's reduce-scatter
-    (the alternative to all-to-all + kernel)."""
+    pairwise round, the all-to-all, the fused shard kernel, the all-gather, RCCL's reduce-scatter
+    (the alternative to all-to-all + kernel) and RCCL's whole-bucket allreduce (reference point)."""
     group = group if group is not None else dist.group.WORLD
     world = dist.get_world_size(group)
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -340,6 +360,8 @@ def phase_breakdown(n: int, group=None, iters: int = 5) -> dict:
         "shard_tree_kernel": lambda: eng.reduce_tree(Op.SUM, Alg.ALLREDUCE, red, parts, rank=0),
         "all_gather": lambda: dist.all_gather_into_tensor(out, red, group=group),
         "reduce_scatter": lambda: dist.reduce_scatter_tensor(red, a, group=group),
+        # RCCL's own whole-bucket allreduce: the floor for any exchange built from RCCL collectives
+        "rccl_allreduce_whole_bucket": lambda: dist.all_reduce(a, group=group),
     }
     result = {}
     for name, fn in phases.items():

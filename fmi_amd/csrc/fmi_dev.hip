@@ -391,6 +391,13 @@ int fmi_event_record(fmi_event_t event, fmi_stream_t stream) {
     return FMI_OK;
 }
 
+int fmi_stream_wait_event(fmi_stream_t stream, fmi_event_t event) {
+    if (!event) return fail(FMI_ERR_INVALID, "event is null");
+    if (int rc = require_device()) return rc;
+    FMI_HIP_TRY(hipStreamWaitEvent(resolve(stream), static_cast<hipEvent_t>(event), 0));
+    return FMI_OK;
+}
+
 int fmi_event_sync(fmi_event_t event) {
     if (!event) return fail(FMI_ERR_INVALID, "event is null");
     FMI_HIP_TRY(hipEventSynchronize(static_cast<hipEvent_t>(event)));

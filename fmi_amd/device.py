@@ -204,6 +204,10 @@ class Event:
     def sync(self) -> None:
         _lib.call("fmi_event_sync", self.handle)
 
+    def wait_on(self, stream=None) -> None:
+        """Make later work on `stream` (None = library stream) wait for this event."""
+        _lib.call("fmi_stream_wait_event", _sptr(stream), self.handle)
+
     def elapsed_ms(self, end: "Event") -> float:
         ms = ctypes.c_float()
         _lib.call("fmi_event_elapsed_ms", ctypes.byref(ms), self.handle, end.handle)

@@ -103,6 +103,9 @@ int fmi_event_create(fmi_event_t* event);
 int fmi_event_destroy(fmi_event_t event);
 int fmi_event_record(fmi_event_t event, fmi_stream_t stream);
 int fmi_event_sync(fmi_event_t event);
+/* Work enqueued on `stream` after this call waits for `event`'s last record (cross-stream ordering, e.g.
+ * a combine on one stream feeding a collective on another). */
+int fmi_stream_wait_event(fmi_stream_t stream, fmi_event_t event);
 int fmi_event_elapsed_ms(float* ms, fmi_event_t start, fmi_event_t stop);
 
 /* ---- the hot path ------------------------------------------------------------------------------ */

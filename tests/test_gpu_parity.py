@@ -123,6 +123,26 @@ def test_combine_out_of_place(device):
     assert_bit_equal(out.numpy(), orc.op_max(a, b))
 
 
+def test_stream_wait_event_orders_cross_stream_work(device):
+    """A combine on a side stream feeding a copy on the library stream (fmi_stream_wait_event): the copy
+    must see the combined bucket. 64 MiB so the combine is still running when the copy is enqueued."""
+    n = 16 << 20
+    a, b = Bucket(n, np.float32).fill_synthetic(3, 0), Bucket(n, np.float32).fill_synthetic(3, 1)
+    want = Bucket(n, np.float32)
+    fmi_amd.combine(Op.SUM, want, a, b)
+    fmi_amd.sync()
+    side, done = fmi_amd.Stream(), fmi_amd.Event()
+    out = Bucket(n, np.float32)
+    fmi_amd.reduce_pair(Op.SUM, a, b, stream=side)
+    done.record(side)
+    done.wait_on(None)
+    out.copy_from(a)
+    fmi_amd.sync()
+    assert_bit_equal(out.numpy(), want.numpy())
+    side.destroy()
+    done.destroy()
+
+
 def test_synthetic_matches_host_generator(device):
     for dtype in DTYPES:
         for peer in (0, 1, 7):
