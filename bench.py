@@ -55,7 +55,7 @@ def parse():
     ap.add_argument("--no-diagnostics", action="store_true", help="skip the untimed N>1 phase breakdown")
     ap.add_argument("--force-dist", action="store_true",
                     help="run the N>1 code path (RCCL exchange) even at world size 1 — plumbing check only")
-    ap.add_argument("--cpu-reps", type=int, default=7)
+    ap.add_argument("--cpu-reps", type=int, default=30, help="adapter combines timed (≈10 s of CPU work)")
     return ap.parse_args()
 
 

@@ -290,10 +290,10 @@ class Communicator:
             values = self._custom_values(mine)
             alg = Alg.REDUCE_LTR if ordered else Alg.ALLREDUCE
             return self._custom(f, t, values, _dev.schedule_expr(alg, self.num_peers, self.peer_id))
-        send, recv = Bucket.from_numpy(mine), Bucket(mine.size, mine.dtype)
-        self._comm.allreduce(Op(int(f.op)), send, recv, ordered=ordered)
-        _dev.sync()
-        return self._py(recv.numpy(), t)
+        # host buckets straight through the host-ingress pipeline (fmi_comm_allreduce_host)
+        recv = np.empty_like(mine)
+        self._comm.allreduce_host(Op(int(f.op)), np.ascontiguousarray(mine), recv, ordered=ordered)
+        return self._py(recv, t)
 
     def scan(self, data, f: func, t: types):
         mine = self._array(data, t)
