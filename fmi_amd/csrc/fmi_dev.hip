@@ -82,7 +82,10 @@ int launch_pair_vec(T* out, const T* a, const T* b, size_t n, hipStream_t s) {
     const size_t nvec = n / kVecLanes<T>;
     const size_t per_block = static_cast<size_t>(block) * static_cast<size_t>(unroll);
     const size_t ntiles = std::max<size_t>(1, (nvec + per_block - 1) / per_block);
-    if (variant == 1) {
+    // One-shot tiles unless the grid would pass HIP's 2^32-thread limit (buckets of > 2^31 tiles' worth):
+    // then the grid-stride form walks the tiles.
+    constexpr size_t kMaxGridThreads = size_t(1) << 31;
+    if (variant == 1 || ntiles * block > kMaxGridThreads) {
         const size_t cap = static_cast<size_t>(g_state.num_cus) * static_cast<size_t>(g_tune[FMI_TUNE_GRID_PER_CU].load());
         const unsigned grid = static_cast<unsigned>(std::max<size_t>(1, std::min(ntiles, cap)));
         switch (unroll) {

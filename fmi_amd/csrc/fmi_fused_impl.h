@@ -1,6 +1,7 @@
 // fmi_fused_impl.h — launch tables for the fused P-way kernels (included by one TU per algorithm).
 #pragma once
 
+#include <algorithm>
 #include <array>
 #include <type_traits>
 
@@ -21,10 +22,11 @@ using FusedFn = void (*)(const PeerPtrs&, size_t, int, hipStream_t);
 template <class Op, class T, int ALG, bool ALL_RANKS, int P>
 void fused_one(const PeerPtrs& ptrs, size_t n, int rank, hipStream_t s) {
     const size_t nvec = n / kVecLanes<T>;
+    const unsigned grid = static_cast<unsigned>(std::min<size_t>(grid_for(nvec, kFusedBlock), kFusedGridCap));
     if constexpr (ALG == sched::kScan || ALG == sched::kScanLtr)
-        scan_kernel<Op, T, ALG, P><<<grid_for(nvec, kFusedBlock), kFusedBlock, 0, s>>>(ptrs, n);
+        scan_kernel<Op, T, ALG, P><<<grid, kFusedBlock, 0, s>>>(ptrs, n);
     else
-        tree_kernel<Op, T, ALG, P, ALL_RANKS><<<grid_for(nvec, kFusedBlock), kFusedBlock, 0, s>>>(ptrs, n, rank);
+        tree_kernel<Op, T, ALG, P, ALL_RANKS><<<grid, kFusedBlock, 0, s>>>(ptrs, n, rank);
 }
 
 template <class Op, class T, int ALG, bool ALL_RANKS, int... I>

@@ -60,10 +60,10 @@ int launch_fused_reduce_ltr(int op, int dtype, int P, const PeerPtrs& ptrs, size
 int launch_fused_scan(int op, int dtype, int P, const PeerPtrs& ptrs, size_t n, hipStream_t s);
 int launch_fused_scan_ltr(int op, int dtype, int P, const PeerPtrs& ptrs, size_t n, hipStream_t s);
 
-inline unsigned grid_for(size_t items, unsigned block) {
-    size_t g = (items + block - 1) / block;
-    if (g == 0) g = 1;
-    return static_cast<unsigned>(g);
+// Workgroups to cover `items` with `block` threads each (at least 1). Callers cap it before narrowing.
+inline size_t grid_for(size_t items, unsigned block) {
+    const size_t g = (items + block - 1) / block;
+    return g == 0 ? 1 : g;
 }
 
 }  // namespace fmi::dev

@@ -249,12 +249,17 @@ __device__ __forceinline__ void tree_group(const PeerPtrs& ptrs, int rank, size_
     store_lanes<kFusedNT, T, W>(static_cast<T*>(ptrs.out[0]) + elem, r);
 }
 
+// Launched with one thread per 16-B lane group up to kFusedGridCap workgroups; beyond that (buckets of
+// > 2^30 lane groups) each thread strides over the rest, so the grid never exceeds HIP's 2^32-thread limit.
+inline constexpr size_t kFusedGridCap = size_t(1) << 22;
+
 template <class Op, class T, int ALG, int P, bool ALL_RANKS>
 __global__ void __launch_bounds__(256) tree_kernel(PeerPtrs ptrs, size_t n, int rank) {
     constexpr int W = kVecLanes<T>;
     const size_t nvec = n / W;
-    const size_t g = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (g < nvec) tree_group<Op, T, ALG, P, ALL_RANKS, W>(ptrs, rank, g * W);
+    const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
+    for (size_t g = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x; g < nvec; g += stride)
+        tree_group<Op, T, ALG, P, ALL_RANKS, W>(ptrs, rank, g * W);
     const size_t first = nvec * W;
     if (blockIdx.x == 0 && first + threadIdx.x < n) tree_group<Op, T, ALG, P, ALL_RANKS, 1>(ptrs, rank, first + threadIdx.x);
 }
@@ -271,8 +276,9 @@ template <class Op, class T, int ALG, int P>
 __global__ void __launch_bounds__(256) scan_kernel(PeerPtrs ptrs, size_t n) {
     constexpr int W = kVecLanes<T>;
     const size_t nvec = n / W;
-    const size_t g = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (g < nvec) scan_group<Op, T, ALG, P, W>(ptrs, g * W);
+    const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
+    for (size_t g = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x; g < nvec; g += stride)
+        scan_group<Op, T, ALG, P, W>(ptrs, g * W);
     const size_t first = nvec * W;
     if (blockIdx.x == 0 && first + threadIdx.x < n) scan_group<Op, T, ALG, P, 1>(ptrs, first + threadIdx.x);
 }

@@ -341,3 +341,40 @@ def test_c3_8peer_f32_scan_64mib(device):
     want, _ = orc.scan([orc.synthetic(np.float32, n, 42, p) for p in range(P)], orc.op_sum)
     for k in range(P):
         assert_bit_equal(outs[k].numpy(), want[k], f"C3 scan peer {k}")
+
+
+def test_beyond_2pow32_elements_64bit_indexing(device):
+    """Maximum sizes: buckets of 2^32 + 1029 f32 elements (16 GiB each) through the pairwise, fused tree and
+    peer-scan kernels. Every launch index is 64-bit; windows around 2^31 and 2^32 and the ragged tail are
+    compared with the oracle's synthetic values."""
+    from fmi_amd import Alg
+
+    n = (1 << 32) + 1029
+    windows = [(0, 4096), ((1 << 31) - 2048, 4096), ((1 << 32) - 2048, 4096), (n - 4096, 4096)]
+
+    def host(peer, lo, m):
+        return orc.synthetic_at(np.float32, np.arange(lo, lo + m, dtype=np.uint64), 42, peer)
+
+    ins = [Bucket(n, np.float32).fill_synthetic(42, p) for p in range(3)]
+    out = Bucket(n, np.float32)
+    fmi_amd.reduce_tree(Op.SUM, Alg.ALLREDUCE, out, ins)
+    fmi_amd.sync()
+    for lo, m in windows:
+        want, _ = orc.allreduce([host(p, lo, m) for p in range(3)], orc.op_sum)
+        assert_bit_equal(out.view(lo, m).numpy(), want[0], f"tree window {lo}")
+    scan_out = [out, Bucket(n, np.float32)]
+    fmi_amd.scan_peers(Op.SUM, Alg.SCAN, scan_out, ins[:2])
+    fmi_amd.sync()
+    for lo, m in windows:
+        want, _ = orc.scan([host(p, lo, m) for p in range(2)], orc.op_sum)
+        for k in range(2):
+            assert_bit_equal(scan_out[k].view(lo, m).numpy(), want[k], f"scan peer {k} window {lo}")
+    scan_out[1].free()
+    out.free()
+    ins[2].free()
+    fmi_amd.reduce_pair(Op.SUM, ins[0], ins[1])
+    fmi_amd.sync()
+    for lo, m in windows:
+        assert_bit_equal(ins[0].view(lo, m).numpy(), host(0, lo, m) + host(1, lo, m), f"pair window {lo}")
+    for b in ins[:2]:
+        b.free()
