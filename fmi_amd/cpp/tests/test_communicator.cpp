@@ -690,8 +690,15 @@ GPU_TEST(rccl_channel_host_ingress_local_transport) {
     Dev::init(0);
     for (peer_num P : {2u, 3u, 8u}) {
         const std::size_t n = 200003;
-        std::vector<std::vector<float>> host_ar(P), host_sc(P), dev_ar(P), dev_send(P), dev_sc(P);
+        std::vector<std::vector<float>> host_ar(P), host_sc(P), dev_ar(P), dev_send(P), dev_sc(P), host_ord(P),
+            dev_ord(P);
         std::vector<float> host_red, dev_red;
+        auto ordered_sum = [] {
+            Function<std::vector<float>> f(Op::sum);
+            f.commutative = false;
+            f.associative = false;
+            return f;
+        };
         with_peers(P, [&](Communicator& c, peer_num p) {
             Data<std::vector<float>> a(synth_f32(n, 8, p)), r(n);
             c.allreduce(a, r, Function<std::vector<float>>(Op::sum));
@@ -702,6 +709,9 @@ GPU_TEST(rccl_channel_host_ingress_local_transport) {
             Data<std::vector<float>> d(synth_f32(n, 8, p)), dr(n);
             c.reduce(d, dr, P - 1, Function<std::vector<float>>(Op::sum));
             if (p == P - 1) host_red = dr.get();
+            Data<std::vector<float>> o(synth_f32(n, 8, p)), orr(n);
+            c.allreduce(o, orr, ordered_sum());
+            host_ord[p] = orr.get();
         });
         auto mailbox = std::make_shared<FMI::Comm::Mailbox>();
         std::vector<std::thread> ts;
@@ -726,6 +736,9 @@ GPU_TEST(rccl_channel_host_ingress_local_transport) {
                     Data<std::vector<float>> d(synth_f32(n, 8, p)), dr(n);
                     c.reduce(d, dr, P - 1, Function<std::vector<float>>(Op::sum));
                     if (p == P - 1) dev_red = dr.get();
+                    Data<std::vector<float>> o(synth_f32(n, 8, p)), orr(n);
+                    c.allreduce(o, orr, ordered_sum());  // reduce_ltr order through the host pipeline
+                    dev_ord[p] = orr.get();
                     Data<std::vector<int64_t>> b(std::vector<int64_t>{static_cast<int64_t>(p), 9});
                     c.bcast(b, P - 1);
                     if (b.get()[0] != static_cast<int64_t>(P - 1)) throw std::runtime_error("host bcast over Rccl");
@@ -749,6 +762,7 @@ GPU_TEST(rccl_channel_host_ingress_local_transport) {
             CHECK(std::memcmp(host_ar[p].data(), dev_ar[p].data(), n * 4) == 0);
             CHECK(std::memcmp(dev_send[p].data(), dev_ar[p].data(), n * 4) == 0);  // sendbuf = result
             CHECK(std::memcmp(host_sc[p].data(), dev_sc[p].data(), n * 4) == 0);
+            CHECK(std::memcmp(host_ord[p].data(), dev_ord[p].data(), n * 4) == 0);
         }
         CHECK(host_red.size() == n && dev_red.size() == n && std::memcmp(host_red.data(), dev_red.data(), n * 4) == 0);
     }
