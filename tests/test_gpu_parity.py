@@ -350,7 +350,7 @@ def test_beyond_2pow32_elements_64bit_indexing(device):
     from fmi_amd import Alg
 
     n = (1 << 32) + 1029
-    windows = [(0, 4096), ((1 << 31) - 2048, 4096), ((1 << 32) - 2048, 4096), (n - 4096, 4096)]
+    windows = [(0, 4096), ((1 << 31) - 2048, 4096), ((1 << 32) - 2048, 3000), (n - 4096, 4096)]
 
     def host(peer, lo, m):
         return orc.synthetic_at(np.float32, np.arange(lo, lo + m, dtype=np.uint64), 42, peer)
