@@ -44,8 +44,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--bucket-mib", type=int, default=256)
     ap.add_argument("--sets", type=int, default=4, help="rotating bucket sets (defeats the 256 MiB MALL)")
-    ap.add_argument("--path", default="tree", choices=["tree", "rccl"],
-                    help="N>1 exchange: tree = all-to-all + fused kernel (bit-exact), rccl = reduce-scatter")
+    ap.add_argument("--path", default="tree", choices=["tree", "rccl", "direct"],
+                    help="N>1 exchange: tree = all-to-all + fused kernel (bit-exact), rccl = reduce-scatter, "
+                         "direct = fused kernel over IPC-mapped peer windows (bit-exact, fmi backend only)")
     ap.add_argument("--backend", default="fmi", choices=["fmi", "torch"],
                     help="N>1 exchange driver: fmi = the C-ABI communicator fmi_comm_* (RCCL transport), "
                          "torch = torch.distributed collectives + our kernels on torch's stream")
@@ -225,6 +226,19 @@ def main():
                                        overlap=not args.overlap_steps)
                 key = "ms_per_step_no_overlap" if args.overlap_steps else "ms_per_step_overlap_steps"
                 extra["diagnostics"][key] = round(ov_ms, 5)
+                # path DIRECT (xGMI reads of IPC-mapped peer windows): bit-identical to TREE? and its step time
+                if args.path != "direct":
+                    saved = ar._path
+                    try:
+                        ok = ar.check_direct(1 << 20)
+                        ar._path = Path.DIRECT
+                        d_ms, _, _ = ar.bench(n, steps=max(10, args.steps // 4), warmup=3, sets=min(2, args.sets))
+                        extra["diagnostics"]["path_direct"] = {"bit_identical_to_tree": ok,
+                                                               "ms_per_step": round(d_ms, 5)}
+                    except Exception as e:  # window setup fails on every rank alike (all-or-nothing)
+                        extra["diagnostics"]["path_direct"] = f"unavailable: {e}"
+                    finally:
+                        ar._path = saved
                 # config C5: 1 GiB host (pinned) bucket per rank, H2D + allreduce + D2H pipelined
                 try:
                     extra["diagnostics"]["c5_host_allreduce_1GiB"] = ar.host_bench(GIB // 4)
@@ -235,8 +249,11 @@ def main():
         algo_bytes = extra.pop("kernel_algo_bytes")
         workload = (f"C4-shaped: {2 * world}-peer float32 sum-allreduce of 256 MiB buckets, 2 peers per GPU, "
                     f"sharded over {world} GPUs")
-        parallelism = f"shard{world} ({args.path}: all-to-all + fused tree + all-gather over RCCL)" \
-            if args.path == "tree" else f"shard{world} (RCCL reduce-scatter + all-gather)"
+        parallelism = {
+            "tree": f"shard{world} (tree: all-to-all + fused tree + all-gather over RCCL)",
+            "rccl": f"shard{world} (RCCL reduce-scatter + all-gather)",
+            "direct": f"shard{world} (direct: fused tree over IPC-mapped peer windows + direct gather, xGMI)",
+        }[args.path]
 
     kernel_avg_ms = float(sum(kernel_ms) / len(kernel_ms))
     value = args.gpus * (nbytes / GIB) / (step_ms * 1e-3)

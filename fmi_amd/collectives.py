@@ -224,7 +224,7 @@ class CommAllreduce:
         self.world = dist.get_world_size(self.group)
         self.rank = dist.get_rank(self.group)
         self.path = path
-        self._path = Path.TREE if path == "tree" else Path.RCCL
+        self._path = {"tree": Path.TREE, "rccl": Path.RCCL, "direct": Path.DIRECT}[path]
         _lib.load()
         _lib.call("fmi_dev_init", torch.cuda.current_device())
         box = [unique_id(Transport.RCCL) if self.rank == 0 else None]
@@ -242,8 +242,16 @@ class CommAllreduce:
 
         from . import device as fdev
 
-        bufs = [[fdev.Bucket(n, np.float32).fill_synthetic(42 + s, peers_per_gpu * self.rank + j)
-                 for j in range(peers_per_gpu)] for s in range(sets)]
+        from .comm import Path
+
+        direct = self._path == Path.DIRECT  # the reduced bucket must live in a symmetric window
+
+        def first(s):
+            b = self.comm.window(n, np.float32) if direct else fdev.Bucket(n, np.float32)
+            return b.fill_synthetic(42 + s, peers_per_gpu * self.rank)
+
+        bufs = [[first(s)] + [fdev.Bucket(n, np.float32).fill_synthetic(42 + s, peers_per_gpu * self.rank + j)
+                              for j in range(1, peers_per_gpu)] for s in range(sets)]
         out = fdev.Bucket(n, np.float32)
         side = fdev.Stream() if overlap else None
         ready = [fdev.Event() for _ in range(sets)]
@@ -296,7 +304,29 @@ class CommAllreduce:
             side.destroy()
         for e in ready + freed:
             e.destroy()
+        if direct:
+            fdev.sync()
+            for pair in bufs:
+                self.comm.window_free(pair[0])
         return step_ms, kernel_ms, extra
+
+    def check_direct(self, n: int) -> bool:
+        """Path DIRECT against path TREE on the same window bucket: bit-identical on every rank?"""
+        import numpy as np
+
+        from . import device as fdev
+        from .comm import Path
+
+        w = self.comm.window(n, np.float32).fill_synthetic(5, self.rank)
+        a, b = fdev.Bucket(n, np.float32), fdev.Bucket(n, np.float32)
+        self.comm.allreduce(Op.SUM, w, a, path=Path.TREE)
+        self.comm.allreduce(Op.SUM, w, b, path=Path.DIRECT)
+        fdev.sync()
+        same = bool(np.array_equal(a.numpy().view(np.uint32), b.numpy().view(np.uint32)))
+        self.comm.window_free(w)
+        flag = torch.tensor([1 if same else 0], dtype=torch.int32, device=torch.cuda.current_device())
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)
+        return bool(flag.item())
 
     def host_bench(self, n: int, iters: int = 3, chunk: int = 64 << 18) -> dict:
         """Config C5 (untimed diagnostic): fmi_comm_allreduce_host of an n-element f32 bucket in page-locked

@@ -14,7 +14,7 @@ from typing import Optional
 from . import _lib
 import numpy as np
 
-from .device import Alg, Bucket, Op, _sptr, dtype_of
+from .device import NP_DTYPE, Alg, Bucket, Op, _sptr, dtype_of
 
 ID_BYTES = 128
 
@@ -27,6 +27,7 @@ class Transport(enum.IntEnum):
 class Path(enum.IntEnum):
     TREE = 0  # all-to-all + fused kernel in the reference's order + all-gather (bit-exact)
     RCCL = 1  # RCCL reduce-scatter + all-gather (RCCL's order)
+    DIRECT = 2  # fused kernel reading every rank's window over xGMI + direct gather (bit-exact, windows only)
 
 
 def unique_id(transport: Transport = Transport.RCCL) -> bytes:
@@ -69,6 +70,18 @@ class Comm:
         alg = Alg.REDUCE_LTR if ordered else Alg.ALLREDUCE
         _lib.call("fmi_comm_allreduce", self.handle, int(op), int(send.dtype), int(alg), int(path), _p(send), _p(recv),
                   send.n, _sptr(stream))
+
+    def window(self, n: int, dtype) -> Bucket:
+        """A symmetric window bucket for Path.DIRECT (collective: every rank, same n and dtype). Release it
+        with window_free (collective) or with the communicator."""
+        nbytes = int(n) * np.dtype(NP_DTYPE[dtype_of(dtype)]).itemsize
+        p = ctypes.c_void_p()
+        _lib.call("fmi_comm_window_alloc", self.handle, nbytes, ctypes.byref(p))
+        return Bucket(n, dtype, ptr=p.value)
+
+    def window_free(self, b: Bucket) -> None:
+        _lib.call("fmi_comm_window_free", self.handle, b.ptr)
+        b.ptr = 0
 
     def allreduce_host(self, op: Op, send: np.ndarray, recv: np.ndarray, ordered: bool = False,
                        path: Path = Path.TREE, chunk: int = 0) -> None:

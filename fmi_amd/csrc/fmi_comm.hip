@@ -139,6 +139,13 @@ public:
     virtual int send(const char* buf, size_t bytes, int peer, hipStream_t s) = 0;
     virtual int recv(char* buf, size_t bytes, int peer, hipStream_t s) = 0;
     virtual int barrier(hipStream_t s) = 0;
+    // Stream-ordered barrier: work enqueued on s after it starts only once every rank has reached it.
+    virtual int barrier_async(hipStream_t s) = 0;
+    // Symmetric window: map every rank's `base` into this process (peers[j] = rank j's base, peers[rank] =
+    // base). Collective, and all-or-nothing: `ok` is this rank's own readiness (its allocation succeeded);
+    // every rank returns FMI_OK only if every rank could export and map, so no rank is left waiting.
+    virtual int map_window(char* base, bool ok, std::vector<char*>& peers, hipStream_t s) = 0;
+    virtual void unmap_window(const std::vector<char*>& peers) = 0;
     virtual int reduce_scatter(int, int, const void*, void*, size_t, hipStream_t) {
         return fail(FMI_ERR_UNSUPPORTED, "path RCCL needs the RCCL transport");
     }
@@ -239,6 +246,54 @@ public:
     int reduce_scatter(int op, int dtype, const void* send, void* recv, size_t count, hipStream_t s) override {
         FMI_NCCL(api_, ReduceScatter(send, recv, count, nccl_type(dtype), nccl_op(op), comm_, s));
         return FMI_OK;
+    }
+    int barrier_async(hipStream_t s) override {
+        if (!token_) FMI_COMM_HIP(hipMalloc(&token_, sizeof(int)));
+        FMI_NCCL(api_, AllReduce(token_, token_, 1, ncclInt32, ncclSum, comm_, s));
+        return FMI_OK;
+    }
+    // IPC handles travel by all-gather; the peer mappings are opened with lazy peer access (xGMI). A final
+    // all-reduce(min) of every rank's success flag makes the outcome identical on all ranks.
+    int map_window(char* base, bool ok, std::vector<char*>& peers, hipStream_t s) override {
+        constexpr size_t H = sizeof(hipIpcMemHandle_t);
+        hipIpcMemHandle_t mine{};
+        if (ok) ok = hipIpcGetMemHandle(&mine, base) == hipSuccess;
+        char* d = nullptr;
+        FMI_COMM_HIP(hipMalloc(&d, (n_ + 1) * H + 2 * sizeof(int)));
+        std::vector<hipIpcMemHandle_t> all(n_);
+        int flag = 0;
+        int rc = [&]() -> int {
+            FMI_COMM_HIP(hipMemcpyAsync(d + n_ * H, &mine, H, hipMemcpyHostToDevice, s));
+            FMI_NCCL(api_, AllGather(d + n_ * H, d, H, ncclUint8, comm_, s));
+            FMI_COMM_HIP(hipMemcpyAsync(all.data(), d, n_ * H, hipMemcpyDeviceToHost, s));
+            FMI_COMM_HIP(hipStreamSynchronize(s));
+            peers.assign(n_, nullptr);
+            peers[rank_] = base;
+            for (int j = 0; j < n_ && ok; ++j) {
+                if (j == rank_) continue;
+                void* p = nullptr;
+                if (hipIpcOpenMemHandle(&p, all[j], hipIpcMemLazyEnablePeerAccess) != hipSuccess) ok = false;
+                peers[j] = static_cast<char*>(p);
+            }
+            int* f = reinterpret_cast<int*>(d + (n_ + 1) * H);
+            const int mine_ok = ok ? 1 : 0;
+            FMI_COMM_HIP(hipMemcpyAsync(f, &mine_ok, sizeof(int), hipMemcpyHostToDevice, s));
+            FMI_NCCL(api_, AllReduce(f, f + 1, 1, ncclInt32, ncclMin, comm_, s));
+            FMI_COMM_HIP(hipMemcpyAsync(&flag, f + 1, sizeof(int), hipMemcpyDeviceToHost, s));
+            FMI_COMM_HIP(hipStreamSynchronize(s));
+            return FMI_OK;
+        }();
+        (void)hipFree(d);
+        if (rc != FMI_OK || flag != 1) {
+            unmap_window(peers);
+            peers.clear();
+            return rc != FMI_OK ? rc : fail(FMI_ERR_COMM, "window: a rank could not export or map its window (IPC)");
+        }
+        return FMI_OK;
+    }
+    void unmap_window(const std::vector<char*>& peers) override {
+        for (int j = 0; j < static_cast<int>(peers.size()); ++j)
+            if (j != rank_ && peers[j]) (void)hipIpcCloseMemHandle(peers[j]);
     }
 
 private:
@@ -356,6 +411,26 @@ public:
         hub_->barrier();
         return FMI_OK;
     }
+    int barrier_async(hipStream_t s) override { return barrier(s); }
+    // Ranks share the process and the device: the window pointers themselves are the mapping.
+    int map_window(char* base, bool ok, std::vector<char*>& peers, hipStream_t s) override {
+        bool all_ok = true;
+        const int rc = exchange(ok ? base : nullptr, s, [&](const std::vector<const char*>& all) -> int {
+            peers.assign(n_, nullptr);
+            for (int j = 0; j < n_; ++j) {
+                peers[j] = const_cast<char*>(all[j]);
+                if (!all[j]) all_ok = false;
+            }
+            return FMI_OK;
+        });
+        if (rc != FMI_OK) return rc;
+        if (!all_ok) {
+            peers.clear();
+            return fail(FMI_ERR_ALLOC, "window: a rank could not allocate its window");
+        }
+        return FMI_OK;
+    }
+    void unmap_window(const std::vector<char*>&) override {}
 
 private:
     // Publish my buffer, wait for everyone, run `work` over all ranks' buffers, wait until everyone's
@@ -411,6 +486,13 @@ struct HostPipe {
     }
 };
 
+// A symmetric window (fmi_comm_window_alloc): 2 * bytes per rank — the caller's bucket area [0, bytes)
+// and the reduced-shard area [bytes, 2 * bytes) — mapped into every rank's address space.
+struct Window {
+    size_t bytes = 0;
+    std::vector<char*> peers;  // peers[j] = rank j's window base, as seen from this rank
+};
+
 struct Comm {
     static constexpr int kSlots = 8;  // 0-3: collective scratch; 4-7: host-pipeline chunk slots
     std::unique_ptr<Transport> t;
@@ -418,11 +500,27 @@ struct Comm {
     void* buf[kSlots] = {};
     size_t cap[kSlots] = {};
     HostPipe pipe;
+    std::map<char*, Window> windows;  // keyed by this rank's base
 
     ~Comm() {
         if (pipe.cs) (void)hipStreamSynchronize(pipe.cs);
         for (void* b : buf)
             if (b) (void)hipFree(b);
+        for (auto& [base, w] : windows) {
+            t->unmap_window(w.peers);
+            (void)hipFree(base);
+        }
+    }
+
+    // The window holding [p, p + len), or nullptr.
+    const Window* window_of(const void* p, size_t len, size_t* offset) const {
+        const char* c = static_cast<const char*>(p);
+        auto it = windows.upper_bound(const_cast<char*>(c));
+        if (it == windows.begin()) return nullptr;
+        --it;
+        if (c < it->first || c + len > it->first + it->second.bytes) return nullptr;
+        *offset = static_cast<size_t>(c - it->first);
+        return &it->second;
     }
 
     // scratch slot k of at least `bytes` (grown after draining the stream that used it)
@@ -471,6 +569,70 @@ int padded_source(Comm* c, size_t n, size_t padded, size_t esz, const void* send
     return FMI_OK;
 }
 
+// recv[i] = (reduced-shard area of the rank owning element i)[i], for the byte range [0, nbytes): 16-B
+// nontemporal accesses over xGMI when every pointer is 16-B aligned, bytes otherwise. Shards are whole
+// multiples of 256 B, so a 16-B group never straddles two owners.
+template <bool VEC>
+__global__ void __launch_bounds__(256) gather_shards(PeerPtrs src, char* dst, size_t nbytes, size_t shard_bytes) {
+    const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
+    const size_t first = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if constexpr (VEC) {
+        const size_t nvec = nbytes / 16;
+        for (size_t g = first; g < nvec; g += stride) {
+            const size_t b = g * 16;
+            const auto* from = reinterpret_cast<const u32x4*>(static_cast<const char*>(src.in[b / shard_bytes]) + b);
+            __builtin_nontemporal_store(__builtin_nontemporal_load(from), reinterpret_cast<u32x4*>(dst + b));
+        }
+        if (blockIdx.x == 0 && nvec * 16 + threadIdx.x < nbytes) {
+            const size_t b = nvec * 16 + threadIdx.x;
+            dst[b] = static_cast<const char*>(src.in[b / shard_bytes])[b];
+        }
+    } else {
+        for (size_t b = first; b < nbytes; b += stride) dst[b] = static_cast<const char*>(src.in[b / shard_bytes])[b];
+    }
+}
+
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+// Path DIRECT: no staging and no all-to-all. Rank k's fused kernel reads shard k of every rank's window
+// over xGMI and reduces it in the reference's order into its reduced-shard area; every rank then gathers
+// the N reduced shards straight from the peers' windows. Two stream-ordered barriers: before the reduce
+// (every bucket written) and before the gather (every shard reduced). The next call's first barrier keeps
+// a rank from overwriting its reduced shard while a peer still gathers it.
+int allreduce_direct(Comm* c, const Window& w, size_t off, int op, int dtype, int alg, void* recv, size_t n,
+                     hipStream_t s) {
+    const int N = c->t->n();
+    const int k = c->t->rank();
+    const size_t esz = dtype_size(dtype);
+    if (N > sched::kMaxFusedPeers)
+        return fail(FMI_ERR_UNSUPPORTED, "path DIRECT supports up to " + std::to_string(sched::kMaxFusedPeers) + " ranks");
+    const size_t shard = shard_elems(n, N);
+    FMI_COMM_RC(c->t->barrier_async(s));
+    const size_t lo = std::min(n, static_cast<size_t>(k) * shard);
+    const size_t len = std::min(shard, n - lo);
+    if (len > 0) {
+        std::vector<const void*> ins(N);
+        for (int j = 0; j < N; ++j) ins[j] = w.peers[j] + off + lo * esz;
+        char* out = w.peers[k] + w.bytes + off + lo * esz;
+        FMI_COMM_RC(fmi_dev_reduce_tree(op, dtype, alg, out, ins.data(), N, 0, len, s));
+    }
+    FMI_COMM_RC(c->t->barrier_async(s));
+    PeerPtrs src{};
+    bool vec = aligned16(recv);
+    for (int j = 0; j < N; ++j) {
+        src.in[j] = w.peers[j] + w.bytes + off;
+        vec = vec && aligned16(src.in[j]);
+    }
+    const size_t nbytes = n * esz;
+    const unsigned grid = static_cast<unsigned>(std::min<size_t>(grid_for(vec ? nbytes / 16 : nbytes, 256), 1u << 20));
+    if (vec)
+        gather_shards<true><<<grid, 256, 0, s>>>(src, static_cast<char*>(recv), nbytes, shard * esz);
+    else
+        gather_shards<false><<<grid, 256, 0, s>>>(src, static_cast<char*>(recv), nbytes, shard * esz);
+    FMI_COMM_HIP(hipGetLastError());
+    return FMI_OK;
+}
+
 // The sharded allreduce of one device bucket on stream s (caller holds c->mu; arguments validated).
 int allreduce_device(Comm* c, int op, int dtype, int alg, int path, const void* send, void* recv, size_t n,
                      hipStream_t s) {
@@ -479,6 +641,12 @@ int allreduce_device(Comm* c, int op, int dtype, int alg, int path, const void* 
     if (N == 1) {  // reference P = 1: a copy
         if (send != recv) FMI_COMM_HIP(hipMemcpyAsync(recv, send, n * esz, hipMemcpyDeviceToDevice, s));
         return FMI_OK;
+    }
+    if (path == FMI_PATH_DIRECT) {
+        size_t off = 0;
+        const Window* w = c->window_of(send, n * esz, &off);
+        if (!w) return fail(FMI_ERR_INVALID, "path DIRECT: send must lie inside a window from fmi_comm_window_alloc");
+        return allreduce_direct(c, *w, off, op, dtype, alg, recv, n, s);
     }
     const size_t shard = shard_elems(n, N);
     const size_t padded = shard * N;
@@ -507,7 +675,8 @@ int allreduce_device(Comm* c, int op, int dtype, int alg, int path, const void* 
 int check_allreduce_args(int alg, int path) {
     if (alg != FMI_ALG_ALLREDUCE && alg != FMI_ALG_REDUCE_LTR)
         return fail(FMI_ERR_INVALID, "allreduce: alg must be ALLREDUCE or REDUCE_LTR");
-    if (path != FMI_PATH_TREE && path != FMI_PATH_RCCL) return fail(FMI_ERR_INVALID, "unknown path");
+    if (path != FMI_PATH_TREE && path != FMI_PATH_RCCL && path != FMI_PATH_DIRECT)
+        return fail(FMI_ERR_INVALID, "unknown path");
     if (path == FMI_PATH_RCCL && alg != FMI_ALG_ALLREDUCE)
         return fail(FMI_ERR_INVALID, "ordered (LTR) allreduce needs the tree path");
     return FMI_OK;
@@ -580,6 +749,40 @@ int fmi_comm_size(fmi_comm_t comm, int* nranks, int* rank) {
     Comm* c = static_cast<Comm*>(comm);
     *nranks = c->t->n();
     *rank = c->t->rank();
+    return FMI_OK;
+}
+
+int fmi_comm_window_alloc(fmi_comm_t comm, size_t bytes, void** ptr) {
+    if (!comm || !ptr) return fail(FMI_ERR_INVALID, "null argument");
+    if (!library_stream()) return fail(FMI_ERR_NO_DEVICE, "fmi_dev_init has not been called");
+    Comm* c = static_cast<Comm*>(comm);
+    std::lock_guard<std::mutex> lk(c->mu);
+    bytes = std::max<size_t>(256, (bytes + 255) / 256 * 256);
+    char* base = nullptr;
+    const bool ok = hipMalloc(&base, 2 * bytes) == hipSuccess;
+    Window w;
+    w.bytes = bytes;
+    const int rc = c->t->map_window(ok ? base : nullptr, ok, w.peers, library_stream());
+    if (rc != FMI_OK) {
+        if (base) (void)hipFree(base);
+        return rc;
+    }
+    c->windows[base] = std::move(w);
+    *ptr = base;
+    return FMI_OK;
+}
+
+int fmi_comm_window_free(fmi_comm_t comm, void* ptr) {
+    if (!comm || !ptr) return fail(FMI_ERR_INVALID, "null argument");
+    Comm* c = static_cast<Comm*>(comm);
+    std::lock_guard<std::mutex> lk(c->mu);
+    auto it = c->windows.find(static_cast<char*>(ptr));
+    if (it == c->windows.end()) return fail(FMI_ERR_INVALID, "not a window of this communicator");
+    // no peer may still be reading it
+    FMI_COMM_RC(c->t->barrier(library_stream()));
+    c->t->unmap_window(it->second.peers);
+    FMI_COMM_HIP(hipFree(it->first));
+    c->windows.erase(it);
     return FMI_OK;
 }
 

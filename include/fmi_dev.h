@@ -163,7 +163,11 @@ int fmi_host_reduce_pair(int op, int dtype, void* inout, const void* in, size_t 
 #define FMI_COMM_ID_BYTES 128
 typedef void* fmi_comm_t;
 typedef enum { FMI_TRANSPORT_RCCL = 0, FMI_TRANSPORT_LOCAL = 1 } fmi_transport_t;
-typedef enum { FMI_PATH_TREE = 0, FMI_PATH_RCCL = 1 } fmi_path_t;
+/* FMI_PATH_DIRECT: no RCCL data movement. `send` must lie in a window (fmi_comm_window_alloc, same offset on
+ * every rank); rank k's fused kernel reads shard k of every rank's window over xGMI (IPC-mapped peer
+ * memory) and reduces it in the reference's order, then every rank reads the N reduced shards from the
+ * peers' windows. Bit-identical to FMI_PATH_TREE; up to 16 ranks. */
+typedef enum { FMI_PATH_TREE = 0, FMI_PATH_RCCL = 1, FMI_PATH_DIRECT = 2 } fmi_path_t;
 
 /* A fresh communicator id (FMI_COMM_ID_BYTES) made by one rank and handed to the others by any host
  * channel (FMI: Communicator::bcast over the host channel, reference include/Communicator.h:43-47). */
@@ -171,6 +175,13 @@ int fmi_comm_unique_id(int transport, void* id, size_t len);
 int fmi_comm_init(fmi_comm_t* comm, const void* id, int nranks, int rank);
 int fmi_comm_destroy(fmi_comm_t comm);
 int fmi_comm_size(fmi_comm_t comm, int* nranks, int* rank);
+/* Symmetric window for FMI_PATH_DIRECT (collective: every rank calls it with the same `bytes`). Returns a
+ * device bucket of `bytes` that every peer of the communicator can read directly (RCCL transport: HIP IPC
+ * handles exchanged by all-gather, mapped with peer access over xGMI). All-or-nothing: if any rank cannot
+ * allocate, export or map, every rank gets an error. Freed (collectively) by fmi_comm_window_free or with
+ * the communicator. */
+int fmi_comm_window_alloc(fmi_comm_t comm, size_t bytes, void** ptr);
+int fmi_comm_window_free(fmi_comm_t comm, void* ptr);
 /* alg: FMI_ALG_ALLREDUCE (commutative+associative) or FMI_ALG_REDUCE_LTR (ordered) */
 int fmi_comm_allreduce(fmi_comm_t comm, int op, int dtype, int alg, int path, const void* send, void* recv, size_t n,
                        fmi_stream_t stream);

@@ -167,6 +167,65 @@ def test_comm_allreduce_host_default_chunk_matches_device(device):
         assert_bit_equal(got, dev, f"rank {r}")
 
 
+@pytest.mark.parametrize("N", [2, 3, 4, 8])
+def test_comm_allreduce_direct_windows(device, N):
+    """Path DIRECT: every rank's fused kernel reads its shard of all windows in place and the reduced shards
+    are gathered from the peers' windows. Bit-exact vs the oracle; windows reused across calls; recv
+    aliasing the window; a bucket at an offset inside the window (aligned and unaligned)."""
+    for n in (1, 1027, 3 * 65536 + 5):
+        for dtype, op in ((np.float32, Op.SUM), (np.int64, Op.PROD), (np.float64, Op.MAX), (np.int32, Op.MIN)):
+            xs = [inputs(dtype, n, r, seed=17) for r in range(N)]
+
+            def body(c, r):
+                w = c.window(n + 65, dtype)
+                out = Bucket(n, dtype)
+                res = []
+                for off in (0, 64, 1):  # 64 elements keeps 16-B alignment, 1 does not
+                    v = w.view(off, n)
+                    v.upload(xs[r])
+                    for _ in range(2):
+                        c.allreduce(op, v, out, path=Path.DIRECT)
+                    fmi_amd.sync()
+                    res.append((out.numpy(), v.numpy()))
+                w.upload(np.concatenate([xs[r], np.zeros(65, dtype)]))
+                c.allreduce(op, w.view(0, n), w.view(0, n), path=Path.DIRECT)  # recv aliases the window
+                fmi_amd.sync()
+                alias = w.view(0, n).numpy()
+                c.window_free(w)
+                return res, alias
+
+            res = run_ranks(N, body)
+            with np.errstate(all="ignore"):
+                want, _ = orc.allreduce(xs, orc.OPS[OPNAME[op]])
+            for r in range(N):
+                for k, (got, sent) in enumerate(res[r][0]):
+                    assert_bit_equal(got, want[0], f"N={N} n={n} {op.name} rank {r} case {k}")
+                    assert_bit_equal(sent, xs[r], "window bucket untouched")
+                assert_bit_equal(res[r][1], want[0], f"N={N} n={n} {op.name} rank {r} aliased")
+
+
+def test_comm_allreduce_direct_ordered_and_errors(device):
+    N, n = 5, 4099
+    xs = [inputs(np.float32, n, r, seed=19) for r in range(N)]
+
+    def body(c, r):
+        w = c.window(n, np.float32)
+        w.upload(xs[r])
+        out = Bucket(n, np.float32)
+        c.allreduce(Op.SUM, w, out, ordered=True, path=Path.DIRECT)
+        fmi_amd.sync()
+        with pytest.raises(fmi_amd.FmiError):  # send outside any window
+            c.allreduce(Op.SUM, out, out, path=Path.DIRECT)
+        got = out.numpy()
+        c.window_free(w)
+        return got
+
+    res = run_ranks(N, body)
+    want, _ = orc.allreduce(xs, orc.op_sum, commutative=False, associative=False)
+    for r in range(N):
+        assert_bit_equal(res[r], want[r], f"rank {r}")
+
+
 def test_comm_point_to_point_and_data_movement(device):
     N, n = 4, 1000
 
