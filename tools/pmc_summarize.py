@@ -33,6 +33,8 @@ def main():
     ap.add_argument("--write", required=True)
     ap.add_argument("--tag", required=True, help="e.g. r01_c2")
     ap.add_argument("--command", required=True)
+    ap.add_argument("--no-default", action="store_true",
+                    help="do not overwrite profiles/pmc_summary.json (the file bench.py reads for C2)")
     ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                                   "profiles"))
     args = ap.parse_args()
@@ -73,8 +75,9 @@ def main():
         "command": args.command,
         "kernels": kernels,
     }
-    with open(os.path.join(args.out, "pmc_summary.json"), "w") as f:
-        json.dump(summary, f, indent=1)
+    if not args.no_default:
+        with open(os.path.join(args.out, "pmc_summary.json"), "w") as f:
+            json.dump(summary, f, indent=1)
     with open(os.path.join(args.out, f"{args.tag}_pmc_summary.json"), "w") as f:
         json.dump(summary, f, indent=1)
     print(json.dumps(summary, indent=1))
