@@ -129,8 +129,18 @@ public:
         if (!ordered(f)) mirror(sendbuf, recvbuf);
     }
 
-    //! FMI_PATH_TREE (default, reference order) or FMI_PATH_RCCL (reduce-scatter, RCCL's order).
+    //! FMI_PATH_TREE (default, reference order), FMI_PATH_RCCL (reduce-scatter, RCCL's order) or
+    //! FMI_PATH_DIRECT (fused kernel over the peers' windows, reference order; buckets from window()).
     void set_path(int path) { path_ = path; }
+
+    //! A device bucket in a symmetric window (collective: every peer, same n), readable by every peer
+    //! over xGMI — the bucket kind FMI_PATH_DIRECT needs. It lives until the channel finalizes.
+    template <class A>
+    Dev::Bucket<A> window(std::size_t n) {
+        void* p = nullptr;
+        Dev::check(fmi_comm_window_alloc(comm_, n * sizeof(A), &p), "fmi_comm_window_alloc");
+        return Dev::Bucket<A>::borrow(static_cast<A*>(p), n);
+    }
 
     void finalize() override {
         if (comm_) (void)fmi_comm_destroy(comm_);

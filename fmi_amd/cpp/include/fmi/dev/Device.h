@@ -59,14 +59,24 @@ public:
         ptr_ = static_cast<A*>(p);
     }
     explicit Bucket(const std::vector<A>& host) : Bucket(host.size()) { upload(host); }
+    //! A bucket over memory owned elsewhere (e.g. a communicator window): never freed by the bucket.
+    static Bucket borrow(A* ptr, std::size_t n) {
+        Bucket b;
+        b.ptr_ = ptr;
+        b.n_ = n;
+        b.owns_ = false;
+        return b;
+    }
     Bucket(const Bucket&) = delete;
     Bucket& operator=(const Bucket&) = delete;
-    Bucket(Bucket&& o) noexcept : ptr_(std::exchange(o.ptr_, nullptr)), n_(std::exchange(o.n_, 0)) {}
+    Bucket(Bucket&& o) noexcept
+        : ptr_(std::exchange(o.ptr_, nullptr)), n_(std::exchange(o.n_, 0)), owns_(std::exchange(o.owns_, true)) {}
     Bucket& operator=(Bucket&& o) noexcept {
         if (this != &o) {
             release();
             ptr_ = std::exchange(o.ptr_, nullptr);
             n_ = std::exchange(o.n_, 0);
+            owns_ = std::exchange(o.owns_, true);
         }
         return *this;
     }
@@ -93,12 +103,14 @@ public:
 
 private:
     void release() noexcept {
-        if (ptr_) (void)fmi_dev_free(ptr_);
+        if (ptr_ && owns_) (void)fmi_dev_free(ptr_);
         ptr_ = nullptr;
         n_ = 0;
+        owns_ = true;
     }
     A* ptr_ = nullptr;
     std::size_t n_ = 0;
+    bool owns_ = true;
 };
 
 // Untyped device scratch used by the channel algorithms for temporaries of device-resident buckets.

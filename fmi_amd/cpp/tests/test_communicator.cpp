@@ -768,6 +768,53 @@ GPU_TEST(rccl_channel_host_ingress_local_transport) {
     }
 }
 
+// FMI_PATH_DIRECT through the C++ surface: window buckets from the channel, the fused kernel reading every
+// peer's window in place; bit-identical to the host-channel allreduce, sendbuf = result as in the reference.
+GPU_TEST(rccl_channel_direct_path_window_buckets) {
+    Dev::init(0);
+    for (peer_num P : {2u, 4u, 7u}) {
+        const std::size_t n = 100003;
+        std::vector<std::vector<float>> host(P), dev(P), sent(P);
+        with_peers(P, [&](Communicator& c, peer_num p) {
+            Data<std::vector<float>> a(synth_f32(n, 11, p)), r(n);
+            c.allreduce(a, r, Function<std::vector<float>>(Op::sum));
+            host[p] = r.get();
+        });
+        auto mailbox = std::make_shared<FMI::Comm::Mailbox>();
+        std::vector<std::thread> ts;
+        std::vector<std::string> errors(P);
+        for (peer_num p = 0; p < P; ++p)
+            ts.emplace_back([&, p] {
+                try {
+                    Communicator c(p, P, "", "rccl-direct");
+                    FMI::Comm::Loopback boot(mailbox, std::chrono::seconds(60));
+                    boot.set_peer_id(p);
+                    boot.set_num_peers(P);
+                    auto rccl = FMI::Comm::Rccl::connect(boot, p, P, FMI_TRANSPORT_LOCAL);
+                    rccl->set_path(FMI_PATH_DIRECT);
+                    c.register_channel("Rccl", rccl);
+                    Data<Dev::Bucket<float>> a(rccl->window<float>(n)), r(n);
+                    a.bucket().upload(synth_f32(n, 11, p));
+                    c.allreduce(a, r, Function<Dev::Bucket<float>>(Op::sum));
+                    dev[p] = r.get();
+                    sent[p] = a.get();
+                } catch (const std::exception& e) {
+                    errors[p] = e.what();
+                }
+            });
+        for (auto& t : ts) t.join();
+        for (peer_num p = 0; p < P; ++p) {
+            if (!errors[p].empty()) {
+                ++g_failures;
+                std::fprintf(stderr, "  peer %u threw: %s\n", p, errors[p].c_str());
+                continue;
+            }
+            CHECK(std::memcmp(host[p].data(), dev[p].data(), n * 4) == 0);
+            CHECK(std::memcmp(sent[p].data(), dev[p].data(), n * 4) == 0);
+        }
+    }
+}
+
 GPU_TEST(policy_host_ingress_keeps_user_functions_and_small_buckets_on_host) {
     Dev::init(0);
     std::map<std::string, std::shared_ptr<FMI::Comm::Channel>> chans;

@@ -506,6 +506,9 @@ struct Comm {
         if (pipe.cs) (void)hipStreamSynchronize(pipe.cs);
         for (void* b : buf)
             if (b) (void)hipFree(b);
+        // Windows are read by the peers: wait until every rank is done with them (communicators are torn
+        // down collectively, as the reference's Communicator destructor finalizes every channel).
+        if (!windows.empty()) (void)t->barrier(library_stream());
         for (auto& [base, w] : windows) {
             t->unmap_window(w.peers);
             (void)hipFree(base);
