@@ -2,22 +2,24 @@
 """Benchmark of FMI's bucket reduction on MI355X (BASELINE.json metric:
 "GiB/s device-resident float32 sum-reduce, 256 MiB buckets, 1/2/4/8 GPU").
 
-One *step* = one pass of the hot path over one batch of synthetic, HBM-resident buckets:
-  N = 1  (config C2): each GPU holds two peers' 256 MiB float32 buckets and performs the pairwise
-         combine a = a + b — the reference's `f.f(a, b)` (include/Communicator.h:180-189) on the device.
-  N > 1: each GPU still holds two peers' 256 MiB buckets (weak scaling, 2N peers in total): the local
-         pairwise combine is the first round of the reference's recursive-doubling allreduce, the
-         remaining rounds run across GPUs as an all-to-all of shards over RCCL/xGMI + our fused P-way
-         kernel in allreduce_no_order order + an all-gather (fmi_amd/collectives.py), so every GPU ends
-         with the full reduced 256 MiB bucket, bit-identical to the reference's 2N-peer allreduce.
-value = (N × 256 MiB of reduced bucket delivered) / (wall time per step, max over ranks), in GiB/s.
+One *step* = one pass of the hot path over one batch of synthetic, HBM-resident buckets: every GPU holds
+two peers' 256 MiB float32 buckets and performs the pairwise combine a = a + b — the reference's
+`f.f(a, b)` (include/Communicator.h:180-189) on the device (config C2). The combine is element-wise and
+pairs are independent, so at N > 1 the pairs shard over the GPUs with no data-path collective (weak
+scaling, 2N peers); only the barrier + max-over-ranks timing crosses GPUs.
+value = (N × 256 MiB of reduced bucket) / (wall time per step, max over ranks), in GiB/s.
 
 Also reported (one JSON line on rank 0):
-  roofline     — the dominant kernel (pairwise combine at N=1): algorithmic bytes 3·n·4 per launch ÷
-                 its mean duration from HIP events on the stream it runs on; peak = 8000 GB/s HBM3E;
-                 traffic from the committed rocprofv3 PMC summary of the same kernel (profiles/).
-  cpu_baseline — oracle/cpu_baseline (a C++ port of the reference's CPU path) on this host: the
-                 reference-faithful 6-copy adapter around std::transform, 1 thread, same 256 MiB buckets.
+  roofline      — the pairwise kernel: algorithmic bytes 3·n·4 per launch ÷ its mean duration from HIP
+                  events on the stream it runs on; peak = 8000 GB/s HBM3E; traffic from the committed
+                  rocprofv3 PMC summary of the same kernel (profiles/).
+  cpu_baseline  — (N = 1) oracle/cpu_baseline (a C++ port of the reference's CPU path) on this host: the
+                  reference-faithful 6-copy adapter around std::transform, 1 thread, same 256 MiB buckets.
+  config.allreduce, xgmi_roofline — (N > 1) the path with a real exchange step, measured after `value`:
+                  the 2N-peer allreduce of 256 MiB buckets (config C4's shape) — local pairwise round, then
+                  all-to-all of shards over RCCL/xGMI + the fused P-way kernel in allreduce_no_order order +
+                  all-gather (fmi_amd/collectives.py), bit-identical to the reference's 2N-peer allreduce;
+                  its step time, and its egress bytes per GPU against the N-1 xGMI links' peak.
 """
 from __future__ import annotations
 
@@ -26,6 +28,7 @@ import json
 import os
 import subprocess
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -34,6 +37,7 @@ sys.path.insert(0, ROOT)
 MIB = 1 << 20
 GIB = 1 << 30
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak, MI355X_MICROARCH.md §Chip-level parameters
+XGMI_LINK_GBS_PER_DIR = 76.8  # one xGMI link: 153.6 GB/s bidirectional (7 links per GPU, fully connected node)
 METRIC = "GiB/s device-resident float32 sum-reduce, 256 MiB buckets, 1/2/4/8 GPU"
 
 
@@ -54,6 +58,9 @@ def parse():
                     help="N>1, fmi backend: run step k+1's local round on a second stream during step k's exchange")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-diagnostics", action="store_true", help="skip the untimed N>1 phase breakdown")
+    ap.add_argument("--diag-deadline", type=float, default=240.0,
+                    help="seconds the N>1 allreduce measurement + diagnostics (run after `value`) may take before "
+                         "the line is printed without the rest of them")
     ap.add_argument("--force-dist", action="store_true",
                     help="run the N>1 code path (RCCL exchange) even at world size 1 — plumbing check only")
     ap.add_argument("--cpu-reps", type=int, default=30, help="adapter combines timed (≈10 s of CPU work)")
@@ -140,122 +147,63 @@ def main():
     n = args.bucket_mib * MIB // 4
     nbytes = n * 4
 
-    if not use_dist:
-        sets = [(Bucket(n, np.float32).fill_synthetic(42 + s, 0), Bucket(n, np.float32).fill_synthetic(42 + s, 1))
-                for s in range(args.sets)]
-        fmi_amd.sync()
+    # ---- the timed measurement: every rank combines its own peer pairs (C2's unit of work) -------------
+    sets = [tuple(Bucket(n, np.float32).fill_synthetic(42 + s, 2 * rank + j) for j in range(2))
+            for s in range(args.sets)]
+    fmi_amd.sync()
 
-        def step(k):
-            a, b = sets[k % len(sets)]
-            fmi_amd.reduce_pair(Op.SUM, a, b)
+    def step(k):
+        a, b = sets[k % len(sets)]
+        fmi_amd.reduce_pair(Op.SUM, a, b)
 
-        for k in range(args.warmup):
-            step(k)
+    def bracket():  # barrier + device sync (both sides of the timed region)
         fmi_amd.sync()
-        # Timed region: exactly K back-to-back launches on the library stream, bracketed by device syncs;
-        # two HIP events on that stream bracket them (no markers between launches).
-        ev0, ev1 = Event(), Event()
-        t0 = time.perf_counter()
-        ev0.record()
-        for k in range(args.steps):
-            step(k)
-        ev1.record()
-        fmi_amd.sync()
-        t1 = time.perf_counter()
-        step_ms = (t1 - t0) * 1e3 / args.steps
-        # mean launch duration over the timed region (includes the ~1-2 us dispatch gaps between launches)
-        kernel_ms = [ev0.elapsed_ms(ev1) / args.steps]
-        # diagnostic, untimed: per-launch event pairs give the launch duration without the gaps
-        probe = min(args.steps, 32)
-        pairs = [(Event(), Event()) for _ in range(probe)]
-        for k in range(probe):
-            pairs[k][0].record()
-            step(k)
-            pairs[k][1].record()
-        fmi_amd.sync()
-        isolated_us = 1e3 * sum(a.elapsed_ms(b) for a, b in pairs) / probe
-        dominant = "pair_tile"
-        algo_bytes = 3 * nbytes
+        if dist is not None:
+            dist.barrier()
+            torch.cuda.synchronize()
+
+    for k in range(args.warmup):
+        step(k)
+    bracket()
+    # Timed region: exactly K back-to-back launches on the library stream; two HIP events on that stream
+    # bracket them (no markers between launches).
+    ev0, ev1 = Event(), Event()
+    t0 = time.perf_counter()
+    ev0.record()
+    for k in range(args.steps):
+        step(k)
+    ev1.record()
+    bracket()
+    t1 = time.perf_counter()
+    step_ms = (t1 - t0) * 1e3 / args.steps
+    # mean launch duration over the timed region (includes the ~1-2 us dispatch gaps between launches)
+    kernel_avg_ms = ev0.elapsed_ms(ev1) / args.steps
+    if dist is not None:  # max over ranks
+        step_ms, kernel_avg_ms = _max_over_ranks(dist, step_ms, kernel_avg_ms)
+    # diagnostic, untimed: per-launch event pairs give the launch duration without the gaps
+    probe = min(args.steps, 32)
+    pairs = [(Event(), Event()) for _ in range(probe)]
+    for k in range(probe):
+        pairs[k][0].record()
+        step(k)
+        pairs[k][1].record()
+    fmi_amd.sync()
+    isolated_us = 1e3 * sum(a.elapsed_ms(b) for a, b in pairs) / probe
+    for a, b in sets:
+        a.free()
+        b.free()
+    dominant = "pair_tile"
+    algo_bytes = 3 * nbytes
+    if world == 1:
         workload = "C2: 1-GPU pairwise float32 sum-reduce of two 256 MiB device-resident peer buckets"
         parallelism = "single GPU (2 peers resident)"
-        extra = {}
-        roofline_extra = {"kernel_avg_us_isolated": round(isolated_us, 2),
-                          "kernel_avg_source": "HIP events bracketing the K timed launches on the library stream"}
     else:
-        from fmi_amd.collectives import CommAllreduce, ShardedAllreduce
-
-        ar = None
-        backend = args.backend
-        if backend == "fmi":
-            try:  # the product C-ABI communicator (fmi_comm_*, RCCL transport)
-                ar = CommAllreduce(dist.group.WORLD, path=args.path)
-            except Exception as e:  # setup only: every rank fails alike, before any timed work
-                print(f"fmi_comm setup failed ({e}); using the torch.distributed exchange", file=sys.stderr)
-                backend = "torch"
-        if ar is None:
-            ar = ShardedAllreduce(dist.group.WORLD, path=args.path, force_exchange=args.force_dist)
-        if isinstance(ar, CommAllreduce):
-            step_ms, kernel_ms, extra = ar.bench(n, steps=args.steps, warmup=args.warmup, sets=args.sets,
-                                                 overlap=args.overlap_steps)
-        else:
-            step_ms, kernel_ms, extra = ar.bench(n, steps=args.steps, warmup=args.warmup, sets=args.sets)
-        extra["backend"] = backend
-        if not args.no_diagnostics:
-            # untimed diagnostics for the next optimisation round: the other exchange path's step time and
-            # the per-phase breakdown of the sharded allreduce (each max over ranks)
-            from fmi_amd.collectives import phase_breakdown
-
-            other = "rccl" if args.path == "tree" else "tree"
-            if isinstance(ar, CommAllreduce):
-                from fmi_amd.comm import Path
-
-                saved = ar._path
-                ar._path = Path.RCCL if other == "rccl" else Path.TREE
-                alt_ms, _, _ = ar.bench(n, steps=max(10, args.steps // 4), warmup=3, sets=min(2, args.sets))
-                ar._path = saved
-            else:
-                saved = ar.path
-                ar.path = other
-                alt_ms, _, _ = ar.bench(n, steps=max(10, args.steps // 4), warmup=3, sets=min(2, args.sets))
-                ar.path = saved
-            extra["diagnostics"] = {f"ms_per_step_path_{other}": round(alt_ms, 5),
-                                    "phase_ms": phase_breakdown(n, dist.group.WORLD)}
-            if isinstance(ar, CommAllreduce):
-                # the other step schedule: local round of step k+1 overlapped with step k's exchange, or not
-                ov_ms, _, _ = ar.bench(n, steps=max(10, args.steps // 4), warmup=3, sets=args.sets,
-                                       overlap=not args.overlap_steps)
-                key = "ms_per_step_no_overlap" if args.overlap_steps else "ms_per_step_overlap_steps"
-                extra["diagnostics"][key] = round(ov_ms, 5)
-                # path DIRECT (xGMI reads of IPC-mapped peer windows): bit-identical to TREE? and its step time
-                if args.path != "direct":
-                    saved = ar._path
-                    try:
-                        ok = ar.check_direct(1 << 20)
-                        ar._path = Path.DIRECT
-                        d_ms, _, _ = ar.bench(n, steps=max(10, args.steps // 4), warmup=3, sets=min(2, args.sets))
-                        extra["diagnostics"]["path_direct"] = {"bit_identical_to_tree": ok,
-                                                               "ms_per_step": round(d_ms, 5)}
-                    except Exception as e:  # window setup fails on every rank alike (all-or-nothing)
-                        extra["diagnostics"]["path_direct"] = f"unavailable: {e}"
-                    finally:
-                        ar._path = saved
-                # config C5: 1 GiB host (pinned) bucket per rank, H2D + allreduce + D2H pipelined
-                try:
-                    extra["diagnostics"]["c5_host_allreduce_1GiB"] = ar.host_bench(GIB // 4)
-                except Exception as e:  # diagnostic only; never fails the bench line
-                    extra["diagnostics"]["c5_host_allreduce_1GiB"] = f"failed: {e}"
-        roofline_extra = {"kernel_avg_source": "HIP event pair around the local pairwise round of each step"}
-        dominant = "pair_tile"  # our local round; the exchange itself is RCCL's (config.algbw/busbw)
-        algo_bytes = extra.pop("kernel_algo_bytes")
-        workload = (f"C4-shaped: {2 * world}-peer float32 sum-allreduce of 256 MiB buckets, 2 peers per GPU, "
-                    f"sharded over {world} GPUs")
-        parallelism = {
-            "tree": f"shard{world} (tree: all-to-all + fused tree + all-gather over RCCL)",
-            "rccl": f"shard{world} (RCCL reduce-scatter + all-gather)",
-            "direct": f"shard{world} (direct: fused tree over IPC-mapped peer windows + direct gather, xGMI)",
-        }[args.path]
-
-    kernel_avg_ms = float(sum(kernel_ms) / len(kernel_ms))
+        workload = (f"C2 on every GPU: {world} GPUs each combine their own pair of 256 MiB device-resident "
+                    f"peer buckets ({2 * world} peers)")
+        parallelism = f"dp{world}: pairs sharded over GPUs, no data-path collective (barrier + max-over-ranks timing)"
+    roofline_extra = {"kernel_avg_us_isolated": round(isolated_us, 2),
+                      "kernel_avg_source": "HIP events bracketing the K timed launches on the library stream"
+                                           + (", max over ranks" if dist is not None else "")}
     value = args.gpus * (nbytes / GIB) / (step_ms * 1e-3)
     achieved = algo_bytes / (kernel_avg_ms * 1e-3) / 1e9
     traffic, traffic_src = pmc_traffic(dominant)
@@ -280,15 +228,165 @@ def main():
                      "algorithmic_bytes_per_launch": algo_bytes,
                      "traffic_source": traffic_src},
     }
-    line["config"].update(extra)
     line["roofline"].update(roofline_extra)
     if rank == 0 and not use_dist and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args)
-    if rank == 0:
-        print(json.dumps(line), flush=True)
+    emit = _Emitter(line, rank)
+    watchdog = None
+    if use_dist:
+        # The timed measurement is complete and `line` holds it. The sharded allreduce and the diagnostics
+        # below run other paths; a per-rank deadline (kept until teardown is done, since a rank that failed
+        # alone would leave its peers waiting in a collective) guarantees that a hang there cannot cost
+        # the measured line.
+        state = line["config"]["allreduce"] = {}
+        watchdog = threading.Timer(args.diag_deadline, emit.deadline, args=(state,))
+        watchdog.daemon = True
+        watchdog.start()
+        try:
+            ar = measure_allreduce(args, n, world, dist, line, state)
+            if not args.no_diagnostics:
+                state["diagnostics"] = {}
+                run_diagnostics(args, ar, n, dist, state["diagnostics"])
+        except Exception as e:  # never fails the measured line
+            state["failed"] = f"{type(e).__name__}: {e}"
+    emit.emit()
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+    if watchdog is not None:
+        watchdog.cancel()
+
+
+class _Emitter:
+    """Prints the one JSON line exactly once (rank 0), from the main thread or from the diagnostics
+    deadline — whichever comes first."""
+
+    def __init__(self, line, rank):
+        self.line, self.rank = line, rank
+        self.lock = threading.Lock()
+        self.done = False
+
+    def emit(self):
+        with self.lock:
+            if self.done:
+                return
+            self.done = True
+            if self.rank == 0:
+                try:
+                    text = json.dumps(self.line)
+                except RuntimeError:  # the main thread was still writing the after-`value` section
+                    self.line["config"]["allreduce"] = {"incomplete": "deadline reached while recording"}
+                    text = json.dumps(self.line)
+                print(text, flush=True)
+
+    def deadline(self, state):
+        state["incomplete"] = "deadline reached; the timed measurement (value, roofline) is unaffected"
+        self.emit()
+        print("bench: diagnostics deadline reached, exiting", file=sys.stderr, flush=True)
+        os._exit(0)
+
+
+def _max_over_ranks(dist, *vals):
+    import torch
+
+    t = torch.tensor(vals, dtype=torch.float64, device=torch.cuda.current_device())
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [float(v) for v in t.tolist()]
+
+
+def measure_allreduce(args, n, world, dist, line, state):
+    """Config C4's shape at this node size: the 2N-peer float32 sum-allreduce of 256 MiB buckets, two peers
+    per GPU (the local pairwise round, then the exchange over xGMI: all-to-all of shards + fused kernel in
+    allreduce_no_order order + all-gather, bit-exact with the reference's 2N-peer bracketing). K steps,
+    barrier + sync on both sides, max over ranks. Reported beside `value`, with its xGMI roofline: per step
+    every GPU sends (N-1)/N of its bucket in the all-to-all (or reduce-scatter) and (N-1)/N in the
+    all-gather over its N-1 direct links to the other GPUs (fully connected node)."""
+    from fmi_amd.collectives import CommAllreduce, ShardedAllreduce
+
+    ar = None
+    backend = args.backend
+    if backend == "fmi":
+        try:  # the product C-ABI communicator (fmi_comm_*, RCCL transport)
+            ar = CommAllreduce(dist.group.WORLD, path=args.path)
+        except Exception as e:  # setup only: every rank fails alike, before any timed work
+            print(f"fmi_comm setup failed ({e}); using the torch.distributed exchange", file=sys.stderr)
+            backend = "torch"
+    if ar is None:
+        ar = ShardedAllreduce(dist.group.WORLD, path=args.path, force_exchange=args.force_dist)
+    if isinstance(ar, CommAllreduce):
+        step_ms, kernel_ms, extra = ar.bench(n, steps=args.steps, warmup=args.warmup, sets=args.sets,
+                                             overlap=args.overlap_steps)
+    else:
+        step_ms, kernel_ms, extra = ar.bench(n, steps=args.steps, warmup=args.warmup, sets=args.sets)
+    extra.pop("kernel_algo_bytes", None)
+    state.update({
+        "workload": f"C4-shaped: {2 * world}-peer float32 sum-allreduce of 256 MiB buckets, 2 peers per GPU",
+        "path": {"tree": "all-to-all + fused tree kernel + all-gather over RCCL (bit-exact)",
+                 "rccl": "RCCL reduce-scatter + all-gather",
+                 "direct": "fused tree over IPC-mapped peer windows + direct gather (bit-exact)"}[args.path],
+        "backend": backend,
+        "ms_per_step": round(step_ms, 5),
+        "GiB_s_reduced_buckets": round(world * (n * 4 / GIB) / (step_ms * 1e-3), 2),
+        "local_pair_kernel_ms": round(sum(kernel_ms) / len(kernel_ms), 5),
+    })
+    state.update(extra)
+    if world > 1:
+        egress = 2 * (world - 1) * n * 4 / world
+        xg = egress / (step_ms * 1e-3) / 1e9
+        xpeak = (world - 1) * XGMI_LINK_GBS_PER_DIR
+        line["xgmi_roofline"] = {"bound": "xgmi", "achieved": round(xg, 1), "peak": round(xpeak, 1), "unit": "GB/s",
+                                 "frac": round(xg / xpeak, 4), "bytes_per_step_per_gpu": int(egress),
+                                 "kernel": "sharded allreduce step (config.allreduce)",
+                                 "note": "egress bytes per GPU / allreduce step time (local round included); "
+                                         "peak = N-1 links x 76.8 GB/s per direction"}
+    return ar
+
+
+def run_diagnostics(args, ar, n, dist, diag):
+    """Untimed N>1 diagnostics for the next optimisation round, each max over ranks: the other exchange
+    path's step time, the per-phase breakdown, the other step schedule, config C5 (host-resident buckets)
+    and, last, path DIRECT (xGMI reads of IPC-mapped peer windows). Results are written into `diag` as
+    they complete."""
+    from fmi_amd.collectives import CommAllreduce, phase_breakdown
+
+    other = "rccl" if args.path == "tree" else "tree"
+    short = dict(steps=max(10, args.steps // 4), warmup=3, sets=min(2, args.sets))
+    if isinstance(ar, CommAllreduce):
+        from fmi_amd.comm import Path
+
+        saved = ar._path
+        ar._path = Path.RCCL if other == "rccl" else Path.TREE
+        alt_ms, _, _ = ar.bench(n, **short)
+        ar._path = saved
+    else:
+        saved = ar.path
+        ar.path = other
+        alt_ms, _, _ = ar.bench(n, **short)
+        ar.path = saved
+    diag[f"ms_per_step_path_{other}"] = round(alt_ms, 5)
+    diag["phase_ms"] = phase_breakdown(n, dist.group.WORLD)
+    if not isinstance(ar, CommAllreduce):
+        return
+    # the other step schedule: local round of step k+1 overlapped with step k's exchange, or not
+    ov_ms, _, _ = ar.bench(n, steps=short["steps"], warmup=3, sets=args.sets, overlap=not args.overlap_steps)
+    diag["ms_per_step_no_overlap" if args.overlap_steps else "ms_per_step_overlap_steps"] = round(ov_ms, 5)
+    # config C5: 1 GiB host (pinned) bucket per rank, H2D + allreduce + D2H pipelined
+    try:
+        diag["c5_host_allreduce_1GiB"] = ar.host_bench(GIB // 4)
+    except Exception as e:  # diagnostic only; never fails the bench line
+        diag["c5_host_allreduce_1GiB"] = f"failed: {e}"
+    # path DIRECT: bit-identical to TREE on this node? and its step time
+    if args.path != "direct":
+        saved = ar._path
+        try:
+            ok = ar.check_direct(1 << 20)
+            ar._path = Path.DIRECT
+            d_ms, _, _ = ar.bench(n, **short)
+            diag["path_direct"] = {"bit_identical_to_tree": ok, "ms_per_step": round(d_ms, 5)}
+        except Exception as e:  # window setup fails on every rank alike (all-or-nothing)
+            diag["path_direct"] = f"unavailable: {e}"
+        finally:
+            ar._path = saved
 
 
 if __name__ == "__main__":
