@@ -18,6 +18,8 @@ thread_local std::string t_last_error;
 struct DeviceState {
     int device = -1;
     int num_cus = 256;
+    size_t lds_per_cu = 160 * 1024;  // gfx950
+    size_t lds_per_wg = 160 * 1024;
     hipStream_t stream = nullptr;
     // host-ingress pipeline scratch (fmi_host_reduce_pair): two slots of (a, b) staging + two streams
     void* stage[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
@@ -35,8 +37,9 @@ DeviceState g_state;  // one process drives one device (one process per GPU, as 
 
 // Defaults from tools/tune_pair.py on MI355X (C2, 256 MiB f32): nontemporal one-shot tiles, 4 × 16 B per
 // operand per thread, 256-thread workgroups — 125 µs = 6.4 TB/s vs 142 µs for plain loads/stores.
-std::atomic<long long> g_tune[6] = {2 /*variant: nontemporal tiles*/, 4 /*unroll*/, 256 /*block*/,
-                                    8 /*grid per CU*/, 64ll << 20 /*host chunk*/, 1 /*host zero-copy*/};
+std::atomic<long long> g_tune[7] = {2 /*variant: nontemporal tiles*/, 4 /*unroll*/, 256 /*block*/,
+                                    8 /*grid per CU*/, 64ll << 20 /*host chunk*/, 1 /*host zero-copy*/,
+                                    64 /*fused in-flight KiB per CU (tools/ab_fused_cap.py)*/};
 
 int hip_fail(const char* what, hipError_t e) {
     return fail(FMI_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
@@ -220,6 +223,16 @@ int fail(int code, const std::string& msg) {
 
 hipStream_t library_stream() { return g_state.stream; }
 
+size_t fused_lds_bytes(int P, size_t wg_load_bytes_per_peer) {
+    const long long budget = g_tune[FMI_TUNE_FUSED_INFLIGHT_KIB].load() << 10;
+    if (budget <= 0 || P <= 0) return 0;
+    const size_t per_wg = static_cast<size_t>(P) * wg_load_bytes_per_peer;
+    // never below 2 workgroups per CU: one alone leaves too few loads in flight (P = 8: 12 % slower)
+    const size_t cap = std::max<size_t>(2, (static_cast<size_t>(budget) + per_wg - 1) / per_wg);
+    if (cap >= 32) return 0;  // beyond any register-limited occupancy: no reservation needed
+    return std::min(g_state.lds_per_cu / cap, g_state.lds_per_wg) & ~size_t(255);
+}
+
 }  // namespace fmi::dev
 
 using namespace fmi::dev;
@@ -256,6 +269,8 @@ int fmi_dev_init(int device) {
     FMI_HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     g_state.device = device;
     g_state.num_cus = prop.multiProcessorCount;
+    g_state.lds_per_cu = prop.maxSharedMemoryPerMultiProcessor;
+    g_state.lds_per_wg = prop.sharedMemPerBlock;
     g_state.stream = s;
     return FMI_OK;
 }
@@ -605,6 +620,9 @@ int fmi_tune_set(int key, long long value) {
         case FMI_TUNE_HOST_ZERO_COPY:
             if (value != 0 && value != 1) return fail(FMI_ERR_INVALID, "host zero-copy must be 0 or 1");
             break;
+        case FMI_TUNE_FUSED_INFLIGHT_KIB:
+            if (value < 0 || value > 4096) return fail(FMI_ERR_INVALID, "fused in-flight budget must be in [0, 4096] KiB");
+            break;
         default: return fail(FMI_ERR_INVALID, "unknown tuning key");
     }
     g_tune[key].store(value);
@@ -612,7 +630,7 @@ int fmi_tune_set(int key, long long value) {
 }
 
 int fmi_tune_get(int key, long long* value) {
-    if (!value || key < 0 || key > FMI_TUNE_HOST_ZERO_COPY) return fail(FMI_ERR_INVALID, "bad tuning query");
+    if (!value || key < 0 || key > FMI_TUNE_FUSED_INFLIGHT_KIB) return fail(FMI_ERR_INVALID, "bad tuning query");
     *value = g_tune[key].load();
     return FMI_OK;
 }

@@ -18,6 +18,11 @@ int fail(int code, const std::string& msg);
 // The library's default stream (what a NULL fmi_stream_t means); nullptr before fmi_dev_init.
 hipStream_t library_stream();
 
+// Dynamic LDS a fused P-way launch reserves (the kernels use none) so that the peer loads its resident
+// workgroups keep in flight per CU stay within FMI_TUNE_FUSED_INFLIGHT_KIB: fewer concurrent HBM streams
+// at large P, better DRAM row locality. `wg_load_bytes_per_peer` = bytes one workgroup loads per peer.
+size_t fused_lds_bytes(int P, size_t wg_load_bytes_per_peer);
+
 // Invoke f.template operator()<Op, T>() for a runtime (op, dtype); returns FMI_ERR_INVALID if unknown.
 template <class F>
 int with_op_dtype(int op, int dtype, F&& f) {

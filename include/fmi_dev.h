@@ -227,8 +227,13 @@ typedef enum {
     FMI_TUNE_BLOCK = 2,        /* threads per workgroup: 256, 512, 1024 */
     FMI_TUNE_GRID_PER_CU = 3,  /* workgroups per CU for the grid-stride variant */
     FMI_TUNE_HOST_CHUNK = 4,   /* bytes per chunk of fmi_host_reduce_pair's staged pipeline */
-    FMI_TUNE_HOST_ZERO_COPY = 5 /* 1: page-locked host buckets are combined in place over PCIe by the
+    FMI_TUNE_HOST_ZERO_COPY = 5, /* 1: page-locked host buckets are combined in place over PCIe by the
                                    kernel (no staging); 0: always the staged H2D/kernel/D2H pipeline */
+    FMI_TUNE_FUSED_INFLIGHT_KIB = 6 /* fused P-way kernels (tree, scan): budget of peer-load bytes in
+                                       flight per CU, in KiB; a workgroup of the P-way kernel loads
+                                       4 KiB x P, so at most max(2, ceil(budget / (4 P))) workgroups stay
+                                       resident per CU (an LDS reservation enforces it); 0 = no cap. Default 64
+                                       (fewer concurrent HBM streams at large P) */
 } fmi_tune_key_t;
 int fmi_tune_set(int key, long long value);
 int fmi_tune_get(int key, long long* value);

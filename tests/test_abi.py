@@ -95,6 +95,12 @@ def test_tuning_knobs_validate():
         fmi_amd.tune_set(fmi_amd.Tune.PAIR_UNROLL, 3)
     with pytest.raises(fmi_amd.FmiError):
         fmi_amd.tune_set(fmi_amd.Tune.BLOCK, 100)
+    assert fmi_amd.tune_get(fmi_amd.Tune.FUSED_INFLIGHT_KIB) == 64  # default (tools/ab_fused_cap.py)
+    fmi_amd.tune_set(fmi_amd.Tune.FUSED_INFLIGHT_KIB, 0)
+    assert fmi_amd.tune_get(fmi_amd.Tune.FUSED_INFLIGHT_KIB) == 0
+    fmi_amd.tune_set(fmi_amd.Tune.FUSED_INFLIGHT_KIB, 64)
+    with pytest.raises(fmi_amd.FmiError):
+        fmi_amd.tune_set(fmi_amd.Tune.FUSED_INFLIGHT_KIB, -1)
 
 
 @pytest.mark.parametrize("P", list(range(1, 34)) + [48, 64])

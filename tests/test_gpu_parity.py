@@ -220,6 +220,29 @@ def test_scan_peers(device, P):
                     assert_bit_equal(outs[k].numpy(), want[k], f"P={P} {alg.name} {op.name} peer {k}")
 
 
+@pytest.mark.parametrize("cap", [0, 4, 32, 96, 256])
+def test_fused_occupancy_cap_keeps_bits(device, cap):
+    """FMI_TUNE_FUSED_INFLIGHT_KIB only reserves LDS to cap residency: results stay bit-exact (multi-wave
+    grids, ragged tail)."""
+    P, n = 8, (1 << 20) + 5
+    xs = _peer_inputs(np.float32, n, P)
+    ins = [dev(x) for x in xs]
+    want_ar, _ = orc.allreduce(xs, orc.op_sum)
+    want_sc, _ = orc.scan(xs, orc.op_sum)
+    old = fmi_amd.tune_get(Tune.FUSED_INFLIGHT_KIB)
+    try:
+        fmi_amd.tune_set(Tune.FUSED_INFLIGHT_KIB, cap)
+        out = Bucket(n, np.float32)
+        fmi_amd.reduce_tree(Op.SUM, Alg.ALLREDUCE, out, ins)
+        assert_bit_equal(out.numpy(), want_ar[0], f"allreduce cap {cap}")
+        outs = [Bucket(n, np.float32) for _ in range(P)]
+        fmi_amd.scan_peers(Op.SUM, Alg.SCAN, outs, ins)
+        for k in range(P):
+            assert_bit_equal(outs[k].numpy(), want_sc[k], f"scan cap {cap} peer {k}")
+    finally:
+        fmi_amd.tune_set(Tune.FUSED_INFLIGHT_KIB, old)
+
+
 def test_scan_in_place(device):
     P, n = 8, 4096
     xs = _peer_inputs(np.float32, n, P)
