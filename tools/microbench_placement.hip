@@ -95,10 +95,20 @@ int main(int argc, char** argv) {
     const int trials = argc > 1 ? std::atoi(argv[1]) : 12;
     constexpr int NB = 48;
     const size_t n = (64u << 20) / 4, nvec = n / 4;
+    // MBP_ARENA=1: carve the 48 buckets out of one hipMalloc (3 GiB) instead of 48 separate allocations
+    const bool arena = std::getenv("MBP_ARENA") != nullptr;
+    std::printf("{\"allocation\": \"%s\"}\n", arena ? "one 3 GiB arena" : "48 separate hipMalloc");
     std::vector<void*> buf(NB);
-    for (auto& b : buf) {
-        CHECK(hipMalloc(&b, n * 4));
-        CHECK(hipMemset(b, 0, n * 4));
+    if (arena) {
+        char* base;
+        CHECK(hipMalloc(&base, NB * n * 4));
+        CHECK(hipMemset(base, 0, NB * n * 4));
+        for (int k = 0; k < NB; ++k) buf[k] = base + static_cast<size_t>(k) * n * 4;
+    } else {
+        for (auto& b : buf) {
+            CHECK(hipMalloc(&b, n * 4));
+            CHECK(hipMemset(b, 0, n * 4));
+        }
     }
     // bit-exactness of the split form against scan_kernel on one draw (inputs: small integers in f32 would
     // hide bracketing; use a counter-based fill instead)
