@@ -114,7 +114,23 @@ def cpu_baseline(args):
                    f"1 thread: {bare['median_ms']:.2f} ms = {bare['bucket_gib_s']:.2f} GiB/s; host '{model}', "
                    f"{os.cpu_count()} CPUs visible"),
         "bare_loop_gib_s": round(bare["bucket_gib_s"], 4),
+        "c1": c1_host(),
     }
+
+
+def c1_host():
+    """Config C1 (CPU, no GPU): 2-peer f32 sum-allreduce of 1 MiB buckets through the C++ FMI::Communicator,
+    peers as fork()ed processes over a socketpair channel, with the reference adapter (untagged lambda)
+    and with the built-in in-place op (build/cpp/c1_bench, fmi_amd/cpp/tools/c1_bench.cpp)."""
+    exe = os.path.join(ROOT, "build", "cpp", "c1_bench")
+    if not os.path.exists(exe):
+        return None
+    try:
+        out = subprocess.run([exe, "--mib", "1", "--reps", "41"], check=True, capture_output=True, text=True,
+                             timeout=120)
+        return json.loads(out.stdout.strip().splitlines()[-1])
+    except Exception as e:  # reported, never required
+        return {"error": str(e)}
 
 
 def main():

@@ -86,3 +86,15 @@ def test_cpp_device_path_matches_oracle(exe, mode, kind):
     P, n = 8, (1 << 16) + 5
     recv, send = _dump(exe, kind, P, n, mode)
     _check(kind, P, n, recv, send)
+
+
+def test_c1_host_bench_runs(exe):
+    """Config C1 (2-peer f32 sum-allreduce, 1 MiB, forked peers over socketpairs): the host benchmark that
+    bench.py reports beside the CPU baseline runs and both combine paths complete."""
+    import json
+
+    out = subprocess.run([os.path.join(ROOT, "build", "cpp", "c1_bench"), "--reps", "3"], check=True,
+                         capture_output=True, text=True, timeout=120)
+    r = json.loads(out.stdout.strip().splitlines()[-1])
+    assert r["config"] == "C1" and r["peers"] == 2 and r["bucket_mib"] == 1
+    assert r["lambda_adapter_ms"] > 0 and r["builtin_inplace_ms"] > 0
