@@ -178,7 +178,10 @@ ncclRedOp_t nccl_op(int op) {
 class RcclTransport final : public Transport {
 public:
     RcclTransport(const RcclApi* api, ncclComm_t comm, int n, int rank) : Transport(n, rank), api_(api), comm_(comm) {}
-    ~RcclTransport() override { (void)api_->CommDestroy(comm_); }
+    ~RcclTransport() override {
+        (void)api_->CommDestroy(comm_);
+        if (token_) (void)hipFree(token_);
+    }
 
     int all_to_all(const char* send, char* recv, size_t bytes, hipStream_t s) override {
         if (api_->AllToAll) {
