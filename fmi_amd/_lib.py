@@ -58,6 +58,8 @@ SIGNATURES = {
     "fmi_dev_free": (_i, [_vp]),
     "fmi_host_pin_alloc": (_i, [_c.POINTER(_vp), _sz]),
     "fmi_host_pin_free": (_i, [_vp]),
+    "fmi_host_register": (_i, [_vp, _sz]),
+    "fmi_host_unregister": (_i, [_vp]),
     "fmi_dev_h2d_async": (_i, [_vp, _vp, _sz, _vp]),
     "fmi_dev_d2h_async": (_i, [_vp, _vp, _sz, _vp]),
     "fmi_dev_d2d_async": (_i, [_vp, _vp, _sz, _vp]),

@@ -154,6 +154,35 @@ private:
     bool device_ = false;
 };
 
+// Page-locks an existing host range for its lifetime (fmi_host_register), e.g. the storage of a
+// Data<std::vector<A>> recv buffer reused across collectives, so host-bucket combines take the zero-copy
+// path. The range must outlive the registration. Move-only.
+class HostRegistration {
+public:
+    HostRegistration() = default;
+    HostRegistration(void* ptr, std::size_t bytes) : ptr_(ptr) { check(fmi_host_register(ptr, bytes), "fmi_host_register"); }
+    template <class A>
+    explicit HostRegistration(std::vector<A>& v) : HostRegistration(v.data(), v.size() * sizeof(A)) {}
+    HostRegistration(const HostRegistration&) = delete;
+    HostRegistration& operator=(const HostRegistration&) = delete;
+    HostRegistration(HostRegistration&& o) noexcept : ptr_(std::exchange(o.ptr_, nullptr)) {}
+    HostRegistration& operator=(HostRegistration&& o) noexcept {
+        if (this != &o) {
+            release();
+            ptr_ = std::exchange(o.ptr_, nullptr);
+        }
+        return *this;
+    }
+    ~HostRegistration() { release(); }
+
+private:
+    void release() noexcept {
+        if (ptr_) (void)fmi_host_unregister(ptr_);
+        ptr_ = nullptr;
+    }
+    void* ptr_ = nullptr;
+};
+
 // Byte copy that knows where both sides live (host-host memcpy, device-device D2D, staged otherwise).
 inline void copy_bytes(char* dst, bool dst_dev, const char* src, bool src_dev, std::size_t len) {
     if (len == 0 || dst == src) return;

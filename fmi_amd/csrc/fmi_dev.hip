@@ -63,7 +63,7 @@ hipStream_t resolve(fmi_stream_t s) { return s ? static_cast<hipStream_t>(s) : g
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
 // Is `p` page-locked host memory the device can address? Returns its device-side address.
-bool host_mapped(void* p, void** dev) {
+bool host_mapped_at(void* p, void** dev) {
     hipPointerAttribute_t attr;
     if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
         (void)hipGetLastError();  // pageable memory reports an error: clear it
@@ -71,6 +71,19 @@ bool host_mapped(void* p, void** dev) {
     }
     if (attr.type != hipMemoryTypeHost || attr.devicePointer == nullptr) return false;
     *dev = attr.devicePointer;
+    return true;
+}
+
+// Is all of [p, p + bytes) page-locked and device-mapped as one contiguous range (first and last byte
+// mapped, at device addresses bytes - 1 apart)? A bucket that only starts inside a pinned or registered
+// range must not be read zero-copy past its end.
+bool host_mapped(void* p, size_t bytes, void** dev) {
+    void* first = nullptr;
+    void* last = nullptr;
+    if (!host_mapped_at(p, &first)) return false;
+    if (!host_mapped_at(static_cast<char*>(p) + bytes - 1, &last)) return false;
+    if (static_cast<char*>(last) - static_cast<char*>(first) != static_cast<std::ptrdiff_t>(bytes - 1)) return false;
+    *dev = first;
     return true;
 }
 
@@ -339,6 +352,21 @@ int fmi_host_pin_free(void* ptr) {
     return FMI_OK;
 }
 
+int fmi_host_register(void* ptr, size_t bytes) {
+    if (!ptr || bytes == 0) return fail(FMI_ERR_INVALID, "fmi_host_register: null or empty range");
+    if (int rc = require_device()) return rc;
+    const hipError_t e = hipHostRegister(ptr, bytes, hipHostRegisterMapped);
+    if (e != hipSuccess) return fail(FMI_ERR_ALLOC, "hipHostRegister(" + std::to_string(bytes) + "): " + hipGetErrorString(e));
+    return FMI_OK;
+}
+
+int fmi_host_unregister(void* ptr) {
+    if (!ptr) return fail(FMI_ERR_INVALID, "fmi_host_unregister: null pointer");
+    if (int rc = require_device()) return rc;
+    FMI_HIP_TRY(hipHostUnregister(ptr));
+    return FMI_OK;
+}
+
 static int copy_async(void* dst, const void* src, size_t bytes, hipMemcpyKind kind, fmi_stream_t stream) {
     if (bytes == 0) return FMI_OK;
     if (!dst || !src) return fail(FMI_ERR_INVALID, "null buffer");
@@ -513,12 +541,22 @@ int fmi_host_reduce_pair(int op, int dtype, void* inout, const void* in, size_t 
     if (n == 0) return FMI_OK;
     if (!inout || !in) return fail(FMI_ERR_INVALID, "null buffer");
     if (int rc = require_device()) return rc;
+    // A bucket partly inside a page-locked range: the zero-copy kernel must not read past that range, and
+    // the runtime rejects copies that start or end inside one. Pin or register all of it, or none.
+    for (const void* p : {static_cast<const void*>(inout), in}) {
+        void* d = nullptr;
+        char* c = static_cast<char*>(const_cast<void*>(p));
+        const bool head = host_mapped_at(c, &d), tail = host_mapped_at(c + n * esz - 1, &d);
+        if ((head || tail) && !host_mapped(c, n * esz, &d))
+            return fail(FMI_ERR_INVALID, "fmi_host_reduce_pair: a bucket straddles the end of a page-locked range "
+                                         "(pin or register the whole bucket, or none of it)");
+    }
     if (g_tune[FMI_TUNE_HOST_ZERO_COPY].load()) {
         // Page-locked buckets: the kernel streams them straight over PCIe (reads of both operands and the
         // write-back share the link concurrently, no staging copies, no DMA-engine serialisation).
         void* dx = nullptr;
         void* dy = nullptr;
-        if (host_mapped(inout, &dx) && host_mapped(const_cast<void*>(in), &dy)) {
+        if (host_mapped(inout, n * esz, &dx) && host_mapped(const_cast<void*>(in), n * esz, &dy)) {
             hipStream_t s = g_state.stream;
             int rc = launch_combine(op, dtype, dx, dx, dy, n, s);
             if (rc != FMI_OK) return rc;

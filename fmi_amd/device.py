@@ -297,6 +297,32 @@ class PinnedArray:
             pass
 
 
+class HostRegistration:
+    """Page-lock an existing contiguous numpy array in place (fmi_host_register), so fmi_host_reduce_pair
+    combines it zero-copy and the host pipelines move it at DMA rate. For recv buffers reused across many
+    collectives: registering costs about one copy of the array. The array must outlive the registration.
+    Use as a context manager, or call .close()."""
+
+    def __init__(self, arr: np.ndarray):
+        if not arr.flags.c_contiguous or arr.nbytes == 0:
+            raise ValueError("HostRegistration: needs a non-empty contiguous array")
+        self.array = arr
+        self.ptr = arr.ctypes.data
+        _lib.call("fmi_host_register", self.ptr, arr.nbytes)
+
+    def close(self) -> None:
+        if self.ptr:
+            _lib.call("fmi_host_unregister", self.ptr)
+            self.ptr = None
+            self.array = None
+
+    def __enter__(self) -> "HostRegistration":
+        return self
+
+    def __exit__(self, *exc) -> None:
+        self.close()
+
+
 def _check_peers(out: Bucket, ins: Sequence[Bucket]) -> None:
     if not ins:
         raise ValueError("need at least one peer bucket")

@@ -90,6 +90,15 @@ int fmi_dev_alloc(void** ptr, size_t bytes);
 int fmi_dev_free(void* ptr);
 int fmi_host_pin_alloc(void** ptr, size_t bytes);  /* page-locked host memory for recv buffers */
 int fmi_host_pin_free(void* ptr);
+/* Page-lock an existing host range in place (hipHostRegister, mapped), e.g. a channel recv buffer that is
+ * reused across collectives (reference include/comm/Data.h:50-73 std::vector storage), so that
+ * fmi_host_reduce_pair combines it zero-copy and the host pipelines move it at DMA rate. Registering
+ * costs about as much as one copy of the range: worth it only for buffers used more than once. The range
+ * must stay allocated until fmi_host_unregister(ptr) with the same ptr. A bucket handed to
+ * fmi_host_reduce_pair must lie wholly inside one page-locked range or wholly outside any
+ * (FMI_ERR_INVALID otherwise). */
+int fmi_host_register(void* ptr, size_t bytes);
+int fmi_host_unregister(void* ptr);
 int fmi_dev_h2d_async(void* dst, const void* src, size_t bytes, fmi_stream_t stream);
 int fmi_dev_d2h_async(void* dst, const void* src, size_t bytes, fmi_stream_t stream);
 int fmi_dev_d2d_async(void* dst, const void* src, size_t bytes, fmi_stream_t stream);

@@ -335,6 +335,55 @@ def test_host_reduce_pair_pinned(device, zero_copy, n):
         fmi_amd.tune_set(Tune.HOST_ZERO_COPY, old)
 
 
+def _page_aligned(n, dtype):
+    """A contiguous numpy array of n elements starting on a 4 KiB boundary."""
+    item = np.dtype(dtype).itemsize
+    raw = np.empty(n * item + 8192, dtype=np.uint8)
+    off = (-raw.ctypes.data) % 4096
+    return raw[off:off + n * item].view(dtype)
+
+
+@pytest.mark.parametrize("n", [5, 4099, (1 << 22) + 3])
+def test_host_reduce_pair_registered(device, n):
+    """fmi_host_register'd (pageable, then page-locked in place) buckets are combined zero-copy, bit-exact."""
+    for dtype, op in ((np.float32, Op.SUM), (np.int32, Op.MAX)):
+        a, b = inputs(dtype, n, 0), inputs(dtype, n, 1)
+        ha, hb = _page_aligned(n, dtype), _page_aligned(n, dtype)
+        ha[:] = a
+        hb[:] = b
+        with fmi_amd.HostRegistration(ha), fmi_amd.HostRegistration(hb):
+            fmi_amd.host_reduce_pair(op, ha, hb)
+        with np.errstate(all="ignore"):
+            assert_bit_equal(ha, orc.pairwise(OPNAME[op], a, b), f"{op.name} n={n}")
+        assert_bit_equal(hb, b, "in operand untouched")
+
+
+def test_host_reduce_pair_partly_registered_is_refused(device):
+    """A bucket that only starts inside a registered range is refused with FMI_ERR_INVALID: the zero-copy
+    kernel must not read past the range, and the runtime rejects copies straddling its end. The buckets
+    are left untouched."""
+    n = 1 << 20
+    a, b = inputs(np.float32, n, 0), inputs(np.float32, n, 1)
+    ha, hb = _page_aligned(n, np.float32), _page_aligned(n, np.float32)
+    ha[:] = a
+    hb[:] = b
+    with fmi_amd.HostRegistration(ha[: n // 2]), fmi_amd.HostRegistration(hb):
+        with pytest.raises(fmi_amd.FmiError, match="straddles"):
+            fmi_amd.host_reduce_pair(Op.SUM, ha, hb)
+    assert_bit_equal(ha, a)
+    with fmi_amd.HostRegistration(ha), fmi_amd.HostRegistration(hb):  # whole buckets: fine
+        fmi_amd.host_reduce_pair(Op.SUM, ha, hb)
+    assert_bit_equal(ha, a + b)
+
+
+def test_host_register_errors(device):
+    with pytest.raises(ValueError):
+        fmi_amd.HostRegistration(np.empty(0, np.float32))
+    lib = fmi_amd.load()
+    assert lib.fmi_host_register(None, 16) != 0
+    assert lib.fmi_host_unregister(None) != 0
+
+
 # ------------------------------------------------------------------------------------------------
 # BASELINE.json full-size configs
 # ------------------------------------------------------------------------------------------------
