@@ -1,9 +1,13 @@
-// FMI::Comm::Data — buffer views handed to the collectives.
+// FMI::Comm::Data — the buffer views the collectives move and combine.
 //
-// Same API as the reference (include/comm/Data.h:11-97): scalar Data<T>, owning Data<std::vector<A>>,
-// non-owning Data<void*>, each with size_in_bytes() and data(). Added: Data<Dev::Bucket<A>>, a bucket
-// resident in MI355X HBM — its data() is a device pointer and on_device() tells the channels so, which
-// routes combines to the HIP kernels and transfers through device-aware staging.
+// The public members are those of reference include/comm/Data.h:11-97 (size_in_bytes(), data(), get(),
+// the same constructors and the same runtime error for a non-fundamental scalar), for four payloads:
+//   Data<T>                 one scalar, held by value
+//   Data<std::vector<A>>    an owned host bucket
+//   Data<void*>             a caller-owned byte range (host, or device when flagged)
+//   Data<Dev::Bucket<A>>    an owned bucket resident in MI355X HBM (extension)
+// Every view also answers on_device(), which the channels use to route the combine to the HIP kernels and
+// transfers through device-aware staging.
 #ifndef FMI_AMD_COMM_DATA_H
 #define FMI_AMD_COMM_DATA_H
 
@@ -18,81 +22,100 @@
 
 namespace FMI::Comm {
 
-template <typename T>
-class Data {
+namespace detail {
+// The (pointer, byte count) face every payload shows the channels; Derived supplies bytes() and base().
+template <class Derived>
+class ByteView {
 public:
-    Data() = default;
-    Data(T value) : val(value) {}
-
-    std::size_t size_in_bytes() {
-        if constexpr (std::is_fundamental_v<T>) {
-            return sizeof(T);
-        } else {
-            throw std::runtime_error("Cannot get size in bytes of non-fundamental type");
-        }
-    }
-    char* data() { return reinterpret_cast<char*>(&val); }
-    T get() const { return val; }
-    static constexpr bool on_device() { return false; }
-
-    friend std::ostream& operator<<(std::ostream& o, const Data& d) { return o << d.get(); }
-    friend bool operator==(const Data& l, const Data& r) { return l.get() == r.get(); }
+    std::size_t size_in_bytes() { return self().bytes(); }
+    char* data() { return reinterpret_cast<char*>(self().base()); }
 
 private:
-    T val{};
+    Derived& self() { return static_cast<Derived&>(*this); }
+};
+}  // namespace detail
+
+template <typename T>
+class Data : public detail::ByteView<Data<T>> {
+public:
+    Data() = default;
+    Data(T value) : value_(value) {}
+
+    T get() const { return value_; }
+    static constexpr bool on_device() { return false; }
+
+    friend std::ostream& operator<<(std::ostream& os, const Data& d) { return os << d.value_; }
+    friend bool operator==(const Data& a, const Data& b) { return a.value_ == b.value_; }
+
+private:
+    friend class detail::ByteView<Data<T>>;
+    std::size_t bytes() const {
+        if constexpr (!std::is_fundamental_v<T>)
+            throw std::runtime_error("Cannot get size in bytes of non-fundamental type");
+        return sizeof(T);
+    }
+    void* base() { return &value_; }
+
+    T value_{};
 };
 
 template <typename A>
-class Data<std::vector<A>> {
+class Data<std::vector<A>> : public detail::ByteView<Data<std::vector<A>>> {
 public:
     Data() = default;
-    Data(std::size_t n) : val(n) {}
-    Data(std::vector<A> value) : val(std::move(value)) {}
+    Data(std::size_t n) : elems_(n) {}
+    Data(std::vector<A> value) : elems_(std::move(value)) {}
 
-    std::size_t size_in_bytes() { return sizeof(A) * val.size(); }
-    char* data() { return reinterpret_cast<char*>(val.data()); }
-    std::vector<A> get() const { return val; }
+    std::vector<A> get() const { return elems_; }
     static constexpr bool on_device() { return false; }
 
 private:
-    std::vector<A> val;
+    friend class detail::ByteView<Data<std::vector<A>>>;
+    std::size_t bytes() const { return elems_.size() * sizeof(A); }
+    void* base() { return elems_.data(); }
+
+    std::vector<A> elems_;
 };
 
 template <>
-class Data<void*> {
+class Data<void*> : public detail::ByteView<Data<void*>> {
 public:
     Data() = default;
-    // `device` marks a pointer into device memory (a raw HBM buffer owned by the caller).
-    Data(void* buf, std::size_t len, bool device = false) : buf(buf), len(len), device(device) {}
+    // `device` marks a range in device memory (a raw HBM buffer the caller owns).
+    Data(void* buf, std::size_t len, bool device = false) : ptr_(buf), len_(len), device_(device) {}
 
-    std::size_t size_in_bytes() { return len; }
-    char* data() { return reinterpret_cast<char*>(buf); }
-    void* get() { return buf; }
-    bool on_device() const { return device; }
+    void* get() { return ptr_; }
+    bool on_device() const { return device_; }
 
 private:
-    void* buf = nullptr;
-    std::size_t len = 0;
-    bool device = false;
+    friend class detail::ByteView<Data<void*>>;
+    std::size_t bytes() const { return len_; }
+    void* base() { return ptr_; }
+
+    void* ptr_ = nullptr;
+    std::size_t len_ = 0;
+    bool device_ = false;
 };
 
-// A peer's bucket resident in HBM (move-only; get() copies it back to the host).
+// A peer's bucket resident in HBM (move-only; get() downloads a host copy).
 template <typename A>
-class Data<Dev::Bucket<A>> {
+class Data<Dev::Bucket<A>> : public detail::ByteView<Data<Dev::Bucket<A>>> {
 public:
     Data() = default;
-    explicit Data(std::size_t n) : val(n) {}
-    explicit Data(const std::vector<A>& host) : val(host) {}
-    Data(Dev::Bucket<A>&& bucket) : val(std::move(bucket)) {}
+    explicit Data(std::size_t n) : bucket_(n) {}
+    explicit Data(const std::vector<A>& host) : bucket_(host) {}
+    Data(Dev::Bucket<A>&& bucket) : bucket_(std::move(bucket)) {}
 
-    std::size_t size_in_bytes() { return val.size_in_bytes(); }
-    char* data() { return reinterpret_cast<char*>(val.data()); }
-    std::vector<A> get() const { return val.download(); }
-    Dev::Bucket<A>& bucket() { return val; }
+    std::vector<A> get() const { return bucket_.download(); }
+    Dev::Bucket<A>& bucket() { return bucket_; }
     static constexpr bool on_device() { return true; }
 
 private:
-    Dev::Bucket<A> val;
+    friend class detail::ByteView<Data<Dev::Bucket<A>>>;
+    std::size_t bytes() const { return bucket_.size_in_bytes(); }
+    void* base() { return bucket_.data(); }
+
+    Dev::Bucket<A> bucket_;
 };
 
 }  // namespace FMI::Comm
