@@ -193,18 +193,20 @@ private:
                 const std::size_t count = size_in_bytes / sizeof(A);
                 const device_op dop{static_cast<int>(op), Dev::dtype_of<A>(), count};
                 if (offload_host_) {
-                    return raw_function{[dop](char* a, char* b) {
-                                            Dev::check(fmi_host_reduce_pair(dop.op, dop.dtype, a, b, dop.count),
-                                                       "fmi_host_reduce_pair");
-                                        },
-                                        f.associative, f.commutative, dop};
+                    auto part = [dop](char* a, char* b, std::size_t off, std::size_t len) {
+                        Dev::check(fmi_host_reduce_pair(dop.op, dop.dtype, a + off, b + off, len / sizeof(A)),
+                                   "fmi_host_reduce_pair");
+                    };
+                    return raw_function{[part, size_in_bytes](char* a, char* b) { part(a, b, 0, size_in_bytes); },
+                                        f.associative, f.commutative, dop, part, sizeof(A)};
                 }
-                return raw_function{[op, count](char* a, char* b) {
-                                        A* x = reinterpret_cast<A*>(a);
-                                        const A* y = reinterpret_cast<const A*>(b);
-                                        for (std::size_t i = 0; i < count; ++i) x[i] = Utils::detail::apply_op<A>(op, x[i], y[i]);
-                                    },
-                                    f.associative, f.commutative, dop};
+                auto part = [op](char* a, char* b, std::size_t off, std::size_t len) {
+                    A* x = reinterpret_cast<A*>(a + off);
+                    const A* y = reinterpret_cast<const A*>(b + off);
+                    for (std::size_t i = 0, m = len / sizeof(A); i < m; ++i) x[i] = Utils::detail::apply_op<A>(op, x[i], y[i]);
+                };
+                return raw_function{[part, size_in_bytes](char* a, char* b) { part(a, b, 0, size_in_bytes); },
+                                    f.associative, f.commutative, dop, part, sizeof(A)};
             }
         }
         // The reference adapter: copy both buckets, call the user function by value, copy back.

@@ -32,11 +32,17 @@ struct device_op {
     bool valid() const { return op >= 0 && dtype >= 0; }
 };
 
+//! The same combine restricted to bytes [offset, offset + len) of both buckets; len and offset are whole
+//! elements. Lets a stream transport combine chunk k while chunk k+1 is still in flight.
+using raw_part_func = std::function<void(char*, char*, std::size_t offset, std::size_t len)>;
+
 struct raw_function {
     raw_func f;  // overwrites the left argument
     bool associative;
     bool commutative;
     device_op device{};
+    raw_part_func part{};     // optional (built-in ops on host buckets)
+    std::size_t granule = 0;  // element size in bytes for `part`
 };
 
 struct channel_data {

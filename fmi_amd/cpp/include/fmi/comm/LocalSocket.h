@@ -103,6 +103,8 @@ public:
         }
     }
 
+    bool stream_transport() const override { return true; }
+
     void finalize() override {
         for (int& f : fds_)
             if (f >= 0) {

@@ -89,12 +89,29 @@ def test_cpp_device_path_matches_oracle(exe, mode, kind):
 
 
 def test_c1_host_bench_runs(exe):
-    """Config C1 (2-peer f32 sum-allreduce, 1 MiB, forked peers over socketpairs): the host benchmark that
-    bench.py reports beside the CPU baseline runs and both combine paths complete."""
+    """Config C1 (2-peer f32 sum-allreduce, forked peers over socketpairs): the host benchmark that bench.py
+    reports beside the CPU baseline runs, and its three combine paths (reference adapter, built-in in place,
+    built-in overlapped with the transfer in 2 MiB pieces) give identical bits. 8 MiB buckets, so the
+    overlapped path really cuts the transfer."""
     import json
 
-    out = subprocess.run([os.path.join(ROOT, "build", "cpp", "c1_bench"), "--reps", "3"], check=True,
+    out = subprocess.run([os.path.join(ROOT, "build", "cpp", "c1_bench"), "--reps", "3", "--mib", "8"], check=True,
                          capture_output=True, text=True, timeout=120)
     r = json.loads(out.stdout.strip().splitlines()[-1])
-    assert r["config"] == "C1" and r["peers"] == 2 and r["bucket_mib"] == 1
-    assert r["lambda_adapter_ms"] > 0 and r["builtin_inplace_ms"] > 0
+    assert r["config"] == "C1" and r["peers"] == 2 and r["bucket_mib"] == 8
+    assert r["lambda_adapter_ms"] > 0 and r["builtin_inplace_ms"] > 0 and r["builtin_overlap_ms"] > 0
+    assert r["paths_bit_identical"] is True
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("peers", [2, 3])
+def test_c1_overlapped_offload_bit_identical(exe, peers):
+    """Host buckets over a socket channel with the combine on the GPU (use_device): the transfer cut into
+    pieces, each piece combined by fmi_host_reduce_pair while the next moves — identical bits to the
+    serial path and to the reference adapter."""
+    import json
+
+    out = subprocess.run([os.path.join(ROOT, "build", "cpp", "c1_bench"), "--reps", "3", "--mib", "16", "--peers",
+                          str(peers), "--device", "0"], check=True, capture_output=True, text=True, timeout=120)
+    r = json.loads(out.stdout.strip().splitlines()[-1])
+    assert r["combine_on"].startswith("gpu") and r["paths_bit_identical"] is True
