@@ -61,6 +61,8 @@ def parse():
     ap.add_argument("--diag-deadline", type=float, default=240.0,
                     help="seconds the N>1 allreduce measurement + diagnostics (run after `value`) may take before "
                          "the line is printed without the rest of them")
+    ap.add_argument("--diag-direct", action="store_true",
+                    help="N>1 diagnostics: also check and time path DIRECT (IPC-mapped peer windows)")
     ap.add_argument("--force-dist", action="store_true",
                     help="run the N>1 code path (RCCL exchange) even at world size 1 — plumbing check only")
     ap.add_argument("--cpu-reps", type=int, default=30, help="adapter combines timed (≈10 s of CPU work)")
@@ -361,8 +363,8 @@ def measure_allreduce(args, n, world, dist, line, state):
 def run_diagnostics(args, ar, n, dist, diag):
     """Untimed N>1 diagnostics for the next optimisation round, each max over ranks: the other exchange
     path's step time, the per-phase breakdown, the other step schedule, config C5 (host-resident buckets)
-    and, last, path DIRECT (xGMI reads of IPC-mapped peer windows). Results are written into `diag` as
-    they complete."""
+    and, last and only with --diag-direct, path DIRECT (xGMI reads of IPC-mapped peer windows). Results are
+    written into `diag` as they complete."""
     from fmi_amd.collectives import CommAllreduce, phase_breakdown
 
     other = "rccl" if args.path == "tree" else "tree"
@@ -391,8 +393,12 @@ def run_diagnostics(args, ar, n, dist, diag):
         diag["c5_host_allreduce_1GiB"] = ar.host_bench(GIB // 4)
     except Exception as e:  # diagnostic only; never fails the bench line
         diag["c5_host_allreduce_1GiB"] = f"failed: {e}"
-    # path DIRECT: bit-identical to TREE on this node? and its step time
-    if args.path != "direct":
+    # path DIRECT: bit-identical to TREE on this node? and its step time. Opt-in (--diag-direct): its
+    # cross-process IPC mappings have only run on the LOCAL transport so far, and a fault there would take
+    # the whole line with it.
+    if not args.diag_direct:
+        diag["path_direct"] = "not run (opt-in: --diag-direct)"
+    elif args.path != "direct":
         saved = ar._path
         try:
             ok = ar.check_direct(1 << 20)
