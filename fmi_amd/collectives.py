@@ -32,7 +32,8 @@ import torch.distributed as dist  # noqa: E402
 from . import _lib  # noqa: E402
 from .device import Alg, DType, Op  # noqa: E402
 
-_TORCH_DTYPE = {torch.float32: DType.F32, torch.float64: DType.F64, torch.int32: DType.I32, torch.int64: DType.I64}
+_TORCH_DTYPE = {torch.float32: DType.F32, torch.float64: DType.F64, torch.int32: DType.I32, torch.int64: DType.I64,
+                torch.int8: DType.I8, torch.uint8: DType.U8, torch.int16: DType.I16}
 _REDUCE_OP = {Op.SUM: dist.ReduceOp.SUM, Op.PROD: dist.ReduceOp.PRODUCT, Op.MAX: dist.ReduceOp.MAX,
               Op.MIN: dist.ReduceOp.MIN}
 SHARD_ALIGN = 64  # elements: keeps every shard 256-B aligned for the 16-B vector kernels

@@ -23,13 +23,24 @@ inline void check(int status, const char* what) {
     if (status != FMI_OK) throw std::runtime_error(std::string(what) + ": " + fmi_last_error());
 }
 
+// The C-ABI element type of a fundamental A (any integer type by width and signedness, so long long and
+// char map too), or -1: bool, long double and non-arithmetic types stay on the host.
 template <class A>
 constexpr int dtype_of() {
     if constexpr (std::is_same_v<A, float>) return FMI_F32;
     else if constexpr (std::is_same_v<A, double>) return FMI_F64;
-    else if constexpr (std::is_same_v<A, int32_t>) return FMI_I32;
-    else if constexpr (std::is_same_v<A, int64_t>) return FMI_I64;
-    else return -1;
+    else if constexpr (std::is_integral_v<A> && !std::is_same_v<A, bool>) {
+        constexpr bool s = std::is_signed_v<A>;
+        switch (sizeof(A)) {
+            case 1: return s ? FMI_I8 : FMI_U8;
+            case 2: return s ? FMI_I16 : FMI_U16;
+            case 4: return s ? FMI_I32 : FMI_U32;
+            case 8: return s ? FMI_I64 : FMI_U64;
+            default: return -1;
+        }
+    } else {
+        return -1;
+    }
 }
 
 template <class A>
@@ -48,7 +59,7 @@ inline void sync() { check(fmi_dev_sync(), "fmi_dev_sync"); }
 // A device-resident bucket of n elements of A (owning, move-only).
 template <class A>
 class Bucket {
-    static_assert(device_type<A>, "device buckets hold float, double, int32_t or int64_t");
+    static_assert(device_type<A>, "device buckets hold float, double or 8/16/32/64-bit integers");
 
 public:
     using value_type = A;

@@ -32,17 +32,22 @@ enum class Op : int { none = -1, sum = FMI_OP_SUM, prod = FMI_OP_PROD, max = FMI
 
 namespace detail {
 
+// Integers wrap: computed in an unsigned type at least as wide as unsigned int (so sub-int types do not
+// promote to a signed int that could overflow), then converted back to A, keeping the low bits.
+template <class A>
+using wrap_t = std::common_type_t<std::make_unsigned_t<A>, unsigned int>;
+
 template <class A>
 A apply_op(Op op, A a, A b) {
     switch (op) {
         case Op::sum:
             if constexpr (std::is_integral_v<A>)
-                return static_cast<A>(static_cast<std::make_unsigned_t<A>>(a) + static_cast<std::make_unsigned_t<A>>(b));
+                return static_cast<A>(static_cast<wrap_t<A>>(a) + static_cast<wrap_t<A>>(b));
             else
                 return a + b;
         case Op::prod:
             if constexpr (std::is_integral_v<A>)
-                return static_cast<A>(static_cast<std::make_unsigned_t<A>>(a) * static_cast<std::make_unsigned_t<A>>(b));
+                return static_cast<A>(static_cast<wrap_t<A>>(a) * static_cast<wrap_t<A>>(b));
             else
                 return a * b;
         case Op::max: return std::max(a, b);  // (a < b) ? b : a

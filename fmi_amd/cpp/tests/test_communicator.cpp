@@ -638,6 +638,44 @@ GPU_TEST(device_buckets_match_host_path_bitwise) {
     }
 }
 
+// Any fundamental integer width is a device dtype (reference Data<std::vector<A>>, include/comm/Data.h:50-73):
+// the reference's allreduce_vector known answers (tests/communicator.cpp:167-192, P = 4, peer p holds p + 1)
+// for sum / prod / max on uint16 device buckets, and on int8 host buckets offloaded to the GPU.
+GPU_TEST(small_integer_buckets_known_answers) {
+    Dev::init(0);
+    std::vector<uint16_t> dsum(4), dprod(4), dmax(4);
+    std::vector<int8_t> hsum(4), hprod(4);
+    with_peers(4, [&](Communicator& c, peer_num p) {
+        const std::size_t n = 4099;
+        auto run = [&](Op op) {
+            Data<Dev::Bucket<uint16_t>> a(std::vector<uint16_t>(n, static_cast<uint16_t>(p + 1))), r(n);
+            c.allreduce(a, r, Function<Dev::Bucket<uint16_t>>(op));
+            return r.get()[n - 1];
+        };
+        dsum[p] = run(Op::sum);
+        dprod[p] = run(Op::prod);
+        dmax[p] = run(Op::max);
+    });
+    with_peers(4, [&](Communicator& c, peer_num p) {
+        c.use_device(0);
+        const std::size_t n = 70001;
+        Data<std::vector<int8_t>> a(std::vector<int8_t>(n, static_cast<int8_t>(p + 1))), r(n);
+        c.allreduce(a, r, Function<std::vector<int8_t>>(Op::sum));
+        hsum[p] = r.get()[n / 2];
+        Data<std::vector<int8_t>> b(std::vector<int8_t>(n, static_cast<int8_t>(100 + p))), rb(n);
+        c.allreduce(b, rb, Function<std::vector<int8_t>>(Op::prod));  // 100·101·102·103 wraps in 8 bits
+        hprod[p] = rb.get()[7];
+    });
+    const int8_t wrapped = static_cast<int8_t>(static_cast<uint8_t>(100u * 101u * 102u * 103u));
+    for (int p = 0; p < 4; ++p) {
+        CHECK(dsum[p] == 10);
+        CHECK(dprod[p] == 24);
+        CHECK(dmax[p] == 4);
+        CHECK(hsum[p] == 10);
+        CHECK(hprod[p] == wrapped);
+    }
+}
+
 GPU_TEST(device_bcast_scatter_gather) {
     Dev::init(0);
     with_peers(5, [](Communicator& c, peer_num p) {

@@ -157,12 +157,18 @@ protected:
     int rank_;
 };
 
-ncclDataType_t nccl_type(int dtype) {
+// RCCL element type of a dtype; false for the 16-bit integers, which RCCL has no reduction type for.
+bool nccl_type(int dtype, ncclDataType_t* t) {
     switch (dtype) {
-        case FMI_F32: return ncclFloat32;
-        case FMI_F64: return ncclFloat64;
-        case FMI_I32: return ncclInt32;
-        default: return ncclInt64;
+        case FMI_F32: *t = ncclFloat32; return true;
+        case FMI_F64: *t = ncclFloat64; return true;
+        case FMI_I32: *t = ncclInt32; return true;
+        case FMI_I64: *t = ncclInt64; return true;
+        case FMI_U32: *t = ncclUint32; return true;
+        case FMI_U64: *t = ncclUint64; return true;
+        case FMI_I8: *t = ncclInt8; return true;
+        case FMI_U8: *t = ncclUint8; return true;
+        default: return false;
     }
 }
 
@@ -247,7 +253,9 @@ public:
         return FMI_OK;
     }
     int reduce_scatter(int op, int dtype, const void* send, void* recv, size_t count, hipStream_t s) override {
-        FMI_NCCL(api_, ReduceScatter(send, recv, count, nccl_type(dtype), nccl_op(op), comm_, s));
+        ncclDataType_t t;
+        if (!nccl_type(dtype, &t)) return fail(FMI_ERR_UNSUPPORTED, "path RCCL: RCCL has no 16-bit integer reductions");
+        FMI_NCCL(api_, ReduceScatter(send, recv, count, t, nccl_op(op), comm_, s));
         return FMI_OK;
     }
     int barrier_async(hipStream_t s) override {

@@ -134,11 +134,18 @@ int launch_combine(int op, int dtype, void* out, const void* a, const void* b, s
         const T* x = static_cast<const T*>(a);
         const T* y = static_cast<const T*>(b);
         if (aligned16(o) && aligned16(x) && aligned16(y)) {
-            switch (g_tune[FMI_TUNE_PAIR_VARIANT].load()) {
-                case 2: return launch_pair_vec<Op, T, 3>(o, x, y, n, s);  // nt loads + nt stores
-                case 3: return launch_pair_vec<Op, T, 1>(o, x, y, n, s);  // nt loads only
-                case 4: return launch_pair_vec<Op, T, 2>(o, x, y, n, s);  // nt stores only
-                default: return launch_pair_vec<Op, T, 0>(o, x, y, n, s);
+            // The cache-policy variants are instantiated for the core dtypes only (tools/tune_pair.py
+            // sweeps them); the other integer widths always take the default policy.
+            if constexpr (!(std::is_same_v<T, float> || std::is_same_v<T, double> || std::is_same_v<T, int32_t> ||
+                            std::is_same_v<T, int64_t>)) {
+                return launch_pair_vec<Op, T, 3>(o, x, y, n, s);
+            } else {
+                switch (g_tune[FMI_TUNE_PAIR_VARIANT].load()) {
+                    case 2: return launch_pair_vec<Op, T, 3>(o, x, y, n, s);  // nt loads + nt stores
+                    case 3: return launch_pair_vec<Op, T, 1>(o, x, y, n, s);  // nt loads only
+                    case 4: return launch_pair_vec<Op, T, 2>(o, x, y, n, s);  // nt stores only
+                    default: return launch_pair_vec<Op, T, 0>(o, x, y, n, s);
+                }
             }
         }
         const unsigned grid = static_cast<unsigned>(std::min<size_t>(grid_for(n, 256), 65536));
@@ -485,7 +492,7 @@ int fmi_dev_reduce_tree(int op, int dtype, int alg, void* out, const void* const
     for (int t = 0; t < P; ++t) order[t] = ins[alg == FMI_ALG_REDUCE ? (t + rank) % P : t];
     bool aligned = aligned16(out);
     for (int p = 0; p < P; ++p) aligned = aligned && aligned16(order[p]);
-    if (P >= 2 && P <= sched::kMaxFusedPeers && aligned) {
+    if (P >= 2 && P <= sched::kMaxFusedPeers && aligned && is_core_dtype(dtype)) {
         PeerPtrs ptrs{};
         for (int p = 0; p < P; ++p) ptrs.in[p] = order[p];
         ptrs.out[0] = out;
@@ -515,7 +522,7 @@ int fmi_dev_scan_peers(int op, int dtype, int alg, void* const* outs, const void
     hipStream_t s = resolve(stream);
     bool aligned = true;
     for (int p = 0; p < P; ++p) aligned = aligned && aligned16(ins[p]) && aligned16(outs[p]);
-    if (P >= 2 && P <= sched::kMaxFusedPeers && aligned) {
+    if (P >= 2 && P <= sched::kMaxFusedPeers && aligned && is_core_dtype(dtype)) {
         PeerPtrs ptrs{};
         for (int p = 0; p < P; ++p) {
             ptrs.in[p] = ins[p];
@@ -613,13 +620,11 @@ int fmi_dev_fill_synthetic(int dtype, void* buf, size_t n, uint64_t seed, uint32
     if (int rc = require_device()) return rc;
     hipStream_t s = resolve(stream);
     const unsigned grid = static_cast<unsigned>(std::min<size_t>(grid_for(n, 256), 16384));
-    switch (dtype) {
-        case FMI_F32: synth_kernel<float><<<grid, 256, 0, s>>>(static_cast<float*>(buf), n, seed, peer); break;
-        case FMI_F64: synth_kernel<double><<<grid, 256, 0, s>>>(static_cast<double*>(buf), n, seed, peer); break;
-        case FMI_I32: synth_kernel<int32_t><<<grid, 256, 0, s>>>(static_cast<int32_t*>(buf), n, seed, peer); break;
-        case FMI_I64: synth_kernel<int64_t><<<grid, 256, 0, s>>>(static_cast<int64_t*>(buf), n, seed, peer); break;
-        default: return fail(FMI_ERR_INVALID, "unknown dtype " + std::to_string(dtype));
-    }
+    if (int rc = with_dtype<true>(dtype, [&]<class T>() -> int {
+            synth_kernel<T><<<grid, 256, 0, s>>>(static_cast<T*>(buf), n, seed, peer);
+            return FMI_OK;
+        }))
+        return rc;
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail("synthetic fill launch", e);
     return FMI_OK;

@@ -41,7 +41,7 @@ template <int ALG, bool RANK_AWARE>
 int launch_fused(int op, int dtype, int P, const PeerPtrs& ptrs, size_t n, int rank, hipStream_t s) {
     if (P < 2 || P > sched::kMaxFusedPeers)
         return fail(FMI_ERR_INVALID, "fused kernel needs 2 <= P <= 16, got " + std::to_string(P));
-    return with_op_dtype(op, dtype, [&]<class Op, class T>() -> int {
+    return with_op_dtype<false>(op, dtype, [&]<class Op, class T>() -> int {
         constexpr bool order_sensitive =
             RANK_AWARE && std::is_floating_point_v<T> && (std::is_same_v<Op, OpMax> || std::is_same_v<Op, OpMin>);
         static constexpr auto table =

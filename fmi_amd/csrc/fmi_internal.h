@@ -23,17 +23,39 @@ hipStream_t library_stream();
 // at large P, better DRAM row locality. `wg_load_bytes_per_peer` = bytes one workgroup loads per peer.
 size_t fused_lds_bytes(int P, size_t wg_load_bytes_per_peer);
 
+// The dtypes every kernel is instantiated for (the fused P-way kernels included).
+inline bool is_core_dtype(int dtype) { return dtype >= FMI_F32 && dtype <= FMI_I64; }
+
+// Invoke f.template operator()<T>() for a runtime dtype (ALL: every fmi_dtype_t; else the core four);
+// returns FMI_ERR_INVALID if unknown.
+template <bool ALL, class F>
+int with_dtype(int dtype, F&& f) {
+    switch (dtype) {
+        case FMI_F32: return f.template operator()<float>();
+        case FMI_F64: return f.template operator()<double>();
+        case FMI_I32: return f.template operator()<int32_t>();
+        case FMI_I64: return f.template operator()<int64_t>();
+        default: break;
+    }
+    if constexpr (ALL) {
+        switch (dtype) {
+            case FMI_U32: return f.template operator()<uint32_t>();
+            case FMI_U64: return f.template operator()<uint64_t>();
+            case FMI_I8: return f.template operator()<int8_t>();
+            case FMI_U8: return f.template operator()<uint8_t>();
+            case FMI_I16: return f.template operator()<int16_t>();
+            case FMI_U16: return f.template operator()<uint16_t>();
+            default: break;
+        }
+    }
+    return fail(FMI_ERR_INVALID, "unknown dtype " + std::to_string(dtype));
+}
+
 // Invoke f.template operator()<Op, T>() for a runtime (op, dtype); returns FMI_ERR_INVALID if unknown.
-template <class F>
+template <bool ALL = true, class F>
 int with_op_dtype(int op, int dtype, F&& f) {
     auto by_dtype = [&]<class Op>() -> int {
-        switch (dtype) {
-            case FMI_F32: return f.template operator()<Op, float>();
-            case FMI_F64: return f.template operator()<Op, double>();
-            case FMI_I32: return f.template operator()<Op, int32_t>();
-            case FMI_I64: return f.template operator()<Op, int64_t>();
-            default: return fail(FMI_ERR_INVALID, "unknown dtype " + std::to_string(dtype));
-        }
+        return with_dtype<ALL>(dtype, [&]<class T>() -> int { return f.template operator()<Op, T>(); });
     };
     switch (op) {
         case FMI_OP_SUM: return by_dtype.template operator()<OpSum>();
@@ -46,10 +68,10 @@ int with_op_dtype(int op, int dtype, F&& f) {
 
 inline size_t dtype_size(int dtype) {
     switch (dtype) {
-        case FMI_F32: return 4;
-        case FMI_F64: return 8;
-        case FMI_I32: return 4;
-        case FMI_I64: return 8;
+        case FMI_F32: case FMI_I32: case FMI_U32: return 4;
+        case FMI_F64: case FMI_I64: case FMI_U64: return 8;
+        case FMI_I8: case FMI_U8: return 1;
+        case FMI_I16: case FMI_U16: return 2;
         default: return 0;
     }
 }

@@ -42,6 +42,24 @@ template <>
 struct Wrap<int64_t> {
     using type = uint64_t;
 };
+// Sub-dword integers compute in 32 bits (no promotion to a signed int that could overflow) and keep the
+// low bits on conversion back, as the reference's std::plus / std::multiplies on A do.
+template <>
+struct Wrap<int8_t> {
+    using type = uint32_t;
+};
+template <>
+struct Wrap<uint8_t> {
+    using type = uint32_t;
+};
+template <>
+struct Wrap<int16_t> {
+    using type = uint32_t;
+};
+template <>
+struct Wrap<uint16_t> {
+    using type = uint32_t;
+};
 
 struct OpSum {
     template <class T>
@@ -299,10 +317,10 @@ __host__ __device__ __forceinline__ T synth_value(uint64_t h) {
         return static_cast<float>(h >> 40) * 0x1p-24f * 2.0f - 1.0f;
     } else if constexpr (std::is_same_v<T, double>) {
         return static_cast<double>(h >> 11) * 0x1p-53 * 2.0 - 1.0;
-    } else if constexpr (std::is_same_v<T, int32_t>) {
-        return static_cast<int32_t>(static_cast<uint32_t>(h >> 32));
     } else {
-        return static_cast<int64_t>(h);
+        // integers: the top 8·sizeof(T) bits of h (i32 = h >> 32, i64 = h, as before)
+        using U = std::make_unsigned_t<T>;
+        return static_cast<T>(static_cast<U>(h >> (64 - 8 * sizeof(T))));
     }
 }
 

@@ -25,10 +25,18 @@ class Op(enum.IntEnum):
 
 
 class DType(enum.IntEnum):
+    """fmi_dtype_t. F32 / F64 / I32 / I64 run every kernel; the other integer widths run the pairwise
+    kernel, and their P-way programs run as pairwise passes."""
     F32 = 0
     F64 = 1
     I32 = 2
     I64 = 3
+    U32 = 4
+    U64 = 5
+    I8 = 6
+    U8 = 7
+    I16 = 8
+    U16 = 9
 
 
 class Alg(enum.IntEnum):
@@ -50,7 +58,9 @@ class Tune(enum.IntEnum):
     FUSED_INFLIGHT_KIB = 6
 
 
-NP_DTYPE = {DType.F32: np.float32, DType.F64: np.float64, DType.I32: np.int32, DType.I64: np.int64}
+NP_DTYPE = {DType.F32: np.float32, DType.F64: np.float64, DType.I32: np.int32, DType.I64: np.int64,
+            DType.U32: np.uint32, DType.U64: np.uint64, DType.I8: np.int8, DType.U8: np.uint8, DType.I16: np.int16,
+            DType.U16: np.uint16}
 
 
 def dtype_of(arr_or_dtype) -> DType:
@@ -61,7 +71,7 @@ def dtype_of(arr_or_dtype) -> DType:
     for k, v in NP_DTYPE.items():
         if np.dtype(v) == dt:
             return k
-    raise TypeError(f"unsupported bucket dtype {dt}; FMI device buckets are f32, f64, i32 or i64")
+    raise TypeError(f"unsupported bucket dtype {dt}; FMI device buckets are f32, f64 or 8/16/32/64-bit integers")
 
 
 def _ptr(x) -> Optional[int]:

@@ -53,7 +53,15 @@ typedef enum {
 /* ---- op / dtype / algorithm descriptors -------------------------------------------------------- */
 /* Op ids mirror the reference Python enum SUM/PROD/MAX/MIN (reference python/PythonCommunicator.h:13-15). */
 typedef enum { FMI_OP_SUM = 0, FMI_OP_PROD = 1, FMI_OP_MAX = 2, FMI_OP_MIN = 3 } fmi_op_t;
-typedef enum { FMI_F32 = 0, FMI_F64 = 1, FMI_I32 = 2, FMI_I64 = 3 } fmi_dtype_t;
+/* Element types. The reference's buckets are Data<std::vector<A>> for any fundamental A
+ * (include/comm/Data.h:50-73); f32 / f64 / i32 / i64 run every kernel, including the fused P-way ones.
+ * The other integer widths run the pairwise kernel, and their P-way programs run as pairwise passes in
+ * the same order (integer results do not depend on it). Integer sum / prod wrap, as the reference's
+ * std::plus / std::multiplies do after conversion back to A. */
+typedef enum {
+    FMI_F32 = 0, FMI_F64 = 1, FMI_I32 = 2, FMI_I64 = 3,
+    FMI_U32 = 4, FMI_U64 = 5, FMI_I8 = 6, FMI_U8 = 7, FMI_I16 = 8, FMI_U16 = 9
+} fmi_dtype_t;
 
 /* Evaluation orders reproduced by the P-way kernels; each is the combine order of one reference
  * collective, so a P-bucket reduction on one device is bit-identical to the distributed one. */

@@ -95,10 +95,10 @@ def synthetic_at(dtype, idx: np.ndarray, seed: int, peer: int) -> np.ndarray:
     if dtype == np.float64:
         u = (h >> np.uint64(11)).astype(np.float64) * (2.0 ** -53)
         return u * 2.0 - 1.0
-    if dtype == np.int32:
-        return (h >> np.uint64(32)).astype(np.uint32).view(np.int32)
-    if dtype == np.int64:
-        return h.view(np.int64)
+    if dtype.kind in "iu":  # the top 8·itemsize bits of h (i32 = h >> 32, i64 = h)
+        bits = 8 * dtype.itemsize
+        top = (h >> np.uint64(64 - bits)) if bits < 64 else h
+        return top.astype(np.dtype(f"u{dtype.itemsize}")).view(dtype)
     raise TypeError(f"unsupported dtype {dtype}")
 
 

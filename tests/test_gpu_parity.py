@@ -16,12 +16,15 @@ from oracle import fmi_oracle as orc
 pytestmark = pytest.mark.gpu
 
 DTYPES = [np.float32, np.float64, np.int32, np.int64]
+# the other fundamental integer widths (pairwise kernel; P-way programs as pairwise passes)
+EXTRA_DTYPES = [np.uint32, np.uint64, np.int8, np.uint8, np.int16, np.uint16]
+ALL_DTYPES = DTYPES + EXTRA_DTYPES
 OPS = [Op.SUM, Op.PROD, Op.MAX, Op.MIN]
 OPNAME = {Op.SUM: "sum", Op.PROD: "prod", Op.MAX: "max", Op.MIN: "min"}
 RAGGED = [0, 1, 2, 3, 4, 5, 7, 8, 9, 15, 17, 1027, 4099, 65536 + 3]
 
 
-UINT = {4: np.uint32, 8: np.uint64}
+UINT = {1: np.uint8, 2: np.uint16, 4: np.uint32, 8: np.uint64}
 
 
 def assert_bit_equal(got, want, what=""):
@@ -48,9 +51,12 @@ def inputs(dtype, n, peer, seed=42):
         if np.issubdtype(dtype, np.floating):
             edge = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, np.finfo(dtype).tiny / 4, -np.finfo(dtype).max,
                              np.finfo(dtype).smallest_subnormal], dtype=dtype)
-        else:
+        elif np.issubdtype(dtype, np.signedinteger):
             info = np.iinfo(dtype)
             edge = np.array([info.min, info.max, 0, -1, 1, info.min + 1, info.max - 1, 2], dtype=dtype)
+        else:
+            info = np.iinfo(dtype)
+            edge = np.array([0, info.max, 1, info.max - 1, 2, info.max // 2, info.max // 2 + 1, 3], dtype=dtype)
         idx = (np.arange(8) * 7919 + peer * 13) % n
         x[idx] = np.roll(edge, peer)
     return x
@@ -63,7 +69,7 @@ def dev(arr):
 # ------------------------------------------------------------------------------------------------
 # pairwise combine — the hot path (reference include/Communicator.h:180-189)
 # ------------------------------------------------------------------------------------------------
-@pytest.mark.parametrize("dtype", DTYPES, ids=lambda d: np.dtype(d).name)
+@pytest.mark.parametrize("dtype", ALL_DTYPES, ids=lambda d: np.dtype(d).name)
 @pytest.mark.parametrize("op", OPS, ids=lambda o: o.name)
 def test_reduce_pair_ragged(device, op, dtype):
     for n in RAGGED:
@@ -76,7 +82,7 @@ def test_reduce_pair_ragged(device, op, dtype):
         assert_bit_equal(db.numpy(), b, "in operand must stay untouched")
 
 
-@pytest.mark.parametrize("dtype", DTYPES, ids=lambda d: np.dtype(d).name)
+@pytest.mark.parametrize("dtype", ALL_DTYPES, ids=lambda d: np.dtype(d).name)
 def test_reduce_pair_unaligned_views(device, dtype):
     n = 4099
     a, b = inputs(dtype, n + 8, 0), inputs(dtype, n + 8, 1)
@@ -144,7 +150,7 @@ def test_stream_wait_event_orders_cross_stream_work(device):
 
 
 def test_synthetic_matches_host_generator(device):
-    for dtype in DTYPES:
+    for dtype in ALL_DTYPES:
         for peer in (0, 1, 7):
             n = 100003
             d = Bucket(n, dtype).fill_synthetic(42, peer)
@@ -241,6 +247,33 @@ def test_fused_occupancy_cap_keeps_bits(device, cap):
             assert_bit_equal(outs[k].numpy(), want_sc[k], f"scan cap {cap} peer {k}")
     finally:
         fmi_amd.tune_set(Tune.FUSED_INFLIGHT_KIB, old)
+
+
+@pytest.mark.parametrize("dtype", EXTRA_DTYPES, ids=lambda d: np.dtype(d).name)
+def test_extra_dtypes_p_way_programs(device, dtype):
+    """The other integer widths through every P-way entry point (pairwise passes in the reference's order),
+    P covering the fused range and beyond, against the oracle's message simulation."""
+    n = 1029
+    for P in (3, 8, 17):
+        xs = _peer_inputs(dtype, n, P)
+        ins = [dev(x) for x in xs]
+        for op in OPS:
+            f = orc.OPS[OPNAME[op]]
+            with np.errstate(all="ignore"):
+                want_ar, _ = orc.allreduce(xs, f)
+                want_red, _ = orc.reduce(xs, f, root=1)
+                want_sc, _ = orc.scan(xs, f)
+                want_ltr, _ = orc.scan(xs, f, commutative=False, associative=False)
+            out = Bucket(n, dtype)
+            fmi_amd.reduce_tree(op, Alg.ALLREDUCE, out, ins, rank=P - 1)
+            assert_bit_equal(out.numpy(), want_ar[P - 1], f"allreduce P={P} {op.name}")
+            fmi_amd.reduce_tree(op, Alg.REDUCE, out, ins, rank=1)
+            assert_bit_equal(out.numpy(), want_red, f"reduce P={P} {op.name}")
+            for alg, want in ((Alg.SCAN, want_sc), (Alg.SCAN_LTR, want_ltr)):
+                outs = [Bucket(n, dtype) for _ in range(P)]
+                fmi_amd.scan_peers(op, alg, outs, ins)
+                for k in range(P):
+                    assert_bit_equal(outs[k].numpy(), want[k], f"{alg.name} P={P} {op.name} peer {k}")
 
 
 def test_scan_in_place(device):
