@@ -91,10 +91,20 @@ struct OpMin {
 // ---------------------------------------------------------------------------------------------------
 // 16-byte lane groups and their loads/stores.
 // ---------------------------------------------------------------------------------------------------
-template <class T, int W>
-struct alignas(sizeof(T) * W) Lanes {
+// Sub-dword elements are held as a clang vector (<16 x i8>, <8 x i16>): reinterpreting one as 32-bit
+// words is then free, where a plain array is split per element and reassembled (it turned the 16-B loads
+// of the 8-bit kernels into 2-byte ones).
+template <class T, int W, bool VEC = (sizeof(T) < 4 && W > 1)>
+struct LaneStorage {
     T v[W];
 };
+template <class T, int W>
+struct LaneStorage<T, W, true> {
+    T __attribute__((ext_vector_type(W))) v;
+};
+
+template <class T, int W>
+struct alignas(sizeof(T) * W) Lanes : LaneStorage<T, W> {};
 
 template <class T>
 inline constexpr int kVecLanes = 16 / static_cast<int>(sizeof(T));
@@ -120,12 +130,50 @@ __device__ __forceinline__ void store_lanes(T* p, const Lanes<T, W>& x) {
     }
 }
 
+// 8-bit lanes, four bytes per 32-bit word: sum by SWAR (the carry out of each byte is dropped, exactly
+// the wrap of the per-byte add), max / min on packed 16-bit halves (even bytes and odd bytes, widened with
+// their sign or zero), one or two instructions per 2-4 bytes instead of several per byte.
+using u16x2 = unsigned short __attribute__((ext_vector_type(2)));
+using i16x2 = short __attribute__((ext_vector_type(2)));
+
+template <class Op, class T>
+__device__ __forceinline__ uint32_t combine_bytes(uint32_t a, uint32_t b) {
+    if constexpr (std::is_same_v<Op, OpSum>) {
+        return ((a & 0x7F7F7F7Fu) + (b & 0x7F7F7F7Fu)) ^ ((a ^ b) & 0x80808080u);
+    } else {
+        using V = std::conditional_t<std::is_signed_v<T>, i16x2, u16x2>;
+        const V a16 = __builtin_bit_cast(V, a), b16 = __builtin_bit_cast(V, b);
+        const V ae = (a16 << 8) >> 8, be = (b16 << 8) >> 8;  // even bytes, widened
+        const V ao = a16 >> 8, bo = b16 >> 8;                  // odd bytes, widened
+        V e, o;
+        if constexpr (std::is_same_v<Op, OpMax>) {
+            e = __builtin_elementwise_max(ae, be);
+            o = __builtin_elementwise_max(ao, bo);
+        } else {
+            e = __builtin_elementwise_min(ae, be);
+            o = __builtin_elementwise_min(ao, bo);
+        }
+        return (__builtin_bit_cast(uint32_t, e) & 0x00FF00FFu) | ((__builtin_bit_cast(uint32_t, o) & 0x00FF00FFu) << 8);
+    }
+}
+
 template <class Op, class T, int W>
 __device__ __forceinline__ Lanes<T, W> combine(const Lanes<T, W>& a, const Lanes<T, W>& b) {
-    Lanes<T, W> r;
+    if constexpr (sizeof(T) == 1 && W % 4 == 0 && !std::is_same_v<Op, OpProd>) {
+        struct Words {
+            uint32_t w[W / 4];
+        };
+        const Words x = __builtin_bit_cast(Words, a), y = __builtin_bit_cast(Words, b);
+        Words r;
 #pragma unroll
-    for (int k = 0; k < W; ++k) r.v[k] = Op::template apply<T>(a.v[k], b.v[k]);
-    return r;
+        for (int k = 0; k < W / 4; ++k) r.w[k] = combine_bytes<Op, T>(x.w[k], y.w[k]);
+        return __builtin_bit_cast(Lanes<T, W>, r);
+    } else {
+        Lanes<T, W> r;
+#pragma unroll
+        for (int k = 0; k < W; ++k) r.v[k] = Op::template apply<T>(a.v[k], b.v[k]);
+        return r;
+    }
 }
 
 // ---------------------------------------------------------------------------------------------------

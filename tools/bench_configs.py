@@ -71,10 +71,11 @@ def main():
         return
 
     # C2 and its siblings: pairwise combine, every dtype/op, 256 MiB buckets, 4 rotating sets
-    for dt in (np.float32, np.float64, np.int32, np.int64):
+    for dt in (np.float32, np.float64, np.int32, np.int64, np.uint32, np.uint64, np.int8, np.uint8, np.int16, np.uint16):
         n = 256 * MIB // np.dtype(dt).itemsize
         sets = [(Bucket(n, dt).fill_synthetic(42 + s, 0), Bucket(n, dt).fill_synthetic(42 + s, 1)) for s in range(4)]
-        for op in (Op.SUM, Op.MAX) if not args.quick else (Op.SUM,):
+        core = np.dtype(dt) in (np.dtype(np.float32), np.dtype(np.float64), np.dtype(np.int32), np.dtype(np.int64))
+        for op in (Op.SUM, Op.MAX) if (core and not args.quick) else (Op.SUM,):
             med, mn = timed(lambda k: fmi_amd.reduce_pair(op, *sets[k]), it, 4)
             row(f"pair {op.name.lower()} {np.dtype(dt).name} 256MiB", 3 * 256 * MIB, med, mn)
         del sets
