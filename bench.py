@@ -95,6 +95,10 @@ def cpu_baseline(args):
         out = subprocess.run([exe, "--mode", "bare", "--dtype", "f32", "--op", "sum", "--mib", str(args.bucket_mib),
                               "--reps", "9"], check=True, capture_output=True, text=True, timeout=600)
         bare = json.loads(out.stdout.strip().splitlines()[-1])
+        # the same loop over the host threads this job may use (OMP_NUM_THREADS): a CPU roofline for scale
+        out = subprocess.run([exe, "--mode", "omp", "--dtype", "f32", "--op", "sum", "--mib", str(args.bucket_mib),
+                              "--reps", "9"], check=True, capture_output=True, text=True, timeout=600)
+        omp = json.loads(out.stdout.strip().splitlines()[-1])
     except Exception as e:  # the baseline is reported, never required
         return {"error": str(e)}
     model = ""
@@ -116,6 +120,8 @@ def cpu_baseline(args):
                    f"1 thread: {bare['median_ms']:.2f} ms = {bare['bucket_gib_s']:.2f} GiB/s; host '{model}', "
                    f"{os.cpu_count()} CPUs visible"),
         "bare_loop_gib_s": round(bare["bucket_gib_s"], 4),
+        "all_threads_loop": {"gib_s": round(omp["bucket_gib_s"], 4), "threads": omp["threads"],
+                             "median_ms": round(omp["median_ms"], 3)},
         "c1": c1_host(),
     }
 
