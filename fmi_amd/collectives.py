@@ -24,7 +24,7 @@ RCCL and our kernels share one runtime, one set of streams and one address space
 """
 from __future__ import annotations
 
-from typing import List, Optional, Sequence
+from typing import List, Sequence
 
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402

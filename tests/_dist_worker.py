@@ -13,7 +13,7 @@ import torch
 import torch.distributed as dist
 
 from fmi_amd import collectives
-from fmi_amd.device import Alg, Op
+from fmi_amd.device import Op
 
 _ELEM = {
     Op.SUM: lambda a, b: a + b,
