@@ -1,7 +1,8 @@
 """Python handle over the C-ABI communicator (include/fmi_dev.h, "sharded device collectives").
 
 `Comm` wraps fmi_comm_*: sharded allreduce / reduce / scan of device buckets across ranks (one rank per
-GPU over RCCL, or ranks as threads of one process over the LOCAL transport), with the combine done by the
+GPU over RCCL, ranks as threads of one process over the LOCAL transport, or processes of one node over
+PROC), with the combine done by the
 fused kernels in the reference's evaluation order (reference src/comm/PeerToPeer.cpp). Buffers are
 `fmi_amd.Bucket`s or raw device pointers.
 """
@@ -22,6 +23,7 @@ ID_BYTES = 128
 class Transport(enum.IntEnum):
     RCCL = 0
     LOCAL = 1
+    PROC = 2  # ranks are processes of one node (same or different GPUs): shared-memory staging + HIP IPC windows
 
 
 class Path(enum.IntEnum):

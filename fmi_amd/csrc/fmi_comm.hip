@@ -14,12 +14,17 @@
 // copies) — the latter runs the exact same schedules, which is how the multi-rank logic is tested on a
 // single MI355X.
 #include <dlfcn.h>
+#include <fcntl.h>
 #include <rccl/rccl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
 #include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <deque>
@@ -28,6 +33,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "fmi_internal.h"
@@ -469,6 +475,279 @@ private:
 };
 
 // ---------------------------------------------------------------------------------------------------
+// PROC: ranks are processes of one node. One POSIX shared-memory segment per communicator holds a control
+// block (barrier, point-to-point mailboxes, window IPC handles) and one staging slot per rank, page-locked
+// in every process so the slots move at DMA rate. Every exchange is: write my part into my slot, barrier,
+// read the parts I need from the peers' slots, barrier — in pieces of the slot size.
+// ---------------------------------------------------------------------------------------------------
+constexpr char kProcMagic[8] = {'F', 'M', 'I', 'P', 'R', 'O', 'C', '\0'};
+constexpr int kProcMaxRanks = 64;
+constexpr size_t kProcSlot = size_t(32) << 20;
+constexpr size_t kProcCtrlBytes = size_t(64) << 10;
+
+struct ProcCtrl {  // lives in the shared segment; all-zero is the initial state
+    std::atomic<uint64_t> arrived;
+    std::atomic<uint64_t> generation;
+    struct Mail {  // what rank src's slot holds for point-to-point: a message for `dst` until ack == seq
+        std::atomic<int> dst;
+        std::atomic<uint64_t> bytes;
+        std::atomic<uint64_t> seq;
+        std::atomic<uint64_t> ack;
+    } mail[kProcMaxRanks];
+    hipIpcMemHandle_t handle[kProcMaxRanks];
+    std::atomic<int> ok[kProcMaxRanks];
+};
+static_assert(sizeof(ProcCtrl) <= kProcCtrlBytes, "control block");
+
+std::string proc_shm_name(const void* id) {
+    uint64_t key;
+    std::memcpy(&key, static_cast<const char*>(id) + 8, 8);
+    char name[64];
+    std::snprintf(name, sizeof(name), "/fmi_proc_%016llx", static_cast<unsigned long long>(key));
+    return name;
+}
+
+class ProcTransport final : public Transport {
+public:
+    ProcTransport(int n, int rank) : Transport(n, rank) {}
+    ~ProcTransport() override {
+        if (registered_) (void)hipHostUnregister(base_);
+        if (base_) munmap(base_, bytes_);
+        if (fd_ >= 0) close(fd_);
+        if (!unlinked_ && !name_.empty()) shm_unlink(name_.c_str());
+    }
+
+    // Collective: map the segment, then a barrier; rank 0 unlinks the name once everyone holds it.
+    int join(const void* id) {
+        if (n_ > kProcMaxRanks) return fail(FMI_ERR_INVALID, "PROC transport: at most 64 ranks");
+        name_ = proc_shm_name(id);
+        bytes_ = kProcCtrlBytes + static_cast<size_t>(n_) * kProcSlot;
+        fd_ = shm_open(name_.c_str(), O_CREAT | O_RDWR, 0600);
+        if (fd_ < 0) return fail(FMI_ERR_COMM, "shm_open(" + name_ + "): " + std::strerror(errno));
+        struct stat st{};
+        if (fstat(fd_, &st) != 0) return fail(FMI_ERR_COMM, std::string("fstat: ") + std::strerror(errno));
+        if (st.st_size != 0 && static_cast<size_t>(st.st_size) != bytes_)
+            return fail(FMI_ERR_INVALID, "PROC communicator joined with a different size");
+        if (st.st_size == 0 && ftruncate(fd_, static_cast<off_t>(bytes_)) != 0)
+            return fail(FMI_ERR_COMM, std::string("ftruncate: ") + std::strerror(errno));
+        void* m = mmap(nullptr, bytes_, PROT_READ | PROT_WRITE, MAP_SHARED, fd_, 0);
+        if (m == MAP_FAILED) return fail(FMI_ERR_COMM, std::string("mmap: ") + std::strerror(errno));
+        base_ = static_cast<char*>(m);
+        ctrl_ = reinterpret_cast<ProcCtrl*>(base_);
+        if (int rc = host_barrier("join")) return rc;
+        if (rank_ == 0) shm_unlink(name_.c_str());
+        unlinked_ = true;
+        return FMI_OK;
+    }
+
+    int all_to_all(const char* send, char* recv, size_t bytes, hipStream_t s) override {
+        const size_t c = std::max<size_t>(1, kProcSlot / static_cast<size_t>(n_));
+        return pieces(bytes, c, s,
+                      [&](size_t o, size_t len) -> int {
+                          for (int d = 0; d < n_; ++d)
+                              FMI_COMM_HIP(hipMemcpyAsync(slot(rank_) + d * c, send + d * bytes + o, len, hipMemcpyDeviceToHost, s));
+                          return FMI_OK;
+                      },
+                      [&](size_t o, size_t len) -> int {
+                          for (int j = 0; j < n_; ++j)
+                              FMI_COMM_HIP(hipMemcpyAsync(recv + j * bytes + o, slot(j) + rank_ * c, len, hipMemcpyHostToDevice, s));
+                          return FMI_OK;
+                      });
+    }
+    int all_gather(const char* send, char* recv, size_t bytes, hipStream_t s) override {
+        return gather_to(send, recv, bytes, -1, s);
+    }
+    int gather(const char* send, char* recv, size_t bytes, int root, hipStream_t s) override {
+        return gather_to(send, recv, bytes, root, s);
+    }
+    int scatter(const char* send, char* recv, size_t bytes, int root, hipStream_t s) override {
+        const size_t c = std::max<size_t>(1, kProcSlot / static_cast<size_t>(n_));
+        return pieces(bytes, c, s,
+                      [&](size_t o, size_t len) -> int {
+                          if (rank_ != root) return FMI_OK;
+                          for (int d = 0; d < n_; ++d)
+                              FMI_COMM_HIP(hipMemcpyAsync(slot(root) + d * c, send + d * bytes + o, len, hipMemcpyDeviceToHost, s));
+                          return FMI_OK;
+                      },
+                      [&](size_t o, size_t len) -> int {
+                          FMI_COMM_HIP(hipMemcpyAsync(recv + o, slot(root) + rank_ * c, len, hipMemcpyHostToDevice, s));
+                          return FMI_OK;
+                      });
+    }
+    int bcast(char* buf, size_t bytes, int root, hipStream_t s) override {
+        return pieces(bytes, kProcSlot, s,
+                      [&](size_t o, size_t len) -> int {
+                          if (rank_ == root) FMI_COMM_HIP(hipMemcpyAsync(slot(root), buf + o, len, hipMemcpyDeviceToHost, s));
+                          return FMI_OK;
+                      },
+                      [&](size_t o, size_t len) -> int {
+                          if (rank_ != root) FMI_COMM_HIP(hipMemcpyAsync(buf + o, slot(root), len, hipMemcpyHostToDevice, s));
+                          return FMI_OK;
+                      });
+    }
+    // Rendezvous point-to-point through the sender's slot: one message in flight per sender, consumed
+    // (ack == seq) before the next is written.
+    int send(const char* buf, size_t bytes, int peer, hipStream_t s) override {
+        FMI_COMM_RC(ensure_registered());
+        auto& m = ctrl_->mail[rank_];
+        size_t o = 0;
+        do {
+            const size_t len = std::min(kProcSlot, bytes - o);
+            FMI_COMM_RC(wait_until([&] { return m.ack.load(std::memory_order_acquire) == m.seq.load(std::memory_order_acquire); }, "send"));
+            if (len) {
+                FMI_COMM_HIP(hipMemcpyAsync(slot(rank_), buf + o, len, hipMemcpyDeviceToHost, s));
+                FMI_COMM_HIP(hipStreamSynchronize(s));
+            }
+            m.dst.store(peer, std::memory_order_relaxed);
+            m.bytes.store(len, std::memory_order_relaxed);
+            const uint64_t seq = m.seq.fetch_add(1, std::memory_order_acq_rel) + 1;
+            FMI_COMM_RC(wait_until([&] { return m.ack.load(std::memory_order_acquire) == seq; }, "send (ack)"));
+            o += len;
+        } while (o < bytes);
+        return FMI_OK;
+    }
+    int recv(char* buf, size_t bytes, int peer, hipStream_t s) override {
+        FMI_COMM_RC(ensure_registered());
+        auto& m = ctrl_->mail[peer];
+        size_t o = 0;
+        do {
+            FMI_COMM_RC(wait_until([&] {
+                return m.dst.load(std::memory_order_acquire) == rank_ &&
+                       m.seq.load(std::memory_order_acquire) != m.ack.load(std::memory_order_acquire);
+            }, "recv"));
+            const size_t len = m.bytes.load(std::memory_order_relaxed);
+            if (o + len > bytes) return fail(FMI_ERR_COMM, "PROC transport: message longer than the receive buffer");
+            if (len) {
+                FMI_COMM_HIP(hipMemcpyAsync(buf + o, slot(peer), len, hipMemcpyHostToDevice, s));
+                FMI_COMM_HIP(hipStreamSynchronize(s));
+            }
+            m.ack.store(m.seq.load(std::memory_order_acquire), std::memory_order_release);
+            o += len;
+        } while (o < bytes);
+        return FMI_OK;
+    }
+    int barrier(hipStream_t s) override {
+        FMI_COMM_HIP(hipStreamSynchronize(s));
+        return host_barrier("barrier");
+    }
+    int barrier_async(hipStream_t s) override { return barrier(s); }
+    // HIP IPC handles through the control block; all-or-nothing like the RCCL transport's.
+    int map_window(char* base, bool ok, std::vector<char*>& peers, hipStream_t s) override {
+        FMI_COMM_HIP(hipStreamSynchronize(s));
+        hipIpcMemHandle_t mine{};
+        if (ok) ok = hipIpcGetMemHandle(&mine, base) == hipSuccess;
+        ctrl_->handle[rank_] = mine;
+        ctrl_->ok[rank_].store(ok ? 1 : 0, std::memory_order_release);
+        FMI_COMM_RC(host_barrier("window (export)"));
+        bool all = true;
+        for (int j = 0; j < n_; ++j) all = all && ctrl_->ok[j].load(std::memory_order_acquire) == 1;
+        peers.assign(n_, nullptr);
+        peers[rank_] = base;
+        bool opened = all;
+        for (int j = 0; j < n_ && opened; ++j) {
+            if (j == rank_) continue;
+            void* p = nullptr;
+            if (hipIpcOpenMemHandle(&p, ctrl_->handle[j], hipIpcMemLazyEnablePeerAccess) != hipSuccess) opened = false;
+            peers[j] = static_cast<char*>(p);
+        }
+        FMI_COMM_RC(host_barrier("window (flags read)"));
+        ctrl_->ok[rank_].store(opened ? 1 : 0, std::memory_order_release);
+        FMI_COMM_RC(host_barrier("window (map)"));
+        for (int j = 0; j < n_; ++j) opened = opened && ctrl_->ok[j].load(std::memory_order_acquire) == 1;
+        FMI_COMM_RC(host_barrier("window (result read)"));
+        if (!opened) {
+            unmap_window(peers);
+            peers.clear();
+            return fail(FMI_ERR_COMM, "window: a rank could not export or map its window (IPC)");
+        }
+        return FMI_OK;
+    }
+    void unmap_window(const std::vector<char*>& peers) override {
+        for (int j = 0; j < static_cast<int>(peers.size()); ++j)
+            if (j != rank_ && peers[j]) (void)hipIpcCloseMemHandle(peers[j]);
+    }
+
+private:
+    char* slot(int r) const { return base_ + kProcCtrlBytes + static_cast<size_t>(r) * kProcSlot; }
+
+    int ensure_registered() {
+        if (registered_) return FMI_OK;
+        FMI_COMM_HIP(hipHostRegister(base_ + kProcCtrlBytes, bytes_ - kProcCtrlBytes, hipHostRegisterDefault));
+        registered_ = true;
+        return FMI_OK;
+    }
+
+    // Split `bytes` per destination into pieces of `c`; each piece: write(o, len), sync, barrier,
+    // read(o, len), sync, barrier (the second barrier frees the slots for the next piece).
+    template <class W, class Rd>
+    int pieces(size_t bytes, size_t c, hipStream_t s, W&& write, Rd&& read) {
+        FMI_COMM_RC(ensure_registered());
+        FMI_COMM_HIP(hipStreamSynchronize(s));
+        for (size_t o = 0; o < bytes; o += c) {
+            const size_t len = std::min(c, bytes - o);
+            FMI_COMM_RC(write(o, len));
+            FMI_COMM_HIP(hipStreamSynchronize(s));
+            FMI_COMM_RC(host_barrier("exchange (published)"));
+            FMI_COMM_RC(read(o, len));
+            FMI_COMM_HIP(hipStreamSynchronize(s));
+            FMI_COMM_RC(host_barrier("exchange (consumed)"));
+        }
+        return FMI_OK;
+    }
+
+    int gather_to(const char* send, char* recv, size_t bytes, int root, hipStream_t s) {
+        return pieces(bytes, kProcSlot, s,
+                      [&](size_t o, size_t len) -> int {
+                          FMI_COMM_HIP(hipMemcpyAsync(slot(rank_), send + o, len, hipMemcpyDeviceToHost, s));
+                          return FMI_OK;
+                      },
+                      [&](size_t o, size_t len) -> int {
+                          if (root >= 0 && rank_ != root) return FMI_OK;
+                          for (int j = 0; j < n_; ++j)
+                              FMI_COMM_HIP(hipMemcpyAsync(recv + j * bytes + o, slot(j), len, hipMemcpyHostToDevice, s));
+                          return FMI_OK;
+                      });
+    }
+
+    int host_barrier(const char* what) {
+        const uint64_t g = ctrl_->generation.load(std::memory_order_acquire);
+        if (ctrl_->arrived.fetch_add(1, std::memory_order_acq_rel) + 1 == static_cast<uint64_t>(n_)) {
+            ctrl_->arrived.store(0, std::memory_order_relaxed);
+            ctrl_->generation.fetch_add(1, std::memory_order_acq_rel);
+            return FMI_OK;
+        }
+        return wait_until([&] { return ctrl_->generation.load(std::memory_order_acquire) != g; }, what);
+    }
+
+    // Spin, then back off to short sleeps; give up after FMI_PROC_TIMEOUT_S (default 300 s) so a dead
+    // peer surfaces as an error instead of a hang.
+    template <class Pred>
+    int wait_until(Pred&& ready, const char* what) {
+        static const double limit = [] {
+            const char* e = std::getenv("FMI_PROC_TIMEOUT_S");
+            return e ? std::atof(e) : 300.0;
+        }();
+        const auto t0 = std::chrono::steady_clock::now();
+        for (int k = 0; !ready(); ++k) {
+            if (k < 1000) continue;
+            std::this_thread::sleep_for(std::chrono::microseconds(k < 10000 ? 5 : 200));
+            if ((k & 255) == 0 &&
+                std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > limit)
+                return fail(FMI_ERR_COMM, std::string("PROC transport: timed out waiting for peers (") + what + ")");
+        }
+        return FMI_OK;
+    }
+
+    std::string name_;
+    int fd_ = -1;
+    char* base_ = nullptr;
+    size_t bytes_ = 0;
+    ProcCtrl* ctrl_ = nullptr;
+    bool registered_ = false;
+    bool unlinked_ = false;
+};
+
+// ---------------------------------------------------------------------------------------------------
 // communicator
 // ---------------------------------------------------------------------------------------------------
 // Streams and events of the host-ingress pipeline (fmi_comm_allreduce_host), created on first use.
@@ -712,6 +991,13 @@ int fmi_comm_unique_id(int transport, void* id, size_t len) {
         std::memcpy(static_cast<char*>(id) + 8, &key, 8);
         return FMI_OK;
     }
+    if (transport == FMI_TRANSPORT_PROC) {
+        const uint64_t t = static_cast<uint64_t>(std::chrono::steady_clock::now().time_since_epoch().count());
+        const uint64_t key = (static_cast<uint64_t>(getpid()) << 40) ^ (g_hub_counter.fetch_add(1) << 24) ^ t;
+        std::memcpy(id, kProcMagic, 8);
+        std::memcpy(static_cast<char*>(id) + 8, &key, 8);
+        return FMI_OK;
+    }
     if (transport != FMI_TRANSPORT_RCCL) return fail(FMI_ERR_INVALID, "unknown transport");
     const RcclApi* api = rccl_api();
     if (!api) return FMI_ERR_COMM;
@@ -740,6 +1026,10 @@ int fmi_comm_init(fmi_comm_t* comm, const void* id, int nranks, int rank) {
         }
         if (hub->n != nranks) return fail(FMI_ERR_INVALID, "local communicator joined with a different size");
         c->t = std::make_unique<LocalTransport>(hub, nranks, rank);
+    } else if (std::memcmp(id, kProcMagic, 8) == 0) {
+        auto t = std::make_unique<ProcTransport>(nranks, rank);
+        FMI_COMM_RC(t->join(id));
+        c->t = std::move(t);
     } else {
         const RcclApi* api = rccl_api();
         if (!api) return FMI_ERR_COMM;

@@ -172,14 +172,17 @@ int fmi_host_reduce_pair(int op, int dtype, void* inout, const void* in, size_t 
  *   reduce: all-to-all -> fused kernel in reduce_no_order / reduce_ltr order for `root` -> gather.
  *   scan:   all-to-all -> fused peer-axis scan -> all-to-all back.
  * One rank = one peer = one GPU. Transports: FMI_TRANSPORT_RCCL (librccl, loaded on first use; with
- * torch imported first it is torch's copy) and FMI_TRANSPORT_LOCAL (ranks are threads of ONE process
+ * torch imported first it is torch's copy), FMI_TRANSPORT_LOCAL (ranks are threads of ONE process
  * sharing one device: the same schedules over device-to-device copies — used to test the multi-rank
- * schedules on a single GPU and to serve several peers co-resident on one GPU).
+ * schedules on a single GPU and to serve several peers co-resident on one GPU) and FMI_TRANSPORT_PROC
+ * (ranks are processes of one node, on the same or different GPUs: data staged through a page-locked
+ * POSIX shared-memory segment, windows mapped with HIP IPC — the same schedules again, so multi-process
+ * runs, FMI_PATH_DIRECT's cross-process mappings included, are testable on a single GPU).
  * All calls enqueue on `stream` (NULL = library stream); results are valid after fmi_stream_sync.
  * Buckets are device pointers; `send` is never modified; recv may alias send. */
 #define FMI_COMM_ID_BYTES 128
 typedef void* fmi_comm_t;
-typedef enum { FMI_TRANSPORT_RCCL = 0, FMI_TRANSPORT_LOCAL = 1 } fmi_transport_t;
+typedef enum { FMI_TRANSPORT_RCCL = 0, FMI_TRANSPORT_LOCAL = 1, FMI_TRANSPORT_PROC = 2 } fmi_transport_t;
 /* FMI_PATH_DIRECT: no RCCL data movement. `send` must lie in a window (fmi_comm_window_alloc, same offset on
  * every rank); rank k's fused kernel reads shard k of every rank's window over xGMI (IPC-mapped peer
  * memory) and reduces it in the reference's order, then every rank reads the N reduced shards from the

@@ -87,6 +87,37 @@ def test_comm_host_side_without_device():
     c1.destroy()
 
 
+_PROC_JOIN = """
+import sys
+from fmi_amd.comm import Comm
+c = Comm(bytes.fromhex(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]))
+c.destroy()
+"""
+
+
+def test_proc_transport_join_and_timeout():
+    """PROC ids carry their magic; N processes join one shared-memory segment (a host barrier) and the
+    name is unlinked once all hold it; a rank whose peers never arrive fails with an error, not a hang."""
+    import subprocess
+    import sys
+
+    from fmi_amd.comm import Transport, unique_id
+
+    a, b = unique_id(Transport.PROC), unique_id(Transport.PROC)
+    assert a[:8] == b"FMIPROC\0" and a != b
+    shm = "/dev/shm/fmi_proc_%016x" % int.from_bytes(a[8:16], "little")
+    env = dict(os.environ, FMI_PROC_TIMEOUT_S="20")
+    procs = [subprocess.Popen([sys.executable, "-c", _PROC_JOIN, a.hex(), "3", str(r)], cwd=ROOT, env=env)
+             for r in range(3)]
+    assert [p.wait(timeout=120) for p in procs] == [0, 0, 0]
+    assert not os.path.exists(shm)
+    env["FMI_PROC_TIMEOUT_S"] = "1"
+    lone = subprocess.run([sys.executable, "-c", _PROC_JOIN, b.hex(), "2", "0"], cwd=ROOT, env=env,
+                          capture_output=True, text=True, timeout=120)
+    assert lone.returncode != 0 and "timed out waiting for peers" in lone.stderr
+    assert not os.path.exists("/dev/shm/fmi_proc_%016x" % int.from_bytes(b[8:16], "little"))
+
+
 def test_tuning_knobs_validate():
     fmi_amd.tune_set(fmi_amd.Tune.PAIR_UNROLL, 8)
     assert fmi_amd.tune_get(fmi_amd.Tune.PAIR_UNROLL) == 8
