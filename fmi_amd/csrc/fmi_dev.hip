@@ -51,6 +51,12 @@ int hip_fail(const char* what, hipError_t e) {
         if (fmi_e_ != hipSuccess) return hip_fail(#call, fmi_e_); \
     } while (0)
 
+#define FMI_RC_TRY(call)                  \
+    do {                                  \
+        const int fmi_rc_ = (call);       \
+        if (fmi_rc_ != FMI_OK) return fmi_rc_; \
+    } while (0)
+
 int require_device() {
     if (g_state.device < 0) return fail(FMI_ERR_NO_DEVICE, "fmi_dev_init has not been called");
     int cur = -1;
@@ -157,17 +163,45 @@ int launch_combine(int op, int dtype, void* out, const void* a, const void* b, s
 }
 
 // ----------------------------------------------------------------------------------------------------
-// P-way programs for P > 16 or unaligned buckets: the same schedule, one pairwise pass per step. Temp
-// buckets live in a library-owned arena; slots are assigned on the host (a value's slot is recycled
-// right after its last use) so the arena holds only the peak number of live temps.
+// Scratch arena for P-way temporaries (caller holds g_mu). Stream s waits until the previous user's work
+// has drained; the caller records g_state.arena_free on s after its last launch touching the arena.
+// ----------------------------------------------------------------------------------------------------
+int arena_acquire(size_t need, hipStream_t s) {
+    if (!g_state.arena_free) FMI_HIP_TRY(hipEventCreateWithFlags(&g_state.arena_free, hipEventDisableTiming));
+    if (g_state.arena_bytes < need) {
+        FMI_HIP_TRY(hipEventSynchronize(g_state.arena_free));  // previous users have drained
+        if (g_state.arena) FMI_HIP_TRY(hipFree(g_state.arena));
+        g_state.arena = nullptr;
+        g_state.arena_bytes = 0;
+        const hipError_t e = hipMalloc(&g_state.arena, need);
+        if (e != hipSuccess) return fail(FMI_ERR_ALLOC, std::string("hipMalloc (P-way scratch): ") + hipGetErrorString(e));
+        g_state.arena_bytes = need;
+    }
+    FMI_HIP_TRY(hipStreamWaitEvent(s, g_state.arena_free, 0));
+    return FMI_OK;
+}
+
+size_t arena_stride(size_t n, size_t esz) { return (std::max<size_t>(n * esz, 16) + 255) / 256 * 256; }
+
+// ----------------------------------------------------------------------------------------------------
+// P-way programs for unaligned buckets, the byte/16-bit dtypes and the scans beyond 16 peers: the same
+// schedule, one pairwise pass per step. Only the steps the requested outputs depend on run (an allreduce
+// for one rank needs P - 1 of its P log P steps). Temp buckets live in the arena; slots are assigned on
+// the host (a value's slot is recycled right after its last use) so the arena holds only the peak number
+// of live temps.
 // ----------------------------------------------------------------------------------------------------
 int run_program_stepwise(int op, int dtype, const sched::HostProgram& prog, void* const* outs, int nouts,
                          const int* out_value, const void* const* ins, size_t n, hipStream_t s) {
     const size_t esz = dtype_size(dtype);
     const int P = prog.peers;
     const int nv = prog.nvalues();
+    std::vector<char> live(nv, 0);
+    for (int k = 0; k < nouts; ++k) live[out_value[k]] = 1;
+    for (int st = prog.nsteps - 1; st >= 0; --st)
+        if (live[P + st]) live[prog.step[st].a] = live[prog.step[st].b] = 1;
     std::vector<int> last_use(nv, -1);
     for (int st = 0; st < prog.nsteps; ++st) {
+        if (!live[P + st]) continue;
         last_use[prog.step[st].a] = st;
         last_use[prog.step[st].b] = st;
     }
@@ -176,6 +210,7 @@ int run_program_stepwise(int op, int dtype, const sched::HostProgram& prog, void
     std::vector<int> slot(nv, -1), free_slots;
     int nslots = 0;
     for (int st = 0; st < prog.nsteps; ++st) {
+        if (!live[P + st]) continue;
         int d;
         if (!free_slots.empty()) {
             d = free_slots.back();
@@ -188,26 +223,16 @@ int run_program_stepwise(int op, int dtype, const sched::HostProgram& prog, void
         if (a >= P && last_use[a] == st) free_slots.push_back(slot[a]);
         if (b >= P && b != a && last_use[b] == st) free_slots.push_back(slot[b]);
     }
-    const size_t stride = (std::max<size_t>(n * esz, 16) + 255) / 256 * 256;
-    const size_t need = stride * static_cast<size_t>(nslots);
+    const size_t stride = arena_stride(n, esz);
     std::lock_guard<std::mutex> lk(g_mu);
-    if (!g_state.arena_free) FMI_HIP_TRY(hipEventCreateWithFlags(&g_state.arena_free, hipEventDisableTiming));
-    if (g_state.arena_bytes < need) {
-        FMI_HIP_TRY(hipEventSynchronize(g_state.arena_free));  // previous users have drained
-        if (g_state.arena) FMI_HIP_TRY(hipFree(g_state.arena));
-        g_state.arena = nullptr;
-        g_state.arena_bytes = 0;
-        const hipError_t e = hipMalloc(&g_state.arena, need);
-        if (e != hipSuccess) return fail(FMI_ERR_ALLOC, std::string("hipMalloc (P-way scratch): ") + hipGetErrorString(e));
-        g_state.arena_bytes = need;
-    }
-    FMI_HIP_TRY(hipStreamWaitEvent(s, g_state.arena_free, 0));
+    FMI_RC_TRY(arena_acquire(stride * static_cast<size_t>(nslots), s));
     auto addr = [&](int v) -> const void* {
         return v < P ? ins[v] : static_cast<const char*>(g_state.arena) + stride * static_cast<size_t>(slot[v]);
     };
     int rc = FMI_OK;
     for (int st = 0; st < prog.nsteps && rc == FMI_OK; ++st)
-        rc = launch_combine(op, dtype, const_cast<void*>(addr(P + st)), addr(prog.step[st].a), addr(prog.step[st].b), n, s);
+        if (live[P + st])
+            rc = launch_combine(op, dtype, const_cast<void*>(addr(P + st)), addr(prog.step[st].a), addr(prog.step[st].b), n, s);
     for (int k = 0; k < nouts && rc == FMI_OK; ++k) {
         const void* src = addr(out_value[k]);
         if (src != outs[k] && n > 0) {
@@ -215,6 +240,125 @@ int run_program_stepwise(int op, int dtype, const sched::HostProgram& prog, void
             if (e != hipSuccess) rc = hip_fail("hipMemcpyAsync (P-way result)", e);
         }
     }
+    FMI_HIP_TRY(hipEventRecord(g_state.arena_free, s));
+    return rc;
+}
+
+// ----------------------------------------------------------------------------------------------------
+// Tree algorithms beyond 16 peers as fused 16-peer sub-programs. Each program splits along blocks of 16
+// consecutive (transformed) peers, and every piece is exactly one of the fused kernels' own programs
+// (fmi_schedule.h), so the bracketing is the reference's:
+//   reduce_ltr  ((x0 + .. + x15) + x16 + .. + x30) + ..: a fused 16-peer fold, then fused folds of the
+//               running value and the next 15 peers.
+//   reduce      binomial rounds 0..3 stay inside blocks of 16 (the block's own reduce program); rounds 4..
+//               combine the block values at spans 16, 32, .. = the reduce program over ceil(P/16) values.
+//   allreduce   after the pre-fold of peers >= 2^k into peer - 2^k, recursive-doubling rounds 0..3 stay
+//               inside blocks of 16 and leave position p holding the block's 16-peer allreduce for rank
+//               p % 16; rounds 4.. pair positions with equal p % 16 = the allreduce program over the
+//               2^k / 16 block values, for rank p / 16.
+// Every input is read once; temps cost one write + one read per block value (P = 64: 73 bucket passes
+// instead of 189 for pairwise steps). A dry run (base == nullptr) only counts the temps.
+// ----------------------------------------------------------------------------------------------------
+struct TreeTemps {
+    char* base = nullptr;  // nullptr: dry run
+    size_t stride = 0;
+    int used = 0;
+    void* next() { return base ? base + stride * static_cast<size_t>(used++) : (++used, nullptr); }
+};
+
+int tree_blocked(int op, int dtype, int alg, void* out, const void* const* ins, int P, int rank, size_t n,
+                 hipStream_t s, TreeTemps& t) {
+    const bool dry = t.base == nullptr;
+    constexpr int B16 = sched::kMaxFusedPeers;
+    if (P == 1) {
+        if (!dry && out != ins[0]) FMI_HIP_TRY(hipMemcpyAsync(out, ins[0], n * dtype_size(dtype), hipMemcpyDeviceToDevice, s));
+        return FMI_OK;
+    }
+    if (P <= B16) {
+        if (dry) return FMI_OK;
+        PeerPtrs ptrs{};
+        for (int p = 0; p < P; ++p) ptrs.in[p] = ins[p];
+        ptrs.out[0] = out;
+        switch (alg) {
+            case FMI_ALG_ALLREDUCE: return launch_fused_allreduce(op, dtype, P, ptrs, n, rank, s);
+            case FMI_ALG_REDUCE: return launch_fused_reduce(op, dtype, P, ptrs, n, s);
+            default: return launch_fused_reduce_ltr(op, dtype, P, ptrs, n, s);
+        }
+    }
+    switch (alg) {
+        case FMI_ALG_REDUCE_LTR: {
+            void* acc = t.next();
+            FMI_RC_TRY(tree_blocked(op, dtype, alg, acc, ins, B16, 0, n, s, t));
+            for (int p = B16; p < P; p += B16 - 1) {
+                const int m = std::min(B16 - 1, P - p);
+                if (dry) continue;
+                PeerPtrs ptrs{};
+                ptrs.in[0] = acc;
+                for (int j = 0; j < m; ++j) ptrs.in[1 + j] = ins[p + j];
+                ptrs.out[0] = p + m == P ? out : acc;  // elementwise: reading and writing acc in one pass is safe
+                FMI_RC_TRY(launch_fused_reduce_ltr(op, dtype, 1 + m, ptrs, n, s));
+            }
+            return FMI_OK;
+        }
+        case FMI_ALG_REDUCE: {
+            const int B = (P + B16 - 1) / B16;
+            std::vector<const void*> vals(B);
+            for (int b = 0; b < B; ++b) {
+                const int m = std::min(B16, P - b * B16);
+                if (m == 1) {
+                    vals[b] = ins[b * B16];
+                    continue;
+                }
+                void* v = t.next();
+                FMI_RC_TRY(tree_blocked(op, dtype, alg, v, ins + b * B16, m, 0, n, s, t));
+                vals[b] = v;
+            }
+            return tree_blocked(op, dtype, alg, out, vals.data(), B, 0, n, s, t);
+        }
+        default: {  // allreduce
+            const int pow2 = 1 << sched::floor_log2(P);
+            const int folded = P - pow2;
+            const int r = rank < pow2 ? rank : rank - pow2;  // folded peers get their partner's value back
+            // pre-fold temps are reused block by block (stream order frees them)
+            std::vector<void*> fold(std::min(folded, B16));
+            for (auto& f : fold) f = t.next();
+            auto block_inputs = [&](int lo, int len, std::vector<const void*>& y) -> int {
+                y.assign(ins + lo, ins + lo + len);
+                for (int j = lo; j < std::min(lo + len, folded); ++j) {
+                    void* f = fold[j - lo];
+                    if (!dry) FMI_RC_TRY(launch_combine(op, dtype, f, ins[j], ins[pow2 + j], n, s));
+                    y[j - lo] = f;
+                }
+                return FMI_OK;
+            };
+            std::vector<const void*> y;
+            if (pow2 <= B16) {
+                FMI_RC_TRY(block_inputs(0, pow2, y));
+                return tree_blocked(op, dtype, alg, out, y.data(), pow2, r, n, s, t);
+            }
+            const int B = pow2 / B16;
+            std::vector<const void*> vals(B);
+            for (int b = 0; b < B; ++b) {
+                FMI_RC_TRY(block_inputs(b * B16, B16, y));
+                void* v = t.next();
+                FMI_RC_TRY(tree_blocked(op, dtype, alg, v, y.data(), B16, r % B16, n, s, t));
+                vals[b] = v;
+            }
+            return tree_blocked(op, dtype, alg, out, vals.data(), B, r / B16, n, s, t);
+        }
+    }
+}
+
+int run_tree_blocked(int op, int dtype, int alg, void* out, const void* const* ins, int P, int rank, size_t n,
+                     hipStream_t s) {
+    TreeTemps count;
+    FMI_RC_TRY(tree_blocked(op, dtype, alg, out, ins, P, rank, n, s, count));
+    std::lock_guard<std::mutex> lk(g_mu);
+    TreeTemps t;
+    t.stride = arena_stride(n, dtype_size(dtype));
+    FMI_RC_TRY(arena_acquire(t.stride * static_cast<size_t>(count.used), s));
+    t.base = static_cast<char*>(g_state.arena);
+    const int rc = tree_blocked(op, dtype, alg, out, ins, P, rank, n, s, t);
     FMI_HIP_TRY(hipEventRecord(g_state.arena_free, s));
     return rc;
 }
@@ -492,7 +636,8 @@ int fmi_dev_reduce_tree(int op, int dtype, int alg, void* out, const void* const
     for (int t = 0; t < P; ++t) order[t] = ins[alg == FMI_ALG_REDUCE ? (t + rank) % P : t];
     bool aligned = aligned16(out);
     for (int p = 0; p < P; ++p) aligned = aligned && aligned16(order[p]);
-    if (P >= 2 && P <= sched::kMaxFusedPeers && aligned && is_core_dtype(dtype)) {
+    if (P >= 2 && aligned && is_core_dtype(dtype)) {
+        if (P > sched::kMaxFusedPeers) return run_tree_blocked(op, dtype, alg, out, order.data(), P, rank, n, s);
         PeerPtrs ptrs{};
         for (int p = 0; p < P; ++p) ptrs.in[p] = order[p];
         ptrs.out[0] = out;

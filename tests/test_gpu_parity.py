@@ -160,7 +160,7 @@ def test_synthetic_matches_host_generator(device):
 # ------------------------------------------------------------------------------------------------
 # P-way fused kernels vs the oracle's simulation of the reference collectives
 # ------------------------------------------------------------------------------------------------
-PEERS = list(range(1, 17)) + [17, 20, 33]
+PEERS = list(range(1, 17)) + [17, 20, 24, 31, 32, 33, 48, 64]
 
 
 def _peer_inputs(dtype, n, P, seed=7):
@@ -254,7 +254,7 @@ def test_extra_dtypes_p_way_programs(device, dtype):
     """The other integer widths through every P-way entry point (pairwise passes in the reference's order),
     P covering the fused range and beyond, against the oracle's message simulation."""
     n = 1029
-    for P in (3, 8, 17):
+    for P in (3, 8, 17, 33):
         xs = _peer_inputs(dtype, n, P)
         ins = [dev(x) for x in xs]
         for op in OPS:
@@ -286,15 +286,19 @@ def test_scan_in_place(device):
         assert_bit_equal(bufs[k].numpy(), want[k], f"peer {k}")
 
 
-def test_tree_unaligned_falls_back_with_same_order(device):
-    P, n = 5, 1000
+@pytest.mark.parametrize("P", [5, 40])
+def test_tree_unaligned_falls_back_with_same_order(device, P):
+    """Unaligned views run the pairwise-pass program (only the steps the rank's result depends on)."""
+    n = 1000
     xs = _peer_inputs(np.float32, n + 1, P)
     big = [dev(x) for x in xs]
     ins = [b.view(1, n) for b in big]
-    want, _ = orc.allreduce([x[1:] for x in xs], orc.op_sum)
-    out = Bucket(n, np.float32)
-    fmi_amd.reduce_tree(Op.SUM, Alg.ALLREDUCE, out, ins)
-    assert_bit_equal(out.numpy(), want[0])
+    with np.errstate(all="ignore"):
+        want, _ = orc.allreduce([x[1:] for x in xs], orc.op_max)
+    for rank in (0, P // 2 + 1, P - 1):
+        out = Bucket(n, np.float32)
+        fmi_amd.reduce_tree(Op.MAX, Alg.ALLREDUCE, out, ins, rank=rank)
+        assert_bit_equal(out.numpy(), want[rank], f"rank {rank}")
 
 
 def test_signed_zero_max_follows_each_ranks_operand_order(device):

@@ -54,11 +54,28 @@ def pinned(n, dtype):
     return np.frombuffer(buf, dtype=dtype, count=n), p.value
 
 
+def wide_tree_rows(it):
+    """P > 16 tree reductions (fused 16-peer sub-programs) over 1 GiB of input in total. algo_bytes is the
+    one-pass ideal (P reads + 1 write); `passes` is what the blocked schedule moves, in buckets."""
+    passes = {(Alg.ALLREDUCE, 32): 32 + 2 + 2 + 1, (Alg.ALLREDUCE, 48): 48 + 16 + 2 + 2 + 1 + 16,
+              (Alg.ALLREDUCE, 64): 64 + 4 + 4 + 1, (Alg.REDUCE, 64): 64 + 4 + 4 + 1,
+              (Alg.REDUCE_LTR, 64): 64 + 4 + 4 + 1}
+    for alg, P in passes:
+        n = 1024 * MIB // 4 // P
+        ins = [Bucket(n, np.float32).fill_synthetic(7, p) for p in range(P)]
+        out = Bucket(n, np.float32)
+        med, mn = timed(lambda k: fmi_amd.reduce_tree(Op.SUM, alg, out, ins, rank=P - 1), max(5, it // 2), 1)
+        row(f"tree {alg.name.lower()} f32 P={P} x {n * 4 // MIB}MiB", (P + 1) * n * 4, med, mn,
+            bucket_passes=passes[(alg, P)], one_pass_buckets=P + 1)
+        del ins, out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=30)
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--c5-only", action="store_true", help="only the host-ingress allreduce rows")
+    ap.add_argument("--wide-only", action="store_true", help="only the P > 16 tree rows")
     ap.add_argument("--torch-runtime", action="store_true",
                     help="import torch first, so the library binds to torch's bundled HIP runtime")
     args = ap.parse_args()
@@ -68,6 +85,9 @@ def main():
     it = args.iters
     if args.c5_only:
         host_allreduce_rows()
+        return
+    if args.wide_only:
+        wide_tree_rows(it)
         return
 
     # C2 and its siblings: pairwise combine, every dtype/op, 256 MiB buckets, 4 rotating sets
@@ -117,6 +137,7 @@ def main():
         row(f"tree allreduce f32 P={P2} x {1024 // P2}MiB", (P2 + 1) * n2 * 4, med, mn)
         del ins2, out2
     del ins, outs, out
+    wide_tree_rows(it)
 
     # host-inclusive (C5-shaped, one GPU): pinned and pageable 256 MiB f32 pairs through the device
     n = 256 * MIB // 4
