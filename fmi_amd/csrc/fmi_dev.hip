@@ -363,6 +363,84 @@ int run_tree_blocked(int op, int dtype, int alg, void* out, const void* const* i
     return rc;
 }
 
+// ----------------------------------------------------------------------------------------------------
+// Scans beyond 16 peers. scan_no_order splits along blocks of 16 (kScanCarry's derivation in
+// fmi_schedule.h):
+//   1. each full block's up-sweep total T_b, which is the binomial reduce over the block in reverse order;
+//   2. the block-level prefixes S_b = scan_no_order over the T_b, written straight into the output of
+//      peer 16b + 15 (b >= 1; S_0 = T_0);
+//   3. block 0 as the fused 16-peer scan, every later block as the carry program from S_{b-1}.
+// scan_ltr: block 0 fused, then 15 peers at a time continued from the previous peer's prefix. No input is
+// read more than twice (P = 64: 201 bucket passes, one pass would be 128, pairwise steps about 490).
+// ----------------------------------------------------------------------------------------------------
+int scan_blocked(int op, int dtype, int alg, void* const* outs, const void* const* ins, int P, size_t n,
+                 hipStream_t s, TreeTemps& t) {
+    constexpr int BL = sched::kScanBlock;
+    const bool dry = t.base == nullptr;
+    if (P == 1) {
+        if (!dry && outs[0] != ins[0]) FMI_HIP_TRY(hipMemcpyAsync(outs[0], ins[0], n * dtype_size(dtype), hipMemcpyDeviceToDevice, s));
+        return FMI_OK;
+    }
+    if (P <= sched::kMaxFusedPeers) {
+        if (dry) return FMI_OK;
+        PeerPtrs ptrs{};
+        for (int p = 0; p < P; ++p) {
+            ptrs.in[p] = ins[p];
+            ptrs.out[p] = outs[p];
+        }
+        return alg == FMI_ALG_SCAN ? launch_fused_scan(op, dtype, P, ptrs, n, s) : launch_fused_scan_ltr(op, dtype, P, ptrs, n, s);
+    }
+    auto carry_block = [&](int lo, int m, const void* carry) -> int {
+        if (dry) return FMI_OK;
+        PeerPtrs ptrs{};
+        ptrs.in[0] = carry;
+        for (int j = 0; j < m; ++j) {
+            ptrs.in[1 + j] = ins[lo + j];
+            ptrs.out[1 + j] = outs[lo + j];
+        }
+        return alg == FMI_ALG_SCAN ? launch_fused_scan_carry(op, dtype, m + 1, ptrs, n, s)
+                                   : launch_fused_scan_ltr_carry(op, dtype, m + 1, ptrs, n, s);
+    };
+    if (alg == FMI_ALG_SCAN_LTR) {
+        FMI_RC_TRY(scan_blocked(op, dtype, alg, outs, ins, BL, n, s, t));
+        for (int p = BL; p < P; p += BL - 1) FMI_RC_TRY(carry_block(p, std::min(BL - 1, P - p), outs[p - 1]));
+        return FMI_OK;
+    }
+    const int B = P / BL;  // full blocks; a partial last block takes no part in the block-level rounds
+    if (B >= 2) {
+        std::vector<const void*> totals(B);
+        std::vector<void*> prefix(B);
+        for (int b = 0; b < B; ++b) {
+            void* tb = t.next();
+            totals[b] = tb;
+            prefix[b] = b == 0 ? tb : outs[b * BL + BL - 1];  // S_0 = T_0 stays in its temp
+            if (dry) continue;
+            PeerPtrs r{};
+            for (int j = 0; j < BL; ++j) r.in[j] = ins[b * BL + BL - 1 - j];
+            r.out[0] = tb;
+            FMI_RC_TRY(launch_fused_reduce(op, dtype, BL, r, n, s));
+        }
+        FMI_RC_TRY(scan_blocked(op, dtype, FMI_ALG_SCAN, prefix.data(), totals.data(), B, n, s, t));
+    }
+    FMI_RC_TRY(scan_blocked(op, dtype, alg, outs, ins, BL, n, s, t));  // block 0; its q = 15 output is S_0
+    for (int b = 1; b * BL < P; ++b) FMI_RC_TRY(carry_block(b * BL, std::min(BL - 1, P - b * BL), outs[b * BL - 1]));
+    return FMI_OK;
+}
+
+int run_scan_blocked(int op, int dtype, int alg, void* const* outs, const void* const* ins, int P, size_t n,
+                     hipStream_t s) {
+    TreeTemps count;
+    FMI_RC_TRY(scan_blocked(op, dtype, alg, outs, ins, P, n, s, count));
+    std::lock_guard<std::mutex> lk(g_mu);
+    TreeTemps t;
+    t.stride = arena_stride(n, dtype_size(dtype));
+    FMI_RC_TRY(arena_acquire(t.stride * static_cast<size_t>(count.used), s));
+    t.base = static_cast<char*>(g_state.arena);
+    const int rc = scan_blocked(op, dtype, alg, outs, ins, P, n, s, t);
+    FMI_HIP_TRY(hipEventRecord(g_state.arena_free, s));
+    return rc;
+}
+
 int check_peer_args(int op, int dtype, int P) {
     if (op < FMI_OP_SUM || op > FMI_OP_MIN) return fail(FMI_ERR_INVALID, "unknown op " + std::to_string(op));
     if (dtype_size(dtype) == 0) return fail(FMI_ERR_INVALID, "unknown dtype " + std::to_string(dtype));
@@ -667,7 +745,8 @@ int fmi_dev_scan_peers(int op, int dtype, int alg, void* const* outs, const void
     hipStream_t s = resolve(stream);
     bool aligned = true;
     for (int p = 0; p < P; ++p) aligned = aligned && aligned16(ins[p]) && aligned16(outs[p]);
-    if (P >= 2 && P <= sched::kMaxFusedPeers && aligned && is_core_dtype(dtype)) {
+    if (P >= 2 && aligned && is_core_dtype(dtype)) {
+        if (P > sched::kMaxFusedPeers) return run_scan_blocked(op, dtype, alg, outs, ins, P, n, s);
         PeerPtrs ptrs{};
         for (int p = 0; p < P; ++p) {
             ptrs.in[p] = ins[p];
@@ -779,6 +858,7 @@ int fmi_schedule_expr(int alg, int P, int rank, char* buf, size_t len) {
     if (!buf || len == 0) return fail(FMI_ERR_INVALID, "null buffer");
     if (P < 1 || P > sched::kMaxPeers) return fail(FMI_ERR_INVALID, "P out of range");
     if (rank < 0 || rank >= P) return fail(FMI_ERR_INVALID, "rank out of range");
+    if (alg < FMI_ALG_ALLREDUCE || alg > FMI_ALG_SCAN_LTR) return fail(FMI_ERR_INVALID, "unknown algorithm " + std::to_string(alg));
     const sched::HostProgram prog = sched::build_host(alg, P);
     if (!prog.ok) return fail(FMI_ERR_INVALID, "unknown algorithm " + std::to_string(alg));
     const std::string e = expr_of(prog, prog.out[rank]);

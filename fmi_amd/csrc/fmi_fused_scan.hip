@@ -9,4 +9,10 @@ int launch_fused_scan(int op, int dtype, int P, const PeerPtrs& ptrs, size_t n, 
 int launch_fused_scan_ltr(int op, int dtype, int P, const PeerPtrs& ptrs, size_t n, hipStream_t s) {
     return launch_fused<sched::kScanLtr, false>(op, dtype, P, ptrs, n, 0, s);
 }
+int launch_fused_scan_carry(int op, int dtype, int P, const PeerPtrs& ptrs, size_t n, hipStream_t s) {
+    return launch_fused<sched::kScanCarry, false>(op, dtype, P, ptrs, n, 0, s);
+}
+int launch_fused_scan_ltr_carry(int op, int dtype, int P, const PeerPtrs& ptrs, size_t n, hipStream_t s) {
+    return launch_fused<sched::kScanLtrCarry, false>(op, dtype, P, ptrs, n, 0, s);
+}
 }  // namespace fmi::dev

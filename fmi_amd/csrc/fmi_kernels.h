@@ -330,12 +330,22 @@ __global__ void __launch_bounds__(256) tree_kernel(PeerPtrs ptrs, size_t n, int 
     if (blockIdx.x == 0 && first + threadIdx.x < n) tree_group<Op, T, ALG, P, ALL_RANKS, 1>(ptrs, rank, first + threadIdx.x);
 }
 
+// Carry programs (sched::is_carry_alg) leave output 0 alone: value 0 is the carry itself.
+template <class T, int W, int ALG, int P, size_t... R>
+__device__ __forceinline__ void store_after_carry(const Lanes<T, W>* v, const PeerPtrs& ptrs, size_t elem,
+                                                  std::index_sequence<R...>) {
+    ((store_lanes<kFusedNT, T, W>(static_cast<T*>(ptrs.out[R + 1]) + elem, v[kOut<ALG, P, R + 1>])), ...);
+}
+
 template <class Op, class T, int ALG, int P, int W>
 __device__ __forceinline__ void scan_group(const PeerPtrs& ptrs, size_t elem) {
     Lanes<T, W> v[P + kNumSteps<ALG, P>];
     load_peers<T, W, P>(v, ptrs, elem, std::make_index_sequence<P>{});
     run_steps<Op, T, W, ALG, P>(v, std::make_index_sequence<kNumSteps<ALG, P>>{});
-    store_all<T, W, ALG, P>(v, ptrs, elem, std::make_index_sequence<P>{});
+    if constexpr (sched::is_carry_alg(ALG))
+        store_after_carry<T, W, ALG, P>(v, ptrs, elem, std::make_index_sequence<P - 1>{});
+    else
+        store_all<T, W, ALG, P>(v, ptrs, elem, std::make_index_sequence<P>{});
 }
 
 template <class Op, class T, int ALG, int P>

@@ -28,7 +28,14 @@ enum Alg : int {
     kReduceLtr = 2,  // reference PeerToPeer::reduce_ltr          (src/comm/PeerToPeer.cpp:44-57)
     kScan = 3,       // reference PeerToPeer::scan_no_order       (src/comm/PeerToPeer.cpp:154-184)
     kScanLtr = 4,    // reference PeerToPeer::scan_ltr            (src/comm/PeerToPeer.cpp:141-152)
+    // Internal pieces of the scans beyond kMaxFusedPeers (not in the C-ABI): value 0 is a carry, the
+    // prefix of every peer before this block; values 1..P-1 are the block's peers; out[0] is not stored.
+    kScanCarry = 5,     // one block of 16 consecutive scan_no_order peers, b >= 1, after the block rounds
+    kScanLtrCarry = 6,  // the scan_ltr chain continued from the carry
 };
+
+inline constexpr bool is_carry_alg(int alg) { return alg == kScanCarry || alg == kScanLtrCarry; }
+inline constexpr int kScanBlock = 16;  // kScanCarry's block: P - 1 <= 15 of its 16 peers are inputs
 
 inline constexpr int kMaxFusedPeers = 16;   // fused single-pass kernels are instantiated for P <= 16
 inline constexpr int kFusedStepCap = 80;    // >= max steps for P <= 16 (allreduce P=16: 64)
@@ -145,9 +152,39 @@ constexpr Program<CapSteps, CapPeers> build(int alg, int P) {
             }
             break;
         }
-        case kScanLtr: {
+        case kScanLtr:
+        case kScanLtrCarry: {
             // Linear chain: peer k receives the prefix of k-1 and combines f(prefix, own) (:146-147).
             for (int p = 1; p < P; ++p) cur[p] = prog.emit(cur[p - 1], static_cast<uint16_t>(p));
+            break;
+        }
+        case kScanCarry: {
+            // scan_no_order over P_all > 16 peers, restricted to block b >= 1 (peers 16b .. 16b+15, local
+            // q = peer - 16b, value 1 + q). Up-sweep rounds 0..3 stay inside the block; rounds >= 4 and
+            // down-sweep rounds >= 5 only touch q = 15 (the block totals), which leaves peer 16b - 1 holding
+            // the prefix of blocks < b: the carry, value 0. Down-sweep rounds 4..1 then run inside the block,
+            // except that a receiver whose source lies before the block (q - 2^(i-1) < 0) combines with the
+            // carry (at full size that source is peer 16b - 1 > 0). The block's q = 15 input is never read:
+            // its result is the block-level prefix, computed separately, so P - 1 <= 15 inputs.
+            if (P - 1 > kScanBlock - 1) {
+                prog.ok = false;
+                return prog;
+            }
+            const int m = P - 1;
+            for (int i = 0; i < 4; ++i) {
+                const int full = (1 << (i + 1)) - 1;
+                for (int q = 0; q < m; ++q)
+                    if ((q & full) == full) cur[1 + q] = prog.emit(cur[1 + q], cur[1 + q - (1 << i)]);
+            }
+            for (int i = 4; i > 0; --i) {
+                const int hi = (1 << i) - 1;
+                const int lo = (1 << (i - 1)) - 1;
+                for (int q = 0; q < m; ++q) {
+                    if ((q & hi) == hi || (q & lo) != lo) continue;
+                    const int src = q - (1 << (i - 1));
+                    cur[1 + q] = prog.emit(cur[1 + q], src >= 0 ? cur[1 + src] : cur[0]);
+                }
+            }
             break;
         }
         default:

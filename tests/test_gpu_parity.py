@@ -276,14 +276,18 @@ def test_extra_dtypes_p_way_programs(device, dtype):
                     assert_bit_equal(outs[k].numpy(), want[k], f"{alg.name} P={P} {op.name} peer {k}")
 
 
-def test_scan_in_place(device):
-    P, n = 8, 4096
+@pytest.mark.parametrize("P", [8, 40, 64])
+def test_scan_in_place(device, P):
+    """outs == ins: beyond 16 peers the blocked scan writes block prefixes into outputs whose inputs the
+    later passes must no longer read."""
+    n = 4096
     xs = _peer_inputs(np.float32, n, P)
-    bufs = [dev(x) for x in xs]
-    want, _ = orc.scan(xs, orc.op_sum)
-    fmi_amd.scan_peers(Op.SUM, Alg.SCAN, bufs, bufs)
-    for k in range(P):
-        assert_bit_equal(bufs[k].numpy(), want[k], f"peer {k}")
+    for alg, ordered in ((Alg.SCAN, False), (Alg.SCAN_LTR, True)):
+        bufs = [dev(x) for x in xs]
+        want, _ = orc.scan(xs, orc.op_sum, commutative=not ordered, associative=not ordered)
+        fmi_amd.scan_peers(Op.SUM, alg, bufs, bufs)
+        for k in range(P):
+            assert_bit_equal(bufs[k].numpy(), want[k], f"{alg.name} peer {k}")
 
 
 @pytest.mark.parametrize("P", [5, 40])

@@ -68,6 +68,16 @@ def wide_tree_rows(it):
         row(f"tree {alg.name.lower()} f32 P={P} x {n * 4 // MIB}MiB", (P + 1) * n * 4, med, mn,
             bucket_passes=passes[(alg, P)], one_pass_buckets=P + 1)
         del ins, out
+    # scans: P outputs; one pass would be 2P buckets, the blocked schedule moves `bucket_passes`
+    for alg, P, moved in ((Alg.SCAN, 32, 101), (Alg.SCAN, 64, 201),
+                          (Alg.SCAN_LTR, 64, 64 + 64 + 4)):
+        n = 1024 * MIB // 4 // P
+        ins = [Bucket(n, np.float32).fill_synthetic(7, p) for p in range(P)]
+        outs = [Bucket(n, np.float32) for _ in range(P)]
+        med, mn = timed(lambda k: fmi_amd.scan_peers(Op.SUM, alg, outs, ins), max(5, it // 2), 1)
+        row(f"scan {alg.name.lower()} f32 P={P} x {n * 4 // MIB}MiB", 2 * P * n * 4, med, mn,
+            bucket_passes=moved, one_pass_buckets=2 * P)
+        del ins, outs
 
 
 def main():
