@@ -39,8 +39,8 @@ inline constexpr int kScanBlock = 16;  // kScanCarry's block: P - 1 <= 15 of its
 
 inline constexpr int kMaxFusedPeers = 16;   // fused single-pass kernels are instantiated for P <= 16
 inline constexpr int kFusedStepCap = 80;    // >= max steps for P <= 16 (allreduce P=16: 64)
-inline constexpr int kMaxPeers = 64;        // run-time programs (pairwise passes) up to this P
-inline constexpr int kHostStepCap = 512;    // >= max steps for P <= 64 (allreduce P=64: 384)
+inline constexpr int kMaxPeers = 256;       // P-way programs beyond the fused kernels, up to this P
+inline constexpr int kHostStepCap = 2560;   // >= max steps for P <= 256 (allreduce P=256: 2048)
 
 struct Step {
     uint16_t a;  // left operand (the buffer f.f overwrites)

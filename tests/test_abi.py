@@ -134,7 +134,7 @@ def test_tuning_knobs_validate():
         fmi_amd.tune_set(fmi_amd.Tune.FUSED_INFLIGHT_KIB, -1)
 
 
-@pytest.mark.parametrize("P", list(range(1, 34)) + [48, 64])
+@pytest.mark.parametrize("P", list(range(1, 34)) + [48, 64, 100, 129, 256])
 def test_kernel_schedules_match_oracle(P):
     """The programs the fused kernels execute (fmi_schedule.h, round-synchronous) against the oracle's
     event-driven message simulation of the reference algorithms — for every rank and root."""
@@ -155,6 +155,6 @@ def test_schedule_expr_rejects_bad_args():
     with pytest.raises(fmi_amd.FmiError):
         fmi_amd.schedule_expr(Alg.ALLREDUCE, 0, 0)
     with pytest.raises(fmi_amd.FmiError):
-        fmi_amd.schedule_expr(Alg.ALLREDUCE, 65, 0)
+        fmi_amd.schedule_expr(Alg.ALLREDUCE, 257, 0)
     with pytest.raises(fmi_amd.FmiError):
         fmi_amd.schedule_expr(Alg.ALLREDUCE, 4, 4)

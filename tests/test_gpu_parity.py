@@ -226,6 +226,41 @@ def test_scan_peers(device, P):
                     assert_bit_equal(outs[k].numpy(), want[k], f"P={P} {alg.name} {op.name} peer {k}")
 
 
+@pytest.mark.parametrize("P", [100, 256])
+def test_many_peers_blocked_programs(device, P):
+    """Beyond 64 peers, up to the 256 cap: two levels of 16-peer blocks (P = 256) and ragged blocks
+    (P = 100), every algorithm, aligned (fused blocks) and unaligned (pairwise passes) buckets."""
+    n = 515
+    for dtype, op in ((np.float32, Op.SUM), (np.int64, Op.MAX), (np.float64, Op.MIN)):
+        xs = _peer_inputs(dtype, n + 1, P, seed=23)
+        big = [dev(x) for x in xs]
+        for ins, sl, what in (([b.view(0, n) for b in big], slice(0, n), "aligned"),
+                              ([b.view(1, n) for b in big], slice(1, n + 1), "unaligned")):
+            ys = [x[sl] for x in xs]
+            fn = orc.OPS[OPNAME[op]]
+            with np.errstate(all="ignore"):
+                want, _ = orc.allreduce(ys, fn)
+                for rank in (0, P // 2 + 3, P - 1):
+                    out = Bucket(n, dtype)
+                    fmi_amd.reduce_tree(op, Alg.ALLREDUCE, out, ins, rank=rank)
+                    assert_bit_equal(out.numpy(), want[rank], f"{what} allreduce P={P} rank {rank}")
+                for root in (0, 37):
+                    want, _ = orc.reduce(ys, fn, root=root)
+                    out = Bucket(n, dtype)
+                    fmi_amd.reduce_tree(op, Alg.REDUCE, out, ins, rank=root)
+                    assert_bit_equal(out.numpy(), want, f"{what} reduce P={P} root {root}")
+                want, _ = orc.reduce(ys, fn, root=0, commutative=False, associative=False)
+                out = Bucket(n, dtype)
+                fmi_amd.reduce_tree(op, Alg.REDUCE_LTR, out, ins)
+                assert_bit_equal(out.numpy(), want, f"{what} reduce_ltr P={P}")
+                for alg, ordered in ((Alg.SCAN, False), (Alg.SCAN_LTR, True)):
+                    want, _ = orc.scan(ys, fn, commutative=not ordered, associative=not ordered)
+                    outs = [Bucket(n, dtype) for _ in range(P)]
+                    fmi_amd.scan_peers(op, alg, outs, ins)
+                    for k in range(P):
+                        assert_bit_equal(outs[k].numpy(), want[k], f"{what} {alg.name} P={P} peer {k}")
+
+
 @pytest.mark.parametrize("cap", [0, 4, 32, 96, 256])
 def test_fused_occupancy_cap_keeps_bits(device, cap):
     """FMI_TUNE_FUSED_INFLIGHT_KIB only reserves LDS to cap residency: results stay bit-exact (multi-wave
