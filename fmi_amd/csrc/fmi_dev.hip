@@ -257,18 +257,19 @@ int run_program_stepwise(int op, int dtype, const sched::HostProgram& prog, void
 //               p % 16; rounds 4.. pair positions with equal p % 16 = the allreduce program over the
 //               2^k / 16 block values, for rank p / 16.
 // Every input is read once; temps cost one write + one read per block value (P = 64: 73 bucket passes
-// instead of 189 for pairwise steps). A dry run (base == nullptr) only counts the temps.
+// instead of 189 for pairwise steps). A dry run only counts the temps.
 // ----------------------------------------------------------------------------------------------------
 struct TreeTemps {
-    char* base = nullptr;  // nullptr: dry run
+    bool dry = true;  // dry run: count the temps, launch nothing
+    char* base = nullptr;
     size_t stride = 0;
     int used = 0;
-    void* next() { return base ? base + stride * static_cast<size_t>(used++) : (++used, nullptr); }
+    void* next() { return dry ? (++used, nullptr) : base + stride * static_cast<size_t>(used++); }
 };
 
 int tree_blocked(int op, int dtype, int alg, void* out, const void* const* ins, int P, int rank, size_t n,
                  hipStream_t s, TreeTemps& t) {
-    const bool dry = t.base == nullptr;
+    const bool dry = t.dry;
     constexpr int B16 = sched::kMaxFusedPeers;
     if (P == 1) {
         if (!dry && out != ins[0]) FMI_HIP_TRY(hipMemcpyAsync(out, ins[0], n * dtype_size(dtype), hipMemcpyDeviceToDevice, s));
@@ -355,6 +356,7 @@ int run_tree_blocked(int op, int dtype, int alg, void* out, const void* const* i
     FMI_RC_TRY(tree_blocked(op, dtype, alg, out, ins, P, rank, n, s, count));
     std::lock_guard<std::mutex> lk(g_mu);
     TreeTemps t;
+    t.dry = false;
     t.stride = arena_stride(n, dtype_size(dtype));
     FMI_RC_TRY(arena_acquire(t.stride * static_cast<size_t>(count.used), s));
     t.base = static_cast<char*>(g_state.arena);
@@ -366,17 +368,18 @@ int run_tree_blocked(int op, int dtype, int alg, void* out, const void* const* i
 // ----------------------------------------------------------------------------------------------------
 // Scans beyond 16 peers. scan_no_order splits along blocks of 16 (kScanCarry's derivation in
 // fmi_schedule.h):
-//   1. each full block's up-sweep total T_b, which is the binomial reduce over the block in reverse order;
+//   1. block 0 as the fused 16-peer scan (its last output is T_0), and every later full block's up-sweep
+//      total T_b, which is the binomial reduce over the block in reverse order;
 //   2. the block-level prefixes S_b = scan_no_order over the T_b, written straight into the output of
-//      peer 16b + 15 (b >= 1; S_0 = T_0);
-//   3. block 0 as the fused 16-peer scan, every later block as the carry program from S_{b-1}.
+//      peer 16b + 15 (S_0 = T_0);
+//   3. every later block as the carry program from S_{b-1}.
 // scan_ltr: block 0 fused, then 15 peers at a time continued from the previous peer's prefix. No input is
-// read more than twice (P = 64: 201 bucket passes, one pass would be 128, pairwise steps about 490).
+// read more than twice (P = 64: 184 bucket passes, one pass would be 128, pairwise steps about 490).
 // ----------------------------------------------------------------------------------------------------
 int scan_blocked(int op, int dtype, int alg, void* const* outs, const void* const* ins, int P, size_t n,
                  hipStream_t s, TreeTemps& t) {
     constexpr int BL = sched::kScanBlock;
-    const bool dry = t.base == nullptr;
+    const bool dry = t.dry;
     if (P == 1) {
         if (!dry && outs[0] != ins[0]) FMI_HIP_TRY(hipMemcpyAsync(outs[0], ins[0], n * dtype_size(dtype), hipMemcpyDeviceToDevice, s));
         return FMI_OK;
@@ -406,14 +409,18 @@ int scan_blocked(int op, int dtype, int alg, void* const* outs, const void* cons
         for (int p = BL; p < P; p += BL - 1) FMI_RC_TRY(carry_block(p, std::min(BL - 1, P - p), outs[p - 1]));
         return FMI_OK;
     }
+    // Block 0 first: the fused 16-peer scan, whose q = 15 output is T_0 = S_0. It reads its inputs before
+    // the block-level scan writes any output (outs may alias ins).
+    FMI_RC_TRY(scan_blocked(op, dtype, alg, outs, ins, BL, n, s, t));
     const int B = P / BL;  // full blocks; a partial last block takes no part in the block-level rounds
     if (B >= 2) {
         std::vector<const void*> totals(B);
         std::vector<void*> prefix(B);
-        for (int b = 0; b < B; ++b) {
+        totals[0] = prefix[0] = outs[BL - 1];  // rewritten in place with the same bits
+        for (int b = 1; b < B; ++b) {
             void* tb = t.next();
             totals[b] = tb;
-            prefix[b] = b == 0 ? tb : outs[b * BL + BL - 1];  // S_0 = T_0 stays in its temp
+            prefix[b] = outs[b * BL + BL - 1];
             if (dry) continue;
             PeerPtrs r{};
             for (int j = 0; j < BL; ++j) r.in[j] = ins[b * BL + BL - 1 - j];
@@ -422,7 +429,6 @@ int scan_blocked(int op, int dtype, int alg, void* const* outs, const void* cons
         }
         FMI_RC_TRY(scan_blocked(op, dtype, FMI_ALG_SCAN, prefix.data(), totals.data(), B, n, s, t));
     }
-    FMI_RC_TRY(scan_blocked(op, dtype, alg, outs, ins, BL, n, s, t));  // block 0; its q = 15 output is S_0
     for (int b = 1; b * BL < P; ++b) FMI_RC_TRY(carry_block(b * BL, std::min(BL - 1, P - b * BL), outs[b * BL - 1]));
     return FMI_OK;
 }
@@ -433,6 +439,7 @@ int run_scan_blocked(int op, int dtype, int alg, void* const* outs, const void* 
     FMI_RC_TRY(scan_blocked(op, dtype, alg, outs, ins, P, n, s, count));
     std::lock_guard<std::mutex> lk(g_mu);
     TreeTemps t;
+    t.dry = false;
     t.stride = arena_stride(n, dtype_size(dtype));
     FMI_RC_TRY(arena_acquire(t.stride * static_cast<size_t>(count.used), s));
     t.base = static_cast<char*>(g_state.arena);

@@ -6,6 +6,8 @@ and signed zeros included). Sizes: ragged small cases the oracle finishes instan
 the reference's element semantics cover, and BASELINE.json's full configs C2 (256 MiB f32 pairwise sum)
 and C3 (64 MiB i64 max, 8 × 64 MiB f32 peer scan).
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -259,6 +261,34 @@ def test_many_peers_blocked_programs(device, P):
                     fmi_amd.scan_peers(op, alg, outs, ins)
                     for k in range(P):
                         assert_bit_equal(outs[k].numpy(), want[k], f"{what} {alg.name} P={P} peer {k}")
+
+
+_FIRST_CALL = """
+import numpy as np, fmi_amd
+from fmi_amd import Alg, Bucket, Op
+from oracle import fmi_oracle as orc
+from tests.test_gpu_parity import assert_bit_equal, inputs
+fmi_amd.init(0)
+P, n = 17, 1031
+xs = [inputs(np.float32, n, p, seed=7) for p in range(P)]
+ins = [Bucket.from_numpy(x) for x in xs]
+outs = [Bucket(n, np.float32) for _ in range(P)]
+fmi_amd.scan_peers(Op.SUM, Alg.SCAN, outs, ins)   # needs no scratch at all
+want, _ = orc.scan(xs, orc.op_sum)
+for k in range(P):
+    assert_bit_equal(outs[k].numpy(), want[k], f"peer {k}")
+print("ok")
+"""
+
+
+def test_blocked_program_as_first_call_of_a_process(device):
+    """A blocked program that needs no temporaries, before anything has sized the scratch arena."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", _FIRST_CALL], cwd=root, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-2000:]
 
 
 @pytest.mark.parametrize("cap", [0, 4, 32, 96, 256])

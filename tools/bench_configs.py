@@ -69,7 +69,7 @@ def wide_tree_rows(it):
             bucket_passes=passes[(alg, P)], one_pass_buckets=P + 1)
         del ins, out
     # scans: P outputs; one pass would be 2P buckets, the blocked schedule moves `bucket_passes`
-    for alg, P, moved in ((Alg.SCAN, 32, 101), (Alg.SCAN, 64, 201),
+    for alg, P, moved in ((Alg.SCAN, 32, 84), (Alg.SCAN, 64, 184),
                           (Alg.SCAN_LTR, 64, 64 + 64 + 4)):
         n = 1024 * MIB // 4 // P
         ins = [Bucket(n, np.float32).fill_synthetic(7, p) for p in range(P)]
