@@ -118,6 +118,30 @@ def test_comm_scan(device, N):
                 assert_bit_equal(res[r], want[r], f"N={N} {op.name} ordered={ordered} rank {r}")
 
 
+def test_comm_more_ranks_than_a_fused_kernel_holds(device):
+    """N = 20 ranks: every rank's shard reduction is a 20-peer program, run as fused 16-peer blocks
+    (allreduce, reduce, scan) — bit-exact with the reference's 20-peer bracketing."""
+    N, n = 20, 4099
+    xs = [inputs(np.float32, n, r, seed=29) for r in range(N)]
+
+    def body(c, r):
+        s, out, red, sc = Bucket.from_numpy(xs[r]), Bucket(n, np.float32), Bucket(n, np.float32), Bucket(n, np.float32)
+        c.allreduce(Op.SUM, s, out)
+        c.reduce(Op.SUM, s, red if r == 3 else None, 3)
+        c.scan(Op.SUM, s, sc)
+        fmi_amd.sync()
+        return out.numpy(), red.numpy() if r == 3 else None, sc.numpy()
+
+    res = run_ranks(N, body)
+    want_ar, _ = orc.allreduce(xs, orc.op_sum)
+    want_red, _ = orc.reduce(xs, orc.op_sum, root=3)
+    want_sc, _ = orc.scan(xs, orc.op_sum)
+    for r in range(N):
+        assert_bit_equal(res[r][0], want_ar[0], f"allreduce rank {r}")
+        assert_bit_equal(res[r][2], want_sc[r], f"scan rank {r}")
+    assert_bit_equal(res[3][1], want_red, "reduce root 3")
+
+
 def _host_allreduce(c, r, x, op, ordered, pinned, chunk):
     n, dtype = x.size, x.dtype
     if pinned:
