@@ -55,6 +55,11 @@ def run(c, N, r):
         fmi_amd.sync()
         out["direct_" + np.dtype(dtype).name] = o.numpy()
         c.window_free(w)
+    # host buckets through the GPU (config C5's shape), pageable, several chunks
+    x = inputs(np.float64, 3 * 4099 + 17, r, seed=36)
+    got = np.zeros_like(x)
+    c.allreduce_host(Op.SUM, x.copy(), got, chunk=4099)
+    out["host_f64"] = got
     # data movement, bcast and point-to-point larger than a slot
     b = Bucket.from_numpy(np.full(BIG, r, dtype=np.int32))
     c.bcast(b, N - 1)

@@ -56,6 +56,9 @@ def test_proc_transport_collectives(device, N, tmp_path):
             want, _ = orc.scan([inputs(dtype, 65536 + 129, r, seed=34) for r in range(N)], orc.OPS[op])
             for r in range(N):
                 assert_bit_equal(res[r]["scan_" + np.dtype(dtype).name], want[r], f"scan {op} rank {r}")
+        want, _ = orc.allreduce([inputs(np.float64, 3 * 4099 + 17, r, seed=36) for r in range(N)], orc.op_sum)
+        for r in range(N):
+            assert_bit_equal(res[r]["host_f64"], want[0], f"host allreduce rank {r}")
         for dtype, op, n in ((np.float32, "sum", 3 * 65536 + 5), (np.int32, "min", 1027)):
             want, _ = orc.allreduce([inputs(dtype, n, r, seed=35) for r in range(N)], orc.OPS[op])
             for r in range(N):
