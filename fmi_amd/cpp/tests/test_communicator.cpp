@@ -4,6 +4,8 @@
 // reference does), plus order, error and device tests. Run by tests/test_cpp_communicator.py.
 //
 //   test_communicator [--gpu] [name-filter]      run the suite (device tests only with --gpu)
+//   test_communicator --proc-channel P           device collectives over the Rccl channel with the PROC
+//        transport, P fork()ed peers on GPU 0, against the same collectives on host buckets
 //   test_communicator --dump KIND P N OUT [--device|--offload]
 //        run KIND (allreduce|reduce|scan|reduce_ltr|allreduce_ltr|scan_ltr) over P peers holding
 //        synthetic f32 buckets of N elements (seed 42, peer p) and write every peer's recvbuf, then every
@@ -988,8 +990,72 @@ static int dump(const std::string& kind, peer_num P, std::size_t n, const std::s
     return g_failures.load() ? 1 : 0;
 }
 
+// --proc-channel P: P peers as fork()ed processes (forked before anything touches the GPU), each with a
+// LocalSocket channel and an Rccl channel over the PROC transport (every process on GPU 0). Device-bucket
+// allreduce / scan / reduce / bcast through the Rccl channel must equal, bit for bit, the same collectives
+// on host buckets through the socket channel. Exit status 0 = every peer agreed.
+static int proc_channel(peer_num P) {
+    const std::size_t n = 300007;
+    FMI::Comm::SocketMesh mesh(P);
+    std::vector<pid_t> kids;
+    for (peer_num p = 0; p < P; ++p) {
+        const pid_t pid = fork();
+        if (pid != 0) {
+            kids.push_back(pid);
+            continue;
+        }
+        int bad = 0;
+        try {
+            Communicator c(p, P, "", "proc-test");
+            auto sock = std::make_shared<FMI::Comm::LocalSocket>(mesh.claim(p), 60000);
+            c.register_channel("Local", sock);
+            std::vector<float> host_ar, host_sc, host_red;
+            {
+                Data<std::vector<float>> a(synth_f32(n, 5, p)), r(n);
+                c.allreduce(a, r, Function<std::vector<float>>(Op::sum));
+                host_ar = r.get();
+                Data<std::vector<float>> sc(synth_f32(n, 5, p)), sr(n);
+                c.scan(sc, sr, Function<std::vector<float>>(Op::sum));
+                host_sc = sr.get();
+                Data<std::vector<float>> d(synth_f32(n, 5, p)), dr(n);
+                c.reduce(d, dr, 1 % P, Function<std::vector<float>>(Op::sum));
+                host_red = dr.get();
+            }
+            Dev::init(0);
+            c.register_channel("Rccl", FMI::Comm::Rccl::connect(*sock, p, P, FMI_TRANSPORT_PROC));
+            Data<Dev::Bucket<float>> a(synth_f32(n, 5, p)), r(n);
+            c.allreduce(a, r, Function<Dev::Bucket<float>>(Op::sum));
+            bad += std::memcmp(r.get().data(), host_ar.data(), n * 4) != 0;
+            Data<Dev::Bucket<float>> sc(synth_f32(n, 5, p)), sr(n);
+            c.scan(sc, sr, Function<Dev::Bucket<float>>(Op::sum));
+            bad += std::memcmp(sr.get().data(), host_sc.data(), n * 4) != 0;
+            Data<Dev::Bucket<float>> d(synth_f32(n, 5, p)), dr(n);
+            c.reduce(d, dr, 1 % P, Function<Dev::Bucket<float>>(Op::sum));
+            if (p == 1 % P) bad += std::memcmp(dr.get().data(), host_red.data(), n * 4) != 0;
+            Data<Dev::Bucket<int64_t>> b(std::vector<int64_t>{static_cast<int64_t>(p), 9});
+            c.bcast(b, P - 1);
+            bad += b.get()[0] != static_cast<int64_t>(P - 1);
+            c.barrier();
+        } catch (const std::exception& e) {
+            std::fprintf(stderr, "peer %u threw: %s\n", p, e.what());
+            _exit(3);
+        }
+        if (bad) std::fprintf(stderr, "peer %u: %d mismatching results\n", p, bad);
+        _exit(bad ? 1 : 0);
+    }
+    int rc = 0;
+    for (pid_t k : kids) {
+        int status = 0;
+        waitpid(k, &status, 0);
+        if (!WIFEXITED(status) || WEXITSTATUS(status) != 0) rc = 1;
+    }
+    std::fprintf(stderr, "proc_channel P=%u: %s\n", P, rc ? "FAIL" : "OK");
+    return rc;
+}
+
 int main(int argc, char** argv) {
     std::vector<std::string> args(argv + 1, argv + argc);
+    if (args.size() == 2 && args[0] == "--proc-channel") return proc_channel(static_cast<peer_num>(std::stoul(args[1])));
     if (!args.empty() && args[0] == "--dump") {
         if (args.size() < 5) return 2;
         const std::string mode = args.size() > 5 ? args[5].substr(2) : "host";

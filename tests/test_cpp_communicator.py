@@ -80,6 +80,15 @@ def test_cpp_suite_gpu(exe):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("P", [2, 3, 4])
+def test_cpp_rccl_channel_across_processes(exe, P):
+    """FMI::Comm::Rccl over the PROC transport: P fork()ed peers on one GPU, device-bucket collectives
+    bit-identical to the host-bucket collectives over the socket channel."""
+    out = subprocess.run([exe, "--proc-channel", str(P)], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-4000:]
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("mode", ["device", "offload"])
 @pytest.mark.parametrize("kind", ["allreduce", "reduce", "scan", "allreduce_ltr", "scan_ltr"])
 def test_cpp_device_path_matches_oracle(exe, mode, kind):
