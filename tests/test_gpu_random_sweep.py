@@ -30,6 +30,7 @@ def _cases(seed):
 
 @pytest.mark.parametrize("seed", [1, 2])
 def test_random_p_way_cases(device, seed):
+    done = 0
     for k, P, alg, op, dtype, n, off, rank in _cases(seed):
         xs = [inputs(dtype, n + off, p, seed=1000 * seed + k) for p in range(P)]
         big = [Bucket.from_numpy(x) for x in xs]
@@ -45,6 +46,7 @@ def test_random_p_way_cases(device, seed):
                 fmi_amd.scan_peers(op, alg, outs, ins)
                 for p in range(P):
                     assert_bit_equal(outs[p].numpy(), want[p], f"{what} peer {p}")
+                done += 1
                 continue
             out = Bucket(n, dtype)
             fmi_amd.reduce_tree(op, alg, out, ins, rank=rank)
@@ -56,3 +58,6 @@ def test_random_p_way_cases(device, seed):
             else:
                 want, _ = orc.reduce(ys, fn, root=0, commutative=False, associative=False)
             assert_bit_equal(out.numpy(), want, what)
+            done += 1
+    print(f"seed {seed}: {done} cases bit-exact")
+    assert done == CASES
