@@ -865,8 +865,12 @@ int padded_source(Comm* c, size_t n, size_t padded, size_t esz, const void* send
 // recv[i] = (reduced-shard area of the rank owning element i)[i], for the byte range [0, nbytes): 16-B
 // nontemporal accesses over xGMI when every pointer is 16-B aligned, bytes otherwise. Shards are whole
 // multiples of 256 B, so a 16-B group never straddles two owners.
+struct WindowPtrs {  // every rank's reduced-shard area (kernel argument: 2 KiB at the 256-rank cap)
+    const void* in[sched::kMaxPeers];
+};
+
 template <bool VEC>
-__global__ void __launch_bounds__(256) gather_shards(PeerPtrs src, char* dst, size_t nbytes, size_t shard_bytes) {
+__global__ void __launch_bounds__(256) gather_shards(WindowPtrs src, char* dst, size_t nbytes, size_t shard_bytes) {
     const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
     const size_t first = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     if constexpr (VEC) {
@@ -897,8 +901,8 @@ int allreduce_direct(Comm* c, const Window& w, size_t off, int op, int dtype, in
     const int N = c->t->n();
     const int k = c->t->rank();
     const size_t esz = dtype_size(dtype);
-    if (N > sched::kMaxFusedPeers)
-        return fail(FMI_ERR_UNSUPPORTED, "path DIRECT supports up to " + std::to_string(sched::kMaxFusedPeers) + " ranks");
+    if (N > sched::kMaxPeers)
+        return fail(FMI_ERR_UNSUPPORTED, "path DIRECT supports up to " + std::to_string(sched::kMaxPeers) + " ranks");
     const size_t shard = shard_elems(n, N);
     FMI_COMM_RC(c->t->barrier_async(s));
     const size_t lo = std::min(n, static_cast<size_t>(k) * shard);
@@ -910,7 +914,7 @@ int allreduce_direct(Comm* c, const Window& w, size_t off, int op, int dtype, in
         FMI_COMM_RC(fmi_dev_reduce_tree(op, dtype, alg, out, ins.data(), N, 0, len, s));
     }
     FMI_COMM_RC(c->t->barrier_async(s));
-    PeerPtrs src{};
+    WindowPtrs src{};
     bool vec = aligned16(recv);
     for (int j = 0; j < N; ++j) {
         src.in[j] = w.peers[j] + w.bytes + off;
@@ -1011,6 +1015,8 @@ int fmi_comm_unique_id(int transport, void* id, size_t len) {
 int fmi_comm_init(fmi_comm_t* comm, const void* id, int nranks, int rank) {
     if (!comm || !id) return fail(FMI_ERR_INVALID, "null argument");
     if (nranks < 1 || rank < 0 || rank >= nranks) return fail(FMI_ERR_INVALID, "rank out of range");
+    if (nranks > fmi::sched::kMaxPeers)  // every shard program is one P = nranks program
+        return fail(FMI_ERR_INVALID, "at most " + std::to_string(fmi::sched::kMaxPeers) + " ranks per communicator");
     auto c = std::make_unique<Comm>();
     if (std::memcmp(id, kLocalMagic, 8) == 0) {
         uint64_t key;

@@ -189,7 +189,7 @@ typedef enum { FMI_TRANSPORT_RCCL = 0, FMI_TRANSPORT_LOCAL = 1, FMI_TRANSPORT_PR
 /* FMI_PATH_DIRECT: no RCCL data movement. `send` must lie in a window (fmi_comm_window_alloc, same offset on
  * every rank); rank k's fused kernel reads shard k of every rank's window over xGMI (IPC-mapped peer
  * memory) and reduces it in the reference's order, then every rank reads the N reduced shards from the
- * peers' windows. Bit-identical to FMI_PATH_TREE; up to 16 ranks. */
+ * peers' windows. Bit-identical to FMI_PATH_TREE; up to 256 ranks. */
 typedef enum { FMI_PATH_TREE = 0, FMI_PATH_RCCL = 1, FMI_PATH_DIRECT = 2 } fmi_path_t;
 
 /* A fresh communicator id (FMI_COMM_ID_BYTES) made by one rank and handed to the others by any host

@@ -83,6 +83,8 @@ def test_comm_host_side_without_device():
         Comm(a, 3, 0)  # joining a 2-rank communicator as a 3-rank one
     with pytest.raises(fmi_amd.FmiError):
         Comm(a, 2, 2)  # rank out of range
+    with pytest.raises(fmi_amd.FmiError):
+        Comm(unique_id(Transport.LOCAL), 257, 0)  # beyond the 256-peer program cap
     c0.destroy()
     c1.destroy()
 

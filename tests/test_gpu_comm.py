@@ -120,7 +120,8 @@ def test_comm_scan(device, N):
 
 def test_comm_more_ranks_than_a_fused_kernel_holds(device):
     """N = 20 ranks: every rank's shard reduction is a 20-peer program, run as fused 16-peer blocks
-    (allreduce, reduce, scan) — bit-exact with the reference's 20-peer bracketing."""
+    (allreduce on the TREE and DIRECT paths, reduce, scan) — bit-exact with the reference's 20-peer
+    bracketing."""
     N, n = 20, 4099
     xs = [inputs(np.float32, n, r, seed=29) for r in range(N)]
 
@@ -129,8 +130,13 @@ def test_comm_more_ranks_than_a_fused_kernel_holds(device):
         c.allreduce(Op.SUM, s, out)
         c.reduce(Op.SUM, s, red if r == 3 else None, 3)
         c.scan(Op.SUM, s, sc)
+        w, direct = c.window(n, np.float32), Bucket(n, np.float32)
+        w.upload(xs[r])
+        c.allreduce(Op.SUM, w, direct, path=Path.DIRECT)
         fmi_amd.sync()
-        return out.numpy(), red.numpy() if r == 3 else None, sc.numpy()
+        got = out.numpy(), red.numpy() if r == 3 else None, sc.numpy(), direct.numpy()
+        c.window_free(w)
+        return got
 
     res = run_ranks(N, body)
     want_ar, _ = orc.allreduce(xs, orc.op_sum)
@@ -139,6 +145,7 @@ def test_comm_more_ranks_than_a_fused_kernel_holds(device):
     for r in range(N):
         assert_bit_equal(res[r][0], want_ar[0], f"allreduce rank {r}")
         assert_bit_equal(res[r][2], want_sc[r], f"scan rank {r}")
+        assert_bit_equal(res[r][3], want_ar[0], f"allreduce DIRECT rank {r}")
     assert_bit_equal(res[3][1], want_red, "reduce root 3")
 
 

@@ -35,8 +35,6 @@ def _cases(seed):
 def test_random_comm_cases(device, seed):
     done = 0
     for k, N, kind, ordered, op, dtype, n, root in _cases(seed):
-        if kind == "allreduce_direct" and N > 16:
-            kind = "allreduce"
         xs = [inputs(dtype, n, r, seed=500 * seed + k) for r in range(N)]
 
         def body(c, r):
