@@ -275,7 +275,7 @@ int tree_blocked(int op, int dtype, int alg, void* out, const void* const* ins, 
         if (!dry && out != ins[0]) FMI_HIP_TRY(hipMemcpyAsync(out, ins[0], n * dtype_size(dtype), hipMemcpyDeviceToDevice, s));
         return FMI_OK;
     }
-    if (P <= B16) {
+    if (P <= sched::max_fused_peers(alg)) {
         if (dry) return FMI_OK;
         PeerPtrs ptrs{};
         for (int p = 0; p < P; ++p) ptrs.in[p] = ins[p];
@@ -316,33 +316,31 @@ int tree_blocked(int op, int dtype, int alg, void* out, const void* const* ins, 
             }
             return tree_blocked(op, dtype, alg, out, vals.data(), B, 0, n, s, t);
         }
-        default: {  // allreduce
+        default: {  // allreduce, P > 31
             const int pow2 = 1 << sched::floor_log2(P);
             const int folded = P - pow2;
             const int r = rank < pow2 ? rank : rank - pow2;  // folded peers get their partner's value back
-            // pre-fold temps are reused block by block (stream order frees them)
-            std::vector<void*> fold(std::min(folded, B16));
-            for (auto& f : fold) f = t.next();
-            auto block_inputs = [&](int lo, int len, std::vector<const void*>& y) -> int {
-                y.assign(ins + lo, ins + lo + len);
-                for (int j = lo; j < std::min(lo + len, folded); ++j) {
-                    void* f = fold[j - lo];
-                    if (!dry) FMI_RC_TRY(launch_combine(op, dtype, f, ins[j], ins[pow2 + j], n, s));
-                    y[j - lo] = f;
-                }
-                return FMI_OK;
-            };
-            std::vector<const void*> y;
-            if (pow2 <= B16) {
-                FMI_RC_TRY(block_inputs(0, pow2, y));
-                return tree_blocked(op, dtype, alg, out, y.data(), pow2, r, n, s, t);
-            }
             const int B = pow2 / B16;
+            // A block of m < 16 pre-folded peers is the fused allreduce program of 16 + m peers (it pre-folds
+            // them itself). A block whose 16 peers all take a pre-fold would need 32 inputs: its pairs go
+            // through temps, reused block by block (stream order frees them).
+            std::vector<void*> fold(folded >= B16 ? B16 : 0);
+            for (auto& f : fold) f = t.next();
             std::vector<const void*> vals(B);
             for (int b = 0; b < B; ++b) {
-                FMI_RC_TRY(block_inputs(b * B16, B16, y));
+                const int lo = b * B16;
+                const int m = std::clamp(folded - lo, 0, B16);
+                std::vector<const void*> y(ins + lo, ins + lo + B16);
+                if (m == B16) {
+                    for (int j = 0; j < B16; ++j) {
+                        if (!dry) FMI_RC_TRY(launch_combine(op, dtype, fold[j], ins[lo + j], ins[pow2 + lo + j], n, s));
+                        y[j] = fold[j];
+                    }
+                } else {
+                    y.insert(y.end(), ins + pow2 + lo, ins + pow2 + lo + m);
+                }
                 void* v = t.next();
-                FMI_RC_TRY(tree_blocked(op, dtype, alg, v, y.data(), B16, r % B16, n, s, t));
+                FMI_RC_TRY(tree_blocked(op, dtype, alg, v, y.data(), static_cast<int>(y.size()), r % B16, n, s, t));
                 vals[b] = v;
             }
             return tree_blocked(op, dtype, alg, out, vals.data(), B, r / B16, n, s, t);
@@ -722,7 +720,7 @@ int fmi_dev_reduce_tree(int op, int dtype, int alg, void* out, const void* const
     bool aligned = aligned16(out);
     for (int p = 0; p < P; ++p) aligned = aligned && aligned16(order[p]);
     if (P >= 2 && aligned && is_core_dtype(dtype)) {
-        if (P > sched::kMaxFusedPeers) return run_tree_blocked(op, dtype, alg, out, order.data(), P, rank, n, s);
+        if (P > sched::max_fused_peers(alg)) return run_tree_blocked(op, dtype, alg, out, order.data(), P, rank, n, s);
         PeerPtrs ptrs{};
         for (int p = 0; p < P; ++p) ptrs.in[p] = order[p];
         ptrs.out[0] = out;

@@ -82,6 +82,8 @@ inline bool is_float(int dtype) { return dtype == FMI_F32 || dtype == FMI_F64; }
 // algorithm family, each defined in its own translation unit so the ~1.2k instantiations build in
 // parallel. Return 0 or a negative fmi_status_t.
 int launch_fused_allreduce(int op, int dtype, int P, const PeerPtrs& ptrs, size_t n, int rank, hipStream_t s);
+// allreduce for P = 17..31 (the pre-folded programs), reached through launch_fused_allreduce
+int launch_fused_allreduce_wide(int op, int dtype, int P, const PeerPtrs& ptrs, size_t n, int rank, hipStream_t s);
 int launch_fused_reduce(int op, int dtype, int P, const PeerPtrs& ptrs, size_t n, hipStream_t s);
 int launch_fused_reduce_ltr(int op, int dtype, int P, const PeerPtrs& ptrs, size_t n, hipStream_t s);
 int launch_fused_scan(int op, int dtype, int P, const PeerPtrs& ptrs, size_t n, hipStream_t s);

@@ -131,8 +131,9 @@ __device__ __forceinline__ void store_lanes(T* p, const Lanes<T, W>& x) {
 }
 
 // 8-bit lanes, four bytes per 32-bit word: sum by SWAR (the carry out of each byte is dropped, exactly
-// the wrap of the per-byte add), max / min on packed 16-bit halves (even bytes and odd bytes, widened with
-// their sign or zero), one or two instructions per 2-4 bytes instead of several per byte.
+// the wrap of the per-byte add), prod / max / min on packed 16-bit halves (even bytes and odd bytes; the
+// low byte of a 16-bit product is the wrapped byte product, signed or not), one or two instructions per
+// 2-4 bytes instead of several per byte.
 using u16x2 = unsigned short __attribute__((ext_vector_type(2)));
 using i16x2 = short __attribute__((ext_vector_type(2)));
 
@@ -140,6 +141,12 @@ template <class Op, class T>
 __device__ __forceinline__ uint32_t combine_bytes(uint32_t a, uint32_t b) {
     if constexpr (std::is_same_v<Op, OpSum>) {
         return ((a & 0x7F7F7F7Fu) + (b & 0x7F7F7F7Fu)) ^ ((a ^ b) & 0x80808080u);
+    } else if constexpr (std::is_same_v<Op, OpProd>) {
+        const u16x2 ae = __builtin_bit_cast(u16x2, a & 0x00FF00FFu), be = __builtin_bit_cast(u16x2, b & 0x00FF00FFu);
+        const u16x2 ao = __builtin_bit_cast(u16x2, (a >> 8) & 0x00FF00FFu), bo = __builtin_bit_cast(u16x2, (b >> 8) & 0x00FF00FFu);
+        const uint32_t e = __builtin_bit_cast(uint32_t, static_cast<u16x2>(ae * be)) & 0x00FF00FFu;
+        const uint32_t o = __builtin_bit_cast(uint32_t, static_cast<u16x2>(ao * bo)) & 0x00FF00FFu;
+        return e | (o << 8);
     } else {
         using V = std::conditional_t<std::is_signed_v<T>, i16x2, u16x2>;
         const V a16 = __builtin_bit_cast(V, a), b16 = __builtin_bit_cast(V, b);
@@ -159,7 +166,7 @@ __device__ __forceinline__ uint32_t combine_bytes(uint32_t a, uint32_t b) {
 
 template <class Op, class T, int W>
 __device__ __forceinline__ Lanes<T, W> combine(const Lanes<T, W>& a, const Lanes<T, W>& b) {
-    if constexpr (sizeof(T) == 1 && W % 4 == 0 && !std::is_same_v<Op, OpProd>) {
+    if constexpr (sizeof(T) == 1 && W % 4 == 0) {
         struct Words {
             uint32_t w[W / 4];
         };
@@ -261,7 +268,7 @@ __global__ void __launch_bounds__(256) pair_scalar(T* out, const T* a, const T* 
 inline constexpr bool kFusedNT = true;
 
 struct PeerPtrs {
-    const void* in[sched::kMaxFusedPeers];
+    const void* in[sched::kFusedInputCap];
     void* out[sched::kMaxFusedPeers];
 };
 
@@ -287,10 +294,31 @@ __device__ __forceinline__ void load_peers(Lanes<T, W>* v, const PeerPtrs& ptrs,
     ((v[I] = load_lanes<kFusedNT, T, W>(static_cast<const T*>(ptrs.in[I]) + elem)), ...);
 }
 
+// The value as an opaque register operand. A select chain over loads from one array (pick_rank below) is
+// otherwise folded by LLVM into a single load at a rank-dependent index, which pins the whole value array
+// in scratch memory (it did, for every rank-aware instantiation, up to 1.3 KiB per thread at P = 16).
+template <class T, int W>
+__device__ __forceinline__ Lanes<T, W> opaque(Lanes<T, W> x) {
+    if constexpr (sizeof(x) == 16) {
+        u32x4 b = __builtin_bit_cast(u32x4, x);
+        asm("" : "+v"(b));
+        return __builtin_bit_cast(Lanes<T, W>, b);
+    } else if constexpr (sizeof(x) == 8) {
+        uint64_t b = __builtin_bit_cast(uint64_t, x);
+        asm("" : "+v"(b));
+        return __builtin_bit_cast(Lanes<T, W>, b);
+    } else {
+        static_assert(sizeof(x) == 4, "lane group of 4, 8 or 16 bytes");
+        uint32_t b = __builtin_bit_cast(uint32_t, x);
+        asm("" : "+v"(b));
+        return __builtin_bit_cast(Lanes<T, W>, b);
+    }
+}
+
 template <class T, int W, int ALG, int P, size_t... R>
 __device__ __forceinline__ Lanes<T, W> pick_rank(const Lanes<T, W>* v, int rank, std::index_sequence<R...>) {
     Lanes<T, W> r = v[kOut<ALG, P, 0>];
-    ((r = (rank == static_cast<int>(R)) ? v[kOut<ALG, P, R>] : r), ...);
+    ((r = (rank == static_cast<int>(R)) ? opaque(v[kOut<ALG, P, R>]) : r), ...);
     return r;
 }
 

@@ -38,7 +38,13 @@ inline constexpr bool is_carry_alg(int alg) { return alg == kScanCarry || alg ==
 inline constexpr int kScanBlock = 16;  // kScanCarry's block: P - 1 <= 15 of its 16 peers are inputs
 
 inline constexpr int kMaxFusedPeers = 16;   // fused single-pass kernels are instantiated for P <= 16
-inline constexpr int kFusedStepCap = 80;    // >= max steps for P <= 16 (allreduce P=16: 64)
+// ... and allreduce_no_order up to 31: the pre-fold of peers 16.. into 0.. then the 16-peer recursive
+// doubling, in one pass (also the block program of larger non-power-of-two P, fmi_dev.hip tree_blocked)
+inline constexpr int kMaxFusedAllreducePeers = 31;
+inline constexpr int kFusedInputCap = 32;
+inline constexpr int kFusedStepCap = 80;    // >= max steps of a fused program (allreduce P=31: 79)
+
+constexpr int max_fused_peers(int alg) { return alg == 0 /*kAllreduce*/ ? kMaxFusedAllreducePeers : kMaxFusedPeers; }
 inline constexpr int kMaxPeers = 256;       // P-way programs beyond the fused kernels, up to this P
 inline constexpr int kHostStepCap = 2560;   // >= max steps for P <= 256 (allreduce P=256: 2048)
 
@@ -197,7 +203,7 @@ constexpr Program<CapSteps, CapPeers> build(int alg, int P) {
 
 template <int Alg_, int P>
 struct Fused {
-    static constexpr Program<kFusedStepCap, kMaxFusedPeers> prog = build<kFusedStepCap, kMaxFusedPeers>(Alg_, P);
+    static constexpr Program<kFusedStepCap, kFusedInputCap> prog = build<kFusedStepCap, kFusedInputCap>(Alg_, P);
     static_assert(prog.ok, "fused schedule exceeds capacity");
 };
 

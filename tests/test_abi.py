@@ -160,3 +160,32 @@ def test_schedule_expr_rejects_bad_args():
         fmi_amd.schedule_expr(Alg.ALLREDUCE, 257, 0)
     with pytest.raises(fmi_amd.FmiError):
         fmi_amd.schedule_expr(Alg.ALLREDUCE, 4, 4)
+
+
+def test_no_kernel_spills_to_scratch(tmp_path):
+    """Every gfx950 kernel in libfmi_dev.so keeps its values in registers: .private_segment_fixed_size is 0
+    for all of them (fused programs index their value arrays with constants only; a select chain over
+    that array, or a per-byte loop, once put it in scratch)."""
+    import subprocess
+
+    llvm = "/opt/rocm/lib/llvm/bin"
+    if not os.path.exists(os.path.join(llvm, "clang-offload-bundler")):
+        pytest.skip("ROCm LLVM tools not installed")
+    fat = tmp_path / "fatbin"
+    subprocess.run([os.path.join(llvm, "llvm-objcopy"), f"--dump-section=.hip_fatbin={fat}", _lib.LIB_PATH,
+                    str(tmp_path / "lib.so")], check=True)
+    data = fat.read_bytes()
+    magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    starts = [m.start() for m in re.finditer(re.escape(magic), data)] + [len(data)]
+    kernels = spilled = 0
+    for k in range(len(starts) - 1):
+        b, elf = tmp_path / f"b{k}", tmp_path / f"b{k}.elf"
+        b.write_bytes(data[starts[k]:starts[k + 1]])
+        subprocess.run([os.path.join(llvm, "clang-offload-bundler"), "--unbundle", "--type=o", f"--input={b}",
+                        f"--output={elf}", "--targets=hipv4-amdgcn-amd-amdhsa--gfx950"], check=True)
+        notes = subprocess.run([os.path.join(llvm, "llvm-readelf"), "--notes", str(elf)], check=True,
+                               capture_output=True, text=True).stdout
+        sizes = re.findall(r"private_segment_fixed_size:\s+(\d+)", notes)
+        kernels += len(sizes)
+        spilled += sum(1 for v in sizes if v != "0")
+    assert kernels > 2000 and spilled == 0, f"{spilled} of {kernels} kernels use scratch"

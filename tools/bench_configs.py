@@ -57,7 +57,8 @@ def pinned(n, dtype):
 def wide_tree_rows(it):
     """P > 16 tree reductions (fused 16-peer sub-programs) over 1 GiB of input in total. algo_bytes is the
     one-pass ideal (P reads + 1 write); `passes` is what the blocked schedule moves, in buckets."""
-    passes = {(Alg.ALLREDUCE, 32): 32 + 2 + 2 + 1, (Alg.ALLREDUCE, 48): 48 + 16 + 2 + 2 + 1 + 16,
+    passes = {(Alg.ALLREDUCE, 24): 25, (Alg.ALLREDUCE, 40): 24 + 1 + 16 + 1 + 2 + 1,
+              (Alg.ALLREDUCE, 32): 32 + 2 + 2 + 1, (Alg.ALLREDUCE, 48): 48 + 16 + 2 + 2 + 1 + 16,
               (Alg.ALLREDUCE, 64): 64 + 4 + 4 + 1, (Alg.REDUCE, 64): 64 + 4 + 4 + 1,
               (Alg.REDUCE_LTR, 64): 64 + 4 + 4 + 1}
     for alg, P in passes:
@@ -67,6 +68,14 @@ def wide_tree_rows(it):
         med, mn = timed(lambda k: fmi_amd.reduce_tree(Op.SUM, alg, out, ins, rank=P - 1), max(5, it // 2), 1)
         row(f"tree {alg.name.lower()} f32 P={P} x {n * 4 // MIB}MiB", (P + 1) * n * 4, med, mn,
             bucket_passes=passes[(alg, P)], one_pass_buckets=P + 1)
+        del ins, out
+    # rank-aware allreduce kernels (float max/min: operand order differs per rank) against the plain ones
+    for P, op in ((16, Op.SUM), (16, Op.MAX), (24, Op.MAX)):
+        n = 1024 * MIB // 4 // P
+        ins = [Bucket(n, np.float32).fill_synthetic(7, p) for p in range(P)]
+        out = Bucket(n, np.float32)
+        med, mn = timed(lambda k: fmi_amd.reduce_tree(op, Alg.ALLREDUCE, out, ins, rank=5), max(5, it // 2), 1)
+        row(f"tree allreduce {op.name.lower()} f32 P={P} x {n * 4 // MIB}MiB rank 5", (P + 1) * n * 4, med, mn)
         del ins, out
     # scans: P outputs; one pass would be 2P buckets, the blocked schedule moves `bucket_passes`
     for alg, P, moved in ((Alg.SCAN, 32, 84), (Alg.SCAN, 64, 184),
