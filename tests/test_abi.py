@@ -153,6 +153,16 @@ def test_kernel_schedules_match_oracle(P):
             break  # larger P: one rank is enough, the oracle simulation is O(P^2 log P) per call
 
 
+def test_allreduce_power_of_two_is_xor_symmetric():
+    """For P = 2^k the value peer r holds is rank 0's expression over inputs x[p ^ r], operand order
+    included: what lets fmi_fused_allreduce.hip run the rank-0 kernel over permuted pointers."""
+    for P in (2, 4, 8, 16, 32, 64, 128, 256):
+        e0 = fmi_amd.schedule_expr(Alg.ALLREDUCE, P, 0)
+        for r in range(P):
+            want = re.sub(r"x(\d+)", lambda m: "x%d" % (int(m.group(1)) ^ r), e0)
+            assert fmi_amd.schedule_expr(Alg.ALLREDUCE, P, r) == want, (P, r)
+
+
 def test_schedule_expr_rejects_bad_args():
     with pytest.raises(fmi_amd.FmiError):
         fmi_amd.schedule_expr(Alg.ALLREDUCE, 0, 0)
