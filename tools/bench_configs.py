@@ -54,6 +54,23 @@ def pinned(n, dtype):
     return np.frombuffer(buf, dtype=dtype, count=n), p.value
 
 
+def op_sweep_rows(it):
+    """Every op x core dtype through the P = 8 fused programs (allreduce for rank 3, scan), 32 MiB buckets:
+    a slow cell points at a kernel that stopped streaming (scratch, an expensive combine)."""
+    P = 8
+    for dt in (np.float32, np.float64, np.int32, np.int64):
+        n = 32 * MIB // np.dtype(dt).itemsize
+        ins = [Bucket(n, dt).fill_synthetic(7, p) for p in range(P)]
+        out = Bucket(n, dt)
+        outs = [Bucket(n, dt) for _ in range(P)]
+        for op in (Op.SUM, Op.PROD, Op.MAX, Op.MIN):
+            med, mn = timed(lambda k: fmi_amd.reduce_tree(op, Alg.ALLREDUCE, out, ins, rank=3), it, 1)
+            row(f"allreduce {op.name.lower()} {np.dtype(dt).name} P=8 x 32MiB rank 3", (P + 1) * 32 * MIB, med, mn)
+            med, mn = timed(lambda k: fmi_amd.scan_peers(op, Alg.SCAN, outs, ins), it, 1)
+            row(f"scan {op.name.lower()} {np.dtype(dt).name} P=8 x 32MiB", 2 * P * 32 * MIB, med, mn)
+        del ins, out, outs
+
+
 def wide_tree_rows(it):
     """P > 16 tree reductions (fused 16-peer sub-programs) over 1 GiB of input in total. algo_bytes is the
     one-pass ideal (P reads + 1 write); `passes` is what the blocked schedule moves, in buckets."""
@@ -95,6 +112,7 @@ def main():
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--c5-only", action="store_true", help="only the host-ingress allreduce rows")
     ap.add_argument("--wide-only", action="store_true", help="only the P > 16 tree rows")
+    ap.add_argument("--op-sweep", action="store_true", help="only the op x dtype sweep of the P = 8 programs")
     ap.add_argument("--torch-runtime", action="store_true",
                     help="import torch first, so the library binds to torch's bundled HIP runtime")
     args = ap.parse_args()
@@ -107,6 +125,9 @@ def main():
         return
     if args.wide_only:
         wide_tree_rows(it)
+        return
+    if args.op_sweep:
+        op_sweep_rows(it)
         return
 
     # C2 and its siblings: pairwise combine, every dtype/op, 256 MiB buckets, 4 rotating sets
