@@ -138,6 +138,18 @@ class ShardedAllreduce:
             staging = self._buf("staging", padded, x)
             dist.all_to_all_single(staging, src, group=self.group)
             parts = [staging[j * shard:(j + 1) * shard] for j in range(N)]
+            if op in (Op.MAX, Op.MIN) and x.dtype in (torch.float32, torch.float64):
+                # float max / min keep the first operand on ±0 ties and NaNs, so each GPU's peer 2g ends
+                # with its own bits: the shard owner computes the shard in every rank's order and an
+                # all-to-all (instead of the all-gather) delivers rank r's versions (same volume)
+                pers = self._buf("per_rank", padded, x)
+                for r in range(N):
+                    self.engine.reduce_tree(op, Alg.ALLREDUCE, pers[r * shard:(r + 1) * shard], parts, rank=r)
+                gathered = out if padded == n else self._buf("pad_out", padded, x)
+                dist.all_to_all_single(gathered, pers, group=self.group)
+                if gathered is not out:
+                    out.copy_(gathered[:n])
+                return out
             self.engine.reduce_tree(op, Alg.ALLREDUCE, red, parts, rank=0)
         else:
             dist.reduce_scatter_tensor(red, src, op=_REDUCE_OP[op], group=self.group)

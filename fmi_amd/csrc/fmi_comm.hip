@@ -939,24 +939,48 @@ int allreduce_device(Comm* c, int op, int dtype, int alg, int path, const void* 
         if (send != recv) FMI_COMM_HIP(hipMemcpyAsync(recv, send, n * esz, hipMemcpyDeviceToDevice, s));
         return FMI_OK;
     }
+    // Float max / min: every peer of the reference allreduce keeps its own operand order, so on ±0 ties
+    // and NaNs the peers' results differ. Each shard owner then computes the shard in every rank's order
+    // and an all-to-all (instead of the all-gather) hands rank r the versions in its order. Same exchange
+    // volume; the owner's kernel writes N versions of its shard. Path DIRECT takes this exchange too.
+    const bool per_rank = path != FMI_PATH_RCCL && alg == FMI_ALG_ALLREDUCE && order_sensitive(op, dtype);
     if (path == FMI_PATH_DIRECT) {
         size_t off = 0;
         const Window* w = c->window_of(send, n * esz, &off);
         if (!w) return fail(FMI_ERR_INVALID, "path DIRECT: send must lie inside a window from fmi_comm_window_alloc");
-        return allreduce_direct(c, *w, off, op, dtype, alg, recv, n, s);
+        if (!per_rank) return allreduce_direct(c, *w, off, op, dtype, alg, recv, n, s);
     }
     const size_t shard = shard_elems(n, N);
     const size_t padded = shard * N;
     const char* src = nullptr;
     FMI_COMM_RC(padded_source(c, n, padded, esz, send, s, &src));
     char* red = nullptr;
-    FMI_COMM_RC(c->scratch(2, shard * esz, s, &red));
-    if (path == FMI_PATH_TREE) {
+    FMI_COMM_RC(c->scratch(2, (per_rank ? padded : shard) * esz, s, &red));
+    if (path != FMI_PATH_RCCL) {
         char* staging = nullptr;
         FMI_COMM_RC(c->scratch(1, padded * esz, s, &staging));
         FMI_COMM_RC(c->t->all_to_all(src, staging, shard * esz, s));
         std::vector<const void*> parts(N);
         for (int j = 0; j < N; ++j) parts[j] = staging + j * shard * esz;
+        if (per_rank) {
+            if (N <= sched::kMaxFusedPeers) {
+                PeerPtrs ptrs{};
+                for (int j = 0; j < N; ++j) {
+                    ptrs.in[j] = parts[j];
+                    ptrs.out[j] = red + j * shard * esz;
+                }
+                FMI_COMM_RC(launch_fused_allreduce_all_ranks(op, dtype, N, ptrs, shard, s));
+            } else {
+                for (int r = 0; r < N; ++r)
+                    FMI_COMM_RC(fmi_dev_reduce_tree(op, dtype, alg, red + r * shard * esz, parts.data(), N, r, shard, s));
+            }
+            if (padded == n) return c->t->all_to_all(red, static_cast<char*>(recv), shard * esz, s);
+            char* out = nullptr;
+            FMI_COMM_RC(c->scratch(3, padded * esz, s, &out));
+            FMI_COMM_RC(c->t->all_to_all(red, out, shard * esz, s));
+            FMI_COMM_HIP(hipMemcpyAsync(recv, out, n * esz, hipMemcpyDeviceToDevice, s));
+            return FMI_OK;
+        }
         FMI_COMM_RC(fmi_dev_reduce_tree(op, dtype, alg, red, parts.data(), N, 0, shard, s));
     } else {
         FMI_COMM_RC(c->t->reduce_scatter(op, dtype, src, red, shard, s));

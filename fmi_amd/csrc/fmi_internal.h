@@ -82,6 +82,11 @@ inline bool is_float(int dtype) { return dtype == FMI_F32 || dtype == FMI_F64; }
 // algorithm family, each defined in its own translation unit so the ~1.2k instantiations build in
 // parallel. Return 0 or a negative fmi_status_t.
 int launch_fused_allreduce(int op, int dtype, int P, const PeerPtrs& ptrs, size_t n, int rank, hipStream_t s);
+// allreduce_no_order's value for every peer at once (outs[r] for r < P), float max / min only
+int launch_fused_allreduce_all_ranks(int op, int dtype, int P, const PeerPtrs& ptrs, size_t n, hipStream_t s);
+// float max / min: which operand is kept on a tie (±0) or a NaN depends on the order, so every peer of an
+// allreduce can end with different bits
+inline bool order_sensitive(int op, int dtype) { return is_float(dtype) && (op == FMI_OP_MAX || op == FMI_OP_MIN); }
 // allreduce for P = 17..31 (the pre-folded programs), reached through launch_fused_allreduce
 int launch_fused_allreduce_wide(int op, int dtype, int P, const PeerPtrs& ptrs, size_t n, int rank, hipStream_t s);
 int launch_fused_reduce(int op, int dtype, int P, const PeerPtrs& ptrs, size_t n, hipStream_t s);

@@ -64,6 +64,16 @@ class HostEngine:
         t.numpy()[...] = orc.synthetic(t.numpy().dtype, t.numel(), seed, peer)
 
 
+def with_edges(x, peer):
+    """Signed zeros and NaNs on shared indices (every 5th element: +0 on peers 0, 3 mod 4 and -0 on the
+    others; every 13th: NaN on peer 0 only): float max / min then depend on each peer's operand order."""
+    x = x.copy()
+    x[::5] = 0.0 if peer % 4 in (0, 3) else -0.0
+    if peer == 0:
+        x[3::13] = np.nan
+    return x
+
+
 def run(rank, world, port, n, dtype, op, path, peers_per_gpu, outdir):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -72,8 +82,13 @@ def run(rank, world, port, n, dtype, op, path, peers_per_gpu, outdir):
         ar = collectives.ShardedAllreduce(path=path, engine=HostEngine())
         from oracle import fmi_oracle as orc
 
-        buckets = [torch.from_numpy(orc.synthetic(np.dtype(dtype), n, 42, peers_per_gpu * rank + j))
-                   for j in range(peers_per_gpu)]
+        edges = dtype.endswith(":edges")
+        dt = np.dtype(dtype.split(":")[0])
+        buckets = []
+        for j in range(peers_per_gpu):
+            p = peers_per_gpu * rank + j
+            x = orc.synthetic(dt, n, 42, p)
+            buckets.append(torch.from_numpy(with_edges(x, p) if edges else x))
         out = torch.empty(n, dtype=buckets[0].dtype)
         ar.allreduce(Op(op), buckets, out)
         np.save(os.path.join(outdir, f"out{rank}.npy"), out.numpy())

@@ -36,7 +36,10 @@ def _run(world, n, dtype, op, path, peers_per_gpu=2):
                  join=True)
         outs = [np.load(os.path.join(d, f"out{r}.npy")) for r in range(world)]
         sends = [np.load(os.path.join(d, f"send{r}.npy")) for r in range(world)]
-    xs = [orc.synthetic(np.dtype(dtype), n, 42, p) for p in range(peers_per_gpu * world)]
+    dt = np.dtype(dtype.split(":")[0])
+    xs = [orc.synthetic(dt, n, 42, p) for p in range(peers_per_gpu * world)]
+    if dtype.endswith(":edges"):
+        xs = [_dist_worker.with_edges(x, p) for p, x in enumerate(xs)]
     return outs, sends, xs
 
 
@@ -64,6 +67,19 @@ def test_tree_path_other_ops_int64(op):
         want, _ = orc.allreduce(xs, orc.OPS[OPS[op]])
     for r in range(2):
         assert np.array_equal(outs[r], want[2 * r])
+
+
+@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("op", [2, 3])
+def test_tree_path_float_max_min_each_rank_keeps_its_operand_order(world, op):
+    """Float max / min on ±0 ties and NaNs: the reference's peers end with different bits. Every GPU must
+    hold its own peer's (2g) bits, not rank 0's: per-rank shard versions delivered by an all-to-all."""
+    n = 4099
+    outs, _, xs = _run(world, n, "float32:edges", op, "tree")
+    want, _ = orc.allreduce(xs, orc.OPS[OPS[op]])
+    assert any(not _bits_equal(want[0], want[2 * r]) for r in range(1, world)), "data must tell the ranks apart"
+    for r in range(world):
+        assert _bits_equal(outs[r], want[2 * r]), f"rank {r}"
 
 
 def test_rccl_path_within_tolerance():

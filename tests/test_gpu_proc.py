@@ -43,7 +43,7 @@ def test_proc_transport_collectives(device, N, tmp_path):
         for name, dtype, op, n in ALLREDUCE_CASES:
             want, _ = orc.allreduce([inputs(dtype, n, r, seed=31) for r in range(N)], orc.OPS[OPNAME[op]])
             for r in range(N):
-                assert_bit_equal(res[r]["allreduce_" + name], want[0], f"allreduce {name} rank {r}")
+                assert_bit_equal(res[r]["allreduce_" + name], want[r], f"allreduce {name} rank {r}")
         want, _ = orc.allreduce([inputs(np.float32, 4099, r, seed=32) for r in range(N)], orc.op_sum,
                                 commutative=False, associative=False)
         for r in range(N):
@@ -58,11 +58,11 @@ def test_proc_transport_collectives(device, N, tmp_path):
                 assert_bit_equal(res[r]["scan_" + np.dtype(dtype).name], want[r], f"scan {op} rank {r}")
         want, _ = orc.allreduce([inputs(np.float64, 3 * 4099 + 17, r, seed=36) for r in range(N)], orc.op_sum)
         for r in range(N):
-            assert_bit_equal(res[r]["host_f64"], want[0], f"host allreduce rank {r}")
+            assert_bit_equal(res[r]["host_f64"], want[r], f"host allreduce rank {r}")
         for dtype, op, n in ((np.float32, "sum", 3 * 65536 + 5), (np.int32, "min", 1027)):
             want, _ = orc.allreduce([inputs(dtype, n, r, seed=35) for r in range(N)], orc.OPS[op])
             for r in range(N):
-                assert_bit_equal(res[r]["direct_" + np.dtype(dtype).name], want[0], f"direct {op} rank {r}")
+                assert_bit_equal(res[r]["direct_" + np.dtype(dtype).name], want[r], f"direct {op} rank {r}")
     assert np.array_equal(res[0]["gather"], np.concatenate([np.arange(1000) + 1000 * j for j in range(N)]))
     for r in range(N):
         assert res[r]["bcast_ok"][0] and res[r]["ring_ok"][0], f"rank {r}"
