@@ -32,8 +32,9 @@ namespace FMI::Comm {
 class Rccl : public Channel {
 public:
     //! Join a communicator: peer 0 creates the id, `bootstrap` (any host channel of the same peers)
-    //! broadcasts it, every peer initialises its rank. transport: FMI_TRANSPORT_RCCL (one process per GPU)
-    //! or FMI_TRANSPORT_LOCAL (peers are threads of one process sharing one GPU).
+    //! broadcasts it, every peer initialises its rank. transport: FMI_TRANSPORT_RCCL (one process per GPU),
+    //! FMI_TRANSPORT_PROC (peers are processes of one node, e.g. several sharing one GPU) or
+    //! FMI_TRANSPORT_LOCAL (peers are threads of one process sharing one GPU).
     static std::shared_ptr<Rccl> connect(Channel& bootstrap, Utils::peer_num peer, Utils::peer_num num_peers,
                                          int transport = FMI_TRANSPORT_RCCL, double link_gb_s = 300.) {
         std::array<char, FMI_COMM_ID_BYTES> id{};
