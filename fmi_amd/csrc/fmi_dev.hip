@@ -322,25 +322,24 @@ int tree_blocked(int op, int dtype, int alg, void* out, const void* const* ins, 
             const int r = rank < pow2 ? rank : rank - pow2;  // folded peers get their partner's value back
             const int B = pow2 / B16;
             // A block of m < 16 pre-folded peers is the fused allreduce program of 16 + m peers (it pre-folds
-            // them itself). A block whose 16 peers all take a pre-fold would need 32 inputs: its pairs go
-            // through temps, reused block by block (stream order frees them).
-            std::vector<void*> fold(folded >= B16 ? B16 : 0);
-            for (auto& f : fold) f = t.next();
+            // them itself); a block whose 16 peers all take a pre-fold is the 32-input kAllreducePrefold16.
             std::vector<const void*> vals(B);
             for (int b = 0; b < B; ++b) {
                 const int lo = b * B16;
                 const int m = std::clamp(folded - lo, 0, B16);
                 std::vector<const void*> y(ins + lo, ins + lo + B16);
+                y.insert(y.end(), ins + pow2 + lo, ins + pow2 + lo + m);
+                void* v = t.next();
                 if (m == B16) {
-                    for (int j = 0; j < B16; ++j) {
-                        if (!dry) FMI_RC_TRY(launch_combine(op, dtype, fold[j], ins[lo + j], ins[pow2 + lo + j], n, s));
-                        y[j] = fold[j];
+                    if (!dry) {
+                        PeerPtrs ptrs{};
+                        for (int j = 0; j < 2 * B16; ++j) ptrs.in[j] = y[j];
+                        ptrs.out[0] = v;
+                        FMI_RC_TRY(launch_fused_allreduce_prefold16(op, dtype, ptrs, n, r % B16, s));
                     }
                 } else {
-                    y.insert(y.end(), ins + pow2 + lo, ins + pow2 + lo + m);
+                    FMI_RC_TRY(tree_blocked(op, dtype, alg, v, y.data(), static_cast<int>(y.size()), r % B16, n, s, t));
                 }
-                void* v = t.next();
-                FMI_RC_TRY(tree_blocked(op, dtype, alg, v, y.data(), static_cast<int>(y.size()), r % B16, n, s, t));
                 vals[b] = v;
             }
             return tree_blocked(op, dtype, alg, out, vals.data(), B, r / B16, n, s, t);

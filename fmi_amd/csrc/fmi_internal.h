@@ -82,6 +82,9 @@ inline bool is_float(int dtype) { return dtype == FMI_F32 || dtype == FMI_F64; }
 // algorithm family, each defined in its own translation unit so the ~1.2k instantiations build in
 // parallel. Return 0 or a negative fmi_status_t.
 int launch_fused_allreduce(int op, int dtype, int P, const PeerPtrs& ptrs, size_t n, int rank, hipStream_t s);
+// a 16-peer allreduce block whose peers all pre-fold a partner: ins[0..16) the block, ins[16..32) the
+// partners; out[0] = the value of block peer `rank` (< 16)
+int launch_fused_allreduce_prefold16(int op, int dtype, const PeerPtrs& ptrs, size_t n, int rank, hipStream_t s);
 // allreduce_no_order's value for every peer at once (outs[r] for r < P), float max / min only
 int launch_fused_allreduce_all_ranks(int op, int dtype, int P, const PeerPtrs& ptrs, size_t n, hipStream_t s);
 // float max / min: which operand is kept on a tie (±0) or a NaN depends on the order, so every peer of an

@@ -32,6 +32,9 @@ enum Alg : int {
     // prefix of every peer before this block; values 1..P-1 are the block's peers; out[0] is not stored.
     kScanCarry = 5,     // one block of 16 consecutive scan_no_order peers, b >= 1, after the block rounds
     kScanLtrCarry = 6,  // the scan_ltr chain continued from the carry
+    // One 16-peer block of allreduce_no_order (P_all > 32) whose 16 peers all take a pre-fold: 32 inputs,
+    // values 16 + j are the partners peer j folds in first; then the 16-peer recursive doubling.
+    kAllreducePrefold16 = 7,
 };
 
 inline constexpr bool is_carry_alg(int alg) { return alg == kScanCarry || alg == kScanLtrCarry; }
@@ -44,7 +47,9 @@ inline constexpr int kMaxFusedAllreducePeers = 31;
 inline constexpr int kFusedInputCap = 32;
 inline constexpr int kFusedStepCap = 80;    // >= max steps of a fused program (allreduce P=31: 79)
 
-constexpr int max_fused_peers(int alg) { return alg == 0 /*kAllreduce*/ ? kMaxFusedAllreducePeers : kMaxFusedPeers; }
+constexpr int max_fused_peers(int alg) {
+    return alg == 0 /*kAllreduce*/ ? kMaxFusedAllreducePeers : alg == 7 /*kAllreducePrefold16*/ ? 32 : kMaxFusedPeers;
+}
 inline constexpr int kMaxPeers = 256;       // P-way programs beyond the fused kernels, up to this P
 inline constexpr int kHostStepCap = 2560;   // >= max steps for P <= 256 (allreduce P=256: 2048)
 
@@ -162,6 +167,22 @@ constexpr Program<CapSteps, CapPeers> build(int alg, int P) {
         case kScanLtrCarry: {
             // Linear chain: peer k receives the prefix of k-1 and combines f(prefix, own) (:146-147).
             for (int p = 1; p < P; ++p) cur[p] = prog.emit(cur[p - 1], static_cast<uint16_t>(p));
+            break;
+        }
+        case kAllreducePrefold16: {
+            // allreduce_no_order's pre-fold (:100-107) for 16 peers at once, then its recursive doubling
+            // (:108-121) over them: the program of a block whose peers all have a partner >= 2^k.
+            if (P != 32) {
+                prog.ok = false;
+                return prog;
+            }
+            for (int j = 0; j < 16; ++j) cur[j] = prog.emit(cur[j], cur[16 + j]);
+            for (int i = 0; i < 4; ++i) {
+                uint16_t prev[CapPeers] = {};
+                for (int p = 0; p < 16; ++p) prev[p] = cur[p];
+                for (int p = 0; p < 16; ++p) cur[p] = prog.emit(prev[p], prev[p ^ (1 << i)]);
+            }
+            for (int p = 16; p < 32; ++p) cur[p] = cur[p - 16];
             break;
         }
         case kScanCarry: {

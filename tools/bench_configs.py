@@ -75,7 +75,7 @@ def wide_tree_rows(it):
     """P > 16 tree reductions (fused 16-peer sub-programs) over 1 GiB of input in total. algo_bytes is the
     one-pass ideal (P reads + 1 write); `passes` is what the blocked schedule moves, in buckets."""
     passes = {(Alg.ALLREDUCE, 24): 25, (Alg.ALLREDUCE, 40): 24 + 1 + 16 + 1 + 2 + 1,
-              (Alg.ALLREDUCE, 32): 32 + 2 + 2 + 1, (Alg.ALLREDUCE, 48): 48 + 16 + 2 + 2 + 1 + 16,
+              (Alg.ALLREDUCE, 32): 32 + 2 + 2 + 1, (Alg.ALLREDUCE, 48): 32 + 1 + 16 + 1 + 2 + 1,
               (Alg.ALLREDUCE, 64): 64 + 4 + 4 + 1, (Alg.REDUCE, 64): 64 + 4 + 4 + 1,
               (Alg.REDUCE_LTR, 64): 64 + 4 + 4 + 1}
     for alg, P in passes:
