@@ -381,7 +381,7 @@ int scan_blocked(int op, int dtype, int alg, void* const* outs, const void* cons
         if (!dry && outs[0] != ins[0]) FMI_HIP_TRY(hipMemcpyAsync(outs[0], ins[0], n * dtype_size(dtype), hipMemcpyDeviceToDevice, s));
         return FMI_OK;
     }
-    if (P <= sched::kMaxFusedPeers) {
+    if (P <= sched::max_fused_peers(alg)) {
         if (dry) return FMI_OK;
         PeerPtrs ptrs{};
         for (int p = 0; p < P; ++p) {
@@ -750,7 +750,7 @@ int fmi_dev_scan_peers(int op, int dtype, int alg, void* const* outs, const void
     bool aligned = true;
     for (int p = 0; p < P; ++p) aligned = aligned && aligned16(ins[p]) && aligned16(outs[p]);
     if (P >= 2 && aligned && is_core_dtype(dtype)) {
-        if (P > sched::kMaxFusedPeers) return run_scan_blocked(op, dtype, alg, outs, ins, P, n, s);
+        if (P > sched::max_fused_peers(alg)) return run_scan_blocked(op, dtype, alg, outs, ins, P, n, s);
         PeerPtrs ptrs{};
         for (int p = 0; p < P; ++p) {
             ptrs.in[p] = ins[p];

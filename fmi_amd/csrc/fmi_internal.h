@@ -96,6 +96,8 @@ int launch_fused_reduce(int op, int dtype, int P, const PeerPtrs& ptrs, size_t n
 int launch_fused_reduce_ltr(int op, int dtype, int P, const PeerPtrs& ptrs, size_t n, hipStream_t s);
 int launch_fused_scan(int op, int dtype, int P, const PeerPtrs& ptrs, size_t n, hipStream_t s);
 int launch_fused_scan_ltr(int op, int dtype, int P, const PeerPtrs& ptrs, size_t n, hipStream_t s);
+// scans for P = 17..31 (alg = sched::kScan or kScanLtr), reached through the two launches above
+int launch_fused_scan_wide(int op, int dtype, int alg, int P, const PeerPtrs& ptrs, size_t n, hipStream_t s);
 // Blocks of a scan beyond 16 peers (sched::kScanCarry / kScanLtrCarry): ptrs.in[0] is the carry, out[0] unused.
 int launch_fused_scan_carry(int op, int dtype, int P, const PeerPtrs& ptrs, size_t n, hipStream_t s);
 int launch_fused_scan_ltr_carry(int op, int dtype, int P, const PeerPtrs& ptrs, size_t n, hipStream_t s);

@@ -269,7 +269,7 @@ inline constexpr bool kFusedNT = true;
 
 struct PeerPtrs {
     const void* in[sched::kFusedInputCap];
-    void* out[sched::kMaxFusedPeers];
+    void* out[sched::kFusedInputCap];
 };
 
 // Program fields as integral constants: reading them through these variable templates guarantees the

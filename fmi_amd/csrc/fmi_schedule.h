@@ -44,11 +44,15 @@ inline constexpr int kMaxFusedPeers = 16;   // fused single-pass kernels are ins
 // ... and allreduce_no_order up to 31: the pre-fold of peers 16.. into 0.. then the 16-peer recursive
 // doubling, in one pass (also the block program of larger non-power-of-two P, fmi_dev.hip tree_blocked)
 inline constexpr int kMaxFusedAllreducePeers = 31;
+inline constexpr int kMaxFusedScanPeers = 31;  // the peer-axis scans likewise (P outputs, one pass)
 inline constexpr int kFusedInputCap = 32;
 inline constexpr int kFusedStepCap = 80;    // >= max steps of a fused program (allreduce P=31: 79)
 
 constexpr int max_fused_peers(int alg) {
-    return alg == 0 /*kAllreduce*/ ? kMaxFusedAllreducePeers : alg == 7 /*kAllreducePrefold16*/ ? 32 : kMaxFusedPeers;
+    return alg == 0 /*kAllreduce*/                    ? kMaxFusedAllreducePeers
+           : alg == 3 || alg == 4 /*kScan, kScanLtr*/ ? kMaxFusedScanPeers
+           : alg == 7 /*kAllreducePrefold16*/         ? 32
+                                                      : kMaxFusedPeers;
 }
 inline constexpr int kMaxPeers = 256;       // P-way programs beyond the fused kernels, up to this P
 inline constexpr int kHostStepCap = 2560;   // >= max steps for P <= 256 (allreduce P=256: 2048)

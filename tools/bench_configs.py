@@ -95,7 +95,7 @@ def wide_tree_rows(it):
         row(f"tree allreduce {op.name.lower()} f32 P={P} x {n * 4 // MIB}MiB rank 5", (P + 1) * n * 4, med, mn)
         del ins, out
     # scans: P outputs; one pass would be 2P buckets, the blocked schedule moves `bucket_passes`
-    for alg, P, moved in ((Alg.SCAN, 32, 84), (Alg.SCAN, 64, 184),
+    for alg, P, moved in ((Alg.SCAN, 24, 48), (Alg.SCAN, 32, 84), (Alg.SCAN, 64, 184),
                           (Alg.SCAN_LTR, 64, 64 + 64 + 4)):
         n = 1024 * MIB // 4 // P
         ins = [Bucket(n, np.float32).fill_synthetic(7, p) for p in range(P)]
