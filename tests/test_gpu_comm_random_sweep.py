@@ -3,6 +3,8 @@ random rank count, collective, order (commutative or left-to-right), op, dtype a
 shard grid, its zero padding, the all-to-all, the fused (or blocked) shard program and the gather /
 all-to-all back — every rank's result bit-exact against the oracle's simulation of the reference
 collective. Deterministic: the case list is a function of the seed."""
+import os
+
 import numpy as np
 import pytest
 
@@ -14,6 +16,15 @@ from tests.test_gpu_comm import run_ranks
 from tests.test_gpu_parity import ALL_DTYPES, OPNAME, OPS, assert_bit_equal, inputs
 
 pytestmark = pytest.mark.gpu
+
+
+def _seeds(default):
+    """FMI_SWEEP_SEEDS=a:b runs seeds a..b-1 instead (long soak runs); the default suite runs two."""
+    spec = os.environ.get("FMI_SWEEP_SEEDS")
+    if not spec:
+        return default
+    lo, hi = (int(v) for v in spec.split(":"))
+    return list(range(lo, hi))
 
 CASES = 48
 
@@ -31,7 +42,7 @@ def _cases(seed):
         yield k, N, kind, ordered, op, dtype, n, root
 
 
-@pytest.mark.parametrize("seed", [11, 12])
+@pytest.mark.parametrize("seed", _seeds([11, 12]))
 def test_random_comm_cases(device, seed):
     done = 0
     for k, N, kind, ordered, op, dtype, n, root in _cases(seed):

@@ -2,6 +2,8 @@
 blocks with ragged last blocks, and the 8/16-bit pairwise-pass programs), algorithm, op, dtype, bucket
 length and element offset (aligned and unaligned views), every result bit-exact against the oracle's
 simulation of the reference collective. Deterministic: the case list is a function of the seed."""
+import os
+
 import numpy as np
 import pytest
 
@@ -11,6 +13,15 @@ from oracle import fmi_oracle as orc
 from tests.test_gpu_parity import ALL_DTYPES, OPNAME, OPS, assert_bit_equal, inputs
 
 pytestmark = pytest.mark.gpu
+
+
+def _seeds(default):
+    """FMI_SWEEP_SEEDS=a:b runs seeds a..b-1 instead (long soak runs); the default suite runs two."""
+    spec = os.environ.get("FMI_SWEEP_SEEDS")
+    if not spec:
+        return default
+    lo, hi = (int(v) for v in spec.split(":"))
+    return list(range(lo, hi))
 
 CASES = 160
 
@@ -28,7 +39,7 @@ def _cases(seed):
         yield k, P, alg, op, dtype, n, off, rank
 
 
-@pytest.mark.parametrize("seed", [1, 2])
+@pytest.mark.parametrize("seed", _seeds([1, 2]))
 def test_random_p_way_cases(device, seed):
     done = 0
     for k, P, alg, op, dtype, n, off, rank in _cases(seed):
