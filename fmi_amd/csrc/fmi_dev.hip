@@ -245,17 +245,18 @@ int run_program_stepwise(int op, int dtype, const sched::HostProgram& prog, void
 }
 
 // ----------------------------------------------------------------------------------------------------
-// Tree algorithms beyond 16 peers as fused 16-peer sub-programs. Each program splits along blocks of 16
+// Tree algorithms beyond the fused kernels as fused sub-programs. Each program splits along blocks of 16
 // consecutive (transformed) peers, and every piece is exactly one of the fused kernels' own programs
 // (fmi_schedule.h), so the bracketing is the reference's:
 //   reduce_ltr  ((x0 + .. + x15) + x16 + .. + x30) + ..: a fused 16-peer fold, then fused folds of the
 //               running value and the next 15 peers.
 //   reduce      binomial rounds 0..3 stay inside blocks of 16 (the block's own reduce program); rounds 4..
 //               combine the block values at spans 16, 32, .. = the reduce program over ceil(P/16) values.
-//   allreduce   after the pre-fold of peers >= 2^k into peer - 2^k, recursive-doubling rounds 0..3 stay
-//               inside blocks of 16 and leave position p holding the block's 16-peer allreduce for rank
-//               p % 16; rounds 4.. pair positions with equal p % 16 = the allreduce program over the
-//               2^k / 16 block values, for rank p / 16.
+//   allreduce   (P > 31; up to 31 it is one fused kernel) after the pre-fold of peers >= 2^k into
+//               peer - 2^k, recursive-doubling rounds 0..3 stay inside blocks of 16 and leave position p
+//               holding the block's 16-peer allreduce for rank p % 16; rounds 4.. pair positions with
+//               equal p % 16 = the allreduce program over the 2^k / 16 block values, for rank p / 16. A
+//               block pre-folds its partners inside its own kernel (16 + m inputs, or 32 for m = 16).
 // Every input is read once; temps cost one write + one read per block value (P = 64: 73 bucket passes
 // instead of 189 for pairwise steps). A dry run only counts the temps.
 // ----------------------------------------------------------------------------------------------------
