@@ -37,9 +37,10 @@ DeviceState g_state;  // one process drives one device (one process per GPU, as 
 
 // Defaults from tools/tune_pair.py on MI355X (C2, 256 MiB f32): nontemporal one-shot tiles, 4 × 16 B per
 // operand per thread, 256-thread workgroups — 125 µs = 6.4 TB/s vs 142 µs for plain loads/stores.
-std::atomic<long long> g_tune[7] = {2 /*variant: nontemporal tiles*/, 4 /*unroll*/, 256 /*block*/,
+std::atomic<long long> g_tune[8] = {2 /*variant: nontemporal tiles*/, 4 /*unroll*/, 256 /*block*/,
                                     8 /*grid per CU*/, 64ll << 20 /*host chunk*/, 1 /*host zero-copy*/,
-                                    64 /*fused in-flight KiB per CU (tools/ab_fused_cap.py)*/};
+                                    64 /*fused in-flight KiB per CU (tools/ab_fused_cap.py)*/,
+                                    1 /*one-pass blocked scan*/};
 
 int hip_fail(const char* what, hipError_t e) {
     return fail(FMI_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
@@ -433,6 +434,26 @@ int scan_blocked(int op, int dtype, int alg, void* const* outs, const void* cons
 
 int run_scan_blocked(int op, int dtype, int alg, void* const* outs, const void* const* ins, int P, size_t n,
                      hipStream_t s) {
+    constexpr int BL = sched::kScanBlock;
+    const int B = P / BL, r = P % BL;
+    if (alg == FMI_ALG_SCAN && B >= 2 && B <= kMaxOnePassScanBlocks && g_tune[FMI_TUNE_SCAN_ONE_PASS].load() != 0) {
+        // every full block in one pass (fmi_fused_scan_blocked.hip), then a ragged block as scan_blocked's
+        // carry program from S_{B-1} = outs[16 B - 1]
+        BlockedScanPtrs ptrs{};
+        for (int p = 0; p < B * BL; ++p) {
+            ptrs.in[p] = ins[p];
+            ptrs.out[p] = outs[p];
+        }
+        FMI_RC_TRY(launch_scan_blocks_one_pass(op, dtype, B, ptrs, n, s));
+        if (r == 0) return FMI_OK;
+        PeerPtrs c{};
+        c.in[0] = outs[B * BL - 1];
+        for (int j = 0; j < r; ++j) {
+            c.in[1 + j] = ins[B * BL + j];
+            c.out[1 + j] = outs[B * BL + j];
+        }
+        return launch_fused_scan_carry(op, dtype, r + 1, c, n, s);
+    }
     TreeTemps count;
     FMI_RC_TRY(scan_blocked(op, dtype, alg, outs, ins, P, n, s, count));
     std::lock_guard<std::mutex> lk(g_mu);
@@ -896,6 +917,9 @@ int fmi_tune_set(int key, long long value) {
         case FMI_TUNE_FUSED_INFLIGHT_KIB:
             if (value < 0 || value > 4096) return fail(FMI_ERR_INVALID, "fused in-flight budget must be in [0, 4096] KiB");
             break;
+        case FMI_TUNE_SCAN_ONE_PASS:
+            if (value != 0 && value != 1) return fail(FMI_ERR_INVALID, "one-pass blocked scan must be 0 or 1");
+            break;
         default: return fail(FMI_ERR_INVALID, "unknown tuning key");
     }
     g_tune[key].store(value);
@@ -903,7 +927,7 @@ int fmi_tune_set(int key, long long value) {
 }
 
 int fmi_tune_get(int key, long long* value) {
-    if (!value || key < 0 || key > FMI_TUNE_FUSED_INFLIGHT_KIB) return fail(FMI_ERR_INVALID, "bad tuning query");
+    if (!value || key < 0 || key > FMI_TUNE_SCAN_ONE_PASS) return fail(FMI_ERR_INVALID, "bad tuning query");
     *value = g_tune[key].load();
     return FMI_OK;
 }

@@ -253,11 +253,13 @@ typedef enum {
     FMI_TUNE_HOST_CHUNK = 4,   /* bytes per chunk of fmi_host_reduce_pair's staged pipeline */
     FMI_TUNE_HOST_ZERO_COPY = 5, /* 1: page-locked host buckets are combined in place over PCIe by the
                                    kernel (no staging); 0: always the staged H2D/kernel/D2H pipeline */
-    FMI_TUNE_FUSED_INFLIGHT_KIB = 6 /* fused P-way kernels (tree, scan): budget of peer-load bytes in
+    FMI_TUNE_FUSED_INFLIGHT_KIB = 6, /* fused P-way kernels (tree, scan): budget of peer-load bytes in
                                        flight per CU, in KiB; a workgroup of the P-way kernel loads
                                        4 KiB x P, so at most max(2, ceil(budget / (4 P))) workgroups stay
                                        resident per CU (an LDS reservation enforces it); 0 = no cap. Default 64
                                        (fewer concurrent HBM streams at large P) */
+    FMI_TUNE_SCAN_ONE_PASS = 7 /* scan_no_order over 32..79 peers: 1 = one pass over every input (default),
+                                  0 = the blocked launches (inputs of blocks >= 1 read twice); same bits */
 } fmi_tune_key_t;
 int fmi_tune_set(int key, long long value);
 int fmi_tune_get(int key, long long* value);

@@ -341,7 +341,32 @@ def test_extra_dtypes_p_way_programs(device, dtype):
                     assert_bit_equal(outs[k].numpy(), want[k], f"{alg.name} P={P} {op.name} peer {k}")
 
 
-@pytest.mark.parametrize("P", [8, 40, 64])
+@pytest.mark.parametrize("P", [32, 37, 48, 64, 79])
+def test_one_pass_blocked_scan_matches_blocked_launches(device, P):
+    """scan_no_order over 32..79 peers: the one-pass kernel (fmi_fused_scan_blocked.hip, every input read
+    once) and the blocked launches (FMI_TUNE_SCAN_ONE_PASS = 0) give the oracle's bits, every op x core
+    dtype, a multi-wave grid with a ragged tail, full and ragged last blocks."""
+    n = 3 * 4096 + 5
+    old = fmi_amd.tune_get(Tune.SCAN_ONE_PASS)
+    try:
+        for dtype in DTYPES:
+            xs = _peer_inputs(dtype, n, P, seed=11)
+            ins = [dev(x) for x in xs]
+            for op in OPS:
+                with np.errstate(all="ignore"):
+                    want, _ = orc.scan(xs, orc.OPS[OPNAME[op]])
+                for one_pass in (1, 0):
+                    fmi_amd.tune_set(Tune.SCAN_ONE_PASS, one_pass)
+                    outs = [Bucket(n, dtype) for _ in range(P)]
+                    fmi_amd.scan_peers(op, Alg.SCAN, outs, ins)
+                    for k in range(P):
+                        assert_bit_equal(outs[k].numpy(), want[k],
+                                         f"P={P} {np.dtype(dtype).name} {op.name} one_pass={one_pass} peer {k}")
+    finally:
+        fmi_amd.tune_set(Tune.SCAN_ONE_PASS, old)
+
+
+@pytest.mark.parametrize("P", [8, 40, 64, 100])
 def test_scan_in_place(device, P):
     """outs == ins: beyond 16 peers the blocked scan writes block prefixes into outputs whose inputs the
     later passes must no longer read."""
