@@ -101,14 +101,16 @@ int launch_fused_scan_wide(int op, int dtype, int alg, int P, const PeerPtrs& pt
 // Blocks of a scan beyond 16 peers (sched::kScanCarry / kScanLtrCarry): ptrs.in[0] is the carry, out[0] unused.
 int launch_fused_scan_carry(int op, int dtype, int P, const PeerPtrs& ptrs, size_t n, hipStream_t s);
 int launch_fused_scan_ltr_carry(int op, int dtype, int P, const PeerPtrs& ptrs, size_t n, hipStream_t s);
-// scan_no_order over B full blocks of 16 peers (2 <= B <= kMaxOnePassScanBlocks) in one pass: every input read
+// scan_no_order over B full blocks of 16 peers (2 <= B <= kMaxOnePassScanBlocks, P = 32..143) in one pass: every input read
 // once, all 16 B outputs written (fmi_fused_scan_blocked.hip); a ragged last block is left to the caller.
-inline constexpr int kMaxOnePassScanBlocks = 4;
+inline constexpr int kMaxOnePassScanBlocks = 8;
+inline constexpr int kOnePassScanBlocksNarrow = 4;  // B <= 4 in one translation unit, 5..8 in another
 struct BlockedScanPtrs {
     const void* in[sched::kScanBlock * kMaxOnePassScanBlocks];
     void* out[sched::kScanBlock * kMaxOnePassScanBlocks];
 };
 int launch_scan_blocks_one_pass(int op, int dtype, int B, const BlockedScanPtrs& ptrs, size_t n, hipStream_t s);
+int launch_scan_blocks_one_pass_wide(int op, int dtype, int B, const BlockedScanPtrs& ptrs, size_t n, hipStream_t s);
 
 // Workgroups to cover `items` with `block` threads each (at least 1). Callers cap it before narrowing.
 inline size_t grid_for(size_t items, unsigned block) {

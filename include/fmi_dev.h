@@ -258,7 +258,7 @@ typedef enum {
                                        4 KiB x P, so at most max(2, ceil(budget / (4 P))) workgroups stay
                                        resident per CU (an LDS reservation enforces it); 0 = no cap. Default 64
                                        (fewer concurrent HBM streams at large P) */
-    FMI_TUNE_SCAN_ONE_PASS = 7 /* scan_no_order over 32..79 peers: 1 = one pass over every input (default),
+    FMI_TUNE_SCAN_ONE_PASS = 7 /* scan_no_order over 32..143 peers: 1 = one pass over every input (default),
                                   0 = the blocked launches (inputs of blocks >= 1 read twice); same bits */
 } fmi_tune_key_t;
 int fmi_tune_set(int key, long long value);

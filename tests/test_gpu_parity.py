@@ -341,9 +341,9 @@ def test_extra_dtypes_p_way_programs(device, dtype):
                     assert_bit_equal(outs[k].numpy(), want[k], f"{alg.name} P={P} {op.name} peer {k}")
 
 
-@pytest.mark.parametrize("P", [32, 37, 48, 64, 79])
+@pytest.mark.parametrize("P", [32, 37, 48, 64, 79, 100, 128])
 def test_one_pass_blocked_scan_matches_blocked_launches(device, P):
-    """scan_no_order over 32..79 peers: the one-pass kernel (fmi_fused_scan_blocked.hip, every input read
+    """scan_no_order over 32..143 peers: the one-pass kernel (fmi_fused_scan_blocked.hip, every input read
     once) and the blocked launches (FMI_TUNE_SCAN_ONE_PASS = 0) give the oracle's bits, every op x core
     dtype, a multi-wave grid with a ragged tail, full and ragged last blocks."""
     n = 3 * 4096 + 5

@@ -95,11 +95,12 @@ def wide_tree_rows(it):
         row(f"tree allreduce {op.name.lower()} f32 P={P} x {n * 4 // MIB}MiB rank 5", (P + 1) * n * 4, med, mn)
         del ins, out
     # scans: P outputs; one pass would be 2P buckets, the schedule moves `bucket_passes`. scan_no_order over
-    # 32..79 peers runs the one-pass kernel by default (2P, +1 carry read for a ragged block); the blocked
+    # 32..143 peers runs the one-pass kernel by default (2P, +1 carry read for a ragged block); the blocked
     # launches (FMI_TUNE_SCAN_ONE_PASS = 0) read the inputs of blocks >= 1 twice.
     for alg, P, moved, one_pass in ((Alg.SCAN, 24, 48, 1), (Alg.SCAN, 32, 64, 1), (Alg.SCAN, 32, 84, 0),
                                     (Alg.SCAN, 40, 81, 1), (Alg.SCAN, 48, 96, 1), (Alg.SCAN, 48, 134, 0),
                                     (Alg.SCAN, 64, 128, 1), (Alg.SCAN, 64, 184, 0),
+                                    (Alg.SCAN, 128, 256, 1), (Alg.SCAN, 128, 384, 0),
                                     (Alg.SCAN_LTR, 64, 64 + 64 + 4, 1)):
         n = 1024 * MIB // 4 // P
         ins = [Bucket(n, np.float32).fill_synthetic(7, p) for p in range(P)]
