@@ -351,6 +351,12 @@ int tree_blocked(int op, int dtype, int alg, void* out, const void* const* ins, 
 
 int run_tree_blocked(int op, int dtype, int alg, void* out, const void* const* ins, int P, int rank, size_t n,
                      hipStream_t s) {
+    if (g_tune[FMI_TUNE_BLOCKS_ONE_PASS].load() != 0 && tree_blocks_one_pass_covers(op, dtype, alg, P)) {
+        BlockedScanPtrs ptrs{};
+        for (int p = 0; p < P; ++p) ptrs.in[p] = ins[p];
+        ptrs.out[0] = out;
+        return launch_tree_blocks_one_pass(op, dtype, alg, P, ptrs, n, s);
+    }
     TreeTemps count;
     FMI_RC_TRY(tree_blocked(op, dtype, alg, out, ins, P, rank, n, s, count));
     std::lock_guard<std::mutex> lk(g_mu);
@@ -436,7 +442,7 @@ int run_scan_blocked(int op, int dtype, int alg, void* const* outs, const void* 
                      hipStream_t s) {
     constexpr int BL = sched::kScanBlock;
     const int B = P / BL, r = P % BL;
-    if (alg == FMI_ALG_SCAN && B >= 2 && B <= kMaxOnePassScanBlocks && g_tune[FMI_TUNE_SCAN_ONE_PASS].load() != 0) {
+    if (alg == FMI_ALG_SCAN && B >= 2 && B <= kMaxOnePassScanBlocks && g_tune[FMI_TUNE_BLOCKS_ONE_PASS].load() != 0) {
         // every full block in one pass (fmi_fused_scan_blocked.hip), then a ragged block as scan_blocked's
         // carry program from S_{B-1} = outs[16 B - 1]
         BlockedScanPtrs ptrs{};
@@ -917,7 +923,7 @@ int fmi_tune_set(int key, long long value) {
         case FMI_TUNE_FUSED_INFLIGHT_KIB:
             if (value < 0 || value > 4096) return fail(FMI_ERR_INVALID, "fused in-flight budget must be in [0, 4096] KiB");
             break;
-        case FMI_TUNE_SCAN_ONE_PASS:
+        case FMI_TUNE_BLOCKS_ONE_PASS:
             if (value != 0 && value != 1) return fail(FMI_ERR_INVALID, "one-pass blocked scan must be 0 or 1");
             break;
         default: return fail(FMI_ERR_INVALID, "unknown tuning key");
@@ -927,7 +933,7 @@ int fmi_tune_set(int key, long long value) {
 }
 
 int fmi_tune_get(int key, long long* value) {
-    if (!value || key < 0 || key > FMI_TUNE_SCAN_ONE_PASS) return fail(FMI_ERR_INVALID, "bad tuning query");
+    if (!value || key < 0 || key > FMI_TUNE_BLOCKS_ONE_PASS) return fail(FMI_ERR_INVALID, "bad tuning query");
     *value = g_tune[key].load();
     return FMI_OK;
 }

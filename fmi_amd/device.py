@@ -56,7 +56,7 @@ class Tune(enum.IntEnum):
     HOST_CHUNK = 4
     HOST_ZERO_COPY = 5
     FUSED_INFLIGHT_KIB = 6
-    SCAN_ONE_PASS = 7
+    BLOCKS_ONE_PASS = 7
 
 
 NP_DTYPE = {DType.F32: np.float32, DType.F64: np.float64, DType.I32: np.int32, DType.I64: np.int64,

@@ -258,8 +258,11 @@ typedef enum {
                                        4 KiB x P, so at most max(2, ceil(budget / (4 P))) workgroups stay
                                        resident per CU (an LDS reservation enforces it); 0 = no cap. Default 64
                                        (fewer concurrent HBM streams at large P) */
-    FMI_TUNE_SCAN_ONE_PASS = 7 /* scan_no_order over 32..143 peers: 1 = one pass over every input (default),
-                                  0 = the blocked launches (inputs of blocks >= 1 read twice); same bits */
+    FMI_TUNE_BLOCKS_ONE_PASS = 7 /* P-way programs beyond 31 peers in one pass over every input (default 1):
+                                    scan_no_order over 32..143 peers, reduce_no_order over 16 B peers (B <= 8),
+                                    allreduce_no_order over 32 / 64 / 128 peers (not float max / min);
+                                    0 = the blocked launches (block values through temps; the scan reads
+                                    the inputs of blocks >= 1 twice). Same bits either way */
 } fmi_tune_key_t;
 int fmi_tune_set(int key, long long value);
 int fmi_tune_get(int key, long long* value);

@@ -134,12 +134,12 @@ def test_tuning_knobs_validate():
     fmi_amd.tune_set(fmi_amd.Tune.FUSED_INFLIGHT_KIB, 64)
     with pytest.raises(fmi_amd.FmiError):
         fmi_amd.tune_set(fmi_amd.Tune.FUSED_INFLIGHT_KIB, -1)
-    assert fmi_amd.tune_get(fmi_amd.Tune.SCAN_ONE_PASS) == 1  # default: one pass over every input
-    fmi_amd.tune_set(fmi_amd.Tune.SCAN_ONE_PASS, 0)
-    assert fmi_amd.tune_get(fmi_amd.Tune.SCAN_ONE_PASS) == 0
-    fmi_amd.tune_set(fmi_amd.Tune.SCAN_ONE_PASS, 1)
+    assert fmi_amd.tune_get(fmi_amd.Tune.BLOCKS_ONE_PASS) == 1  # default: one pass over every input
+    fmi_amd.tune_set(fmi_amd.Tune.BLOCKS_ONE_PASS, 0)
+    assert fmi_amd.tune_get(fmi_amd.Tune.BLOCKS_ONE_PASS) == 0
+    fmi_amd.tune_set(fmi_amd.Tune.BLOCKS_ONE_PASS, 1)
     with pytest.raises(fmi_amd.FmiError):
-        fmi_amd.tune_set(fmi_amd.Tune.SCAN_ONE_PASS, 2)
+        fmi_amd.tune_set(fmi_amd.Tune.BLOCKS_ONE_PASS, 2)
 
 
 @pytest.mark.parametrize("P", list(range(1, 34)) + [48, 64, 100, 129, 256])

@@ -344,10 +344,10 @@ def test_extra_dtypes_p_way_programs(device, dtype):
 @pytest.mark.parametrize("P", [32, 37, 48, 64, 79, 100, 128])
 def test_one_pass_blocked_scan_matches_blocked_launches(device, P):
     """scan_no_order over 32..143 peers: the one-pass kernel (fmi_fused_scan_blocked.hip, every input read
-    once) and the blocked launches (FMI_TUNE_SCAN_ONE_PASS = 0) give the oracle's bits, every op x core
+    once) and the blocked launches (FMI_TUNE_BLOCKS_ONE_PASS = 0) give the oracle's bits, every op x core
     dtype, a multi-wave grid with a ragged tail, full and ragged last blocks."""
     n = 3 * 4096 + 5
-    old = fmi_amd.tune_get(Tune.SCAN_ONE_PASS)
+    old = fmi_amd.tune_get(Tune.BLOCKS_ONE_PASS)
     try:
         for dtype in DTYPES:
             xs = _peer_inputs(dtype, n, P, seed=11)
@@ -356,14 +356,48 @@ def test_one_pass_blocked_scan_matches_blocked_launches(device, P):
                 with np.errstate(all="ignore"):
                     want, _ = orc.scan(xs, orc.OPS[OPNAME[op]])
                 for one_pass in (1, 0):
-                    fmi_amd.tune_set(Tune.SCAN_ONE_PASS, one_pass)
+                    fmi_amd.tune_set(Tune.BLOCKS_ONE_PASS, one_pass)
                     outs = [Bucket(n, dtype) for _ in range(P)]
                     fmi_amd.scan_peers(op, Alg.SCAN, outs, ins)
                     for k in range(P):
                         assert_bit_equal(outs[k].numpy(), want[k],
                                          f"P={P} {np.dtype(dtype).name} {op.name} one_pass={one_pass} peer {k}")
     finally:
-        fmi_amd.tune_set(Tune.SCAN_ONE_PASS, old)
+        fmi_amd.tune_set(Tune.BLOCKS_ONE_PASS, old)
+
+
+@pytest.mark.parametrize("P", [32, 48, 64, 128])
+def test_one_pass_blocked_tree_matches_blocked_launches(device, P):
+    """reduce over 16 B peers and allreduce over 32 / 64 / 128 peers: the one-pass kernel
+    (fmi_fused_tree_blocked.hip) and the blocked launches (FMI_TUNE_BLOCKS_ONE_PASS = 0) give the oracle's bits
+    for every op x core dtype, several roots / ranks, and in place (out = an input)."""
+    n = 2 * 4096 + 3
+    old = fmi_amd.tune_get(Tune.BLOCKS_ONE_PASS)
+    try:
+        for dtype in DTYPES:
+            xs = _peer_inputs(dtype, n, P, seed=13)
+            ins = [dev(x) for x in xs]
+            for op in OPS:
+                f = orc.OPS[OPNAME[op]]
+                with np.errstate(all="ignore"):
+                    want_ar, _ = orc.allreduce(xs, f) if P & (P - 1) == 0 else (None, None)
+                    want_red = {root: orc.reduce(xs, f, root=root)[0] for root in (0, 5)}
+                for one_pass in (1, 0):
+                    fmi_amd.tune_set(Tune.BLOCKS_ONE_PASS, one_pass)
+                    what = f"P={P} {np.dtype(dtype).name} {op.name} one_pass={one_pass}"
+                    out = Bucket(n, dtype)
+                    for root in (0, 5):
+                        fmi_amd.reduce_tree(op, Alg.REDUCE, out, ins, rank=root)
+                        assert_bit_equal(out.numpy(), want_red[root], f"reduce root {root} {what}")
+                    if want_ar is not None:
+                        for rank in (0, P - 1):
+                            fmi_amd.reduce_tree(op, Alg.ALLREDUCE, out, ins, rank=rank)
+                            assert_bit_equal(out.numpy(), want_ar[rank], f"allreduce rank {rank} {what}")
+                        acc = [dev(x) for x in xs[:1]] + ins[1:]  # in place: out is peer 0's bucket
+                        fmi_amd.reduce_tree(op, Alg.ALLREDUCE, acc[0], acc, rank=0)
+                        assert_bit_equal(acc[0].numpy(), want_ar[0], f"allreduce in place {what}")
+    finally:
+        fmi_amd.tune_set(Tune.BLOCKS_ONE_PASS, old)
 
 
 @pytest.mark.parametrize("P", [8, 40, 64, 100])

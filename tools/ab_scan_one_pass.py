@@ -1,5 +1,5 @@
 """A/B of the one-pass blocked scan (P = 32, 48, 64, 128 over 1 GiB of f32 input): against the blocked launches
-(FMI_TUNE_SCAN_ONE_PASS = 0) and over the residency cap FMI_TUNE_FUSED_INFLIGHT_KIB (64 -> 2 workgroups per CU,
+(FMI_TUNE_BLOCKS_ONE_PASS = 0) and over the residency cap FMI_TUNE_FUSED_INFLIGHT_KIB (64 -> 2 workgroups per CU,
 192 -> 3, 0 -> register-limited), interleaved in one process over several rounds. One JSON object per
 (round, form, cap, P): median µs and fraction of the 8 TB/s peak (on the one-pass bytes, 2P buckets).
 Usage: ab_scan_one_pass.py [caps, default 64] [rounds, default 3]"""
@@ -46,14 +46,14 @@ def main():
             fmi_amd.tune_set(Tune.FUSED_INFLIGHT_KIB, cap)
             for P, (ins, outs, n) in sets.items():
                 for one_pass in (1, 0):
-                    fmi_amd.tune_set(Tune.SCAN_ONE_PASS, one_pass)
+                    fmi_amd.tune_set(Tune.BLOCKS_ONE_PASS, one_pass)
                     ms = timed(lambda: fmi_amd.scan_peers(Op.SUM, Alg.SCAN, outs, ins), 10)
                     frac = 2 * P * n * 4 / (ms * 1e-3) / 8e12
                     print(json.dumps({"round": r, "form": "one-pass" if one_pass else "blocked launches",
                                       "cap_kib": cap, "P": P, "median_us": round(ms * 1e3, 2),
                                       "frac_of_peak": round(frac, 4)}), flush=True)
     fmi_amd.tune_set(Tune.FUSED_INFLIGHT_KIB, old)
-    fmi_amd.tune_set(Tune.SCAN_ONE_PASS, 1)
+    fmi_amd.tune_set(Tune.BLOCKS_ONE_PASS, 1)
 
 
 if __name__ == "__main__":

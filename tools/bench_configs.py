@@ -78,13 +78,20 @@ def wide_tree_rows(it):
               (Alg.ALLREDUCE, 32): 32 + 2 + 2 + 1, (Alg.ALLREDUCE, 48): 32 + 1 + 16 + 1 + 2 + 1,
               (Alg.ALLREDUCE, 64): 64 + 4 + 4 + 1, (Alg.REDUCE, 64): 64 + 4 + 4 + 1,
               (Alg.REDUCE_LTR, 64): 64 + 4 + 4 + 1}
+    # allreduce / reduce over 16 B peers (32, 64 here) run one pass by default (P + 1 buckets); the blocked
+    # launches (FMI_TUNE_BLOCKS_ONE_PASS = 0) write and re-read a temp per block
     for alg, P in passes:
         n = 1024 * MIB // 4 // P
         ins = [Bucket(n, np.float32).fill_synthetic(7, p) for p in range(P)]
         out = Bucket(n, np.float32)
-        med, mn = timed(lambda k: fmi_amd.reduce_tree(Op.SUM, alg, out, ins, rank=P - 1), max(5, it // 2), 1)
-        row(f"tree {alg.name.lower()} f32 P={P} x {n * 4 // MIB}MiB", (P + 1) * n * 4, med, mn,
-            bucket_passes=passes[(alg, P)], one_pass_buckets=P + 1)
+        forms = (1, 0) if alg != Alg.REDUCE_LTR and P % 16 == 0 and (alg == Alg.REDUCE or P & (P - 1) == 0) else (1,)
+        for one_pass in forms:
+            fmi_amd.tune_set(fmi_amd.Tune.BLOCKS_ONE_PASS, one_pass)
+            med, mn = timed(lambda k: fmi_amd.reduce_tree(Op.SUM, alg, out, ins, rank=P - 1), max(5, it // 2), 1)
+            fmi_amd.tune_set(fmi_amd.Tune.BLOCKS_ONE_PASS, 1)
+            form = "" if len(forms) == 1 else (" one-pass" if one_pass else " blocked launches")
+            row(f"tree {alg.name.lower()} f32 P={P} x {n * 4 // MIB}MiB{form}", (P + 1) * n * 4, med, mn,
+                bucket_passes=P + 1 if len(forms) == 2 and one_pass else passes[(alg, P)], one_pass_buckets=P + 1)
         del ins, out
     # rank-aware allreduce kernels (float max/min: operand order differs per rank) against the plain ones
     for P, op in ((16, Op.SUM), (16, Op.MAX), (24, Op.MAX)):
@@ -96,7 +103,7 @@ def wide_tree_rows(it):
         del ins, out
     # scans: P outputs; one pass would be 2P buckets, the schedule moves `bucket_passes`. scan_no_order over
     # 32..143 peers runs the one-pass kernel by default (2P, +1 carry read for a ragged block); the blocked
-    # launches (FMI_TUNE_SCAN_ONE_PASS = 0) read the inputs of blocks >= 1 twice.
+    # launches (FMI_TUNE_BLOCKS_ONE_PASS = 0) read the inputs of blocks >= 1 twice.
     for alg, P, moved, one_pass in ((Alg.SCAN, 24, 48, 1), (Alg.SCAN, 32, 64, 1), (Alg.SCAN, 32, 84, 0),
                                     (Alg.SCAN, 40, 81, 1), (Alg.SCAN, 48, 96, 1), (Alg.SCAN, 48, 134, 0),
                                     (Alg.SCAN, 64, 128, 1), (Alg.SCAN, 64, 184, 0),
@@ -105,9 +112,9 @@ def wide_tree_rows(it):
         n = 1024 * MIB // 4 // P
         ins = [Bucket(n, np.float32).fill_synthetic(7, p) for p in range(P)]
         outs = [Bucket(n, np.float32) for _ in range(P)]
-        fmi_amd.tune_set(fmi_amd.Tune.SCAN_ONE_PASS, one_pass)
+        fmi_amd.tune_set(fmi_amd.Tune.BLOCKS_ONE_PASS, one_pass)
         med, mn = timed(lambda k: fmi_amd.scan_peers(Op.SUM, alg, outs, ins), max(5, it // 2), 1)
-        fmi_amd.tune_set(fmi_amd.Tune.SCAN_ONE_PASS, 1)
+        fmi_amd.tune_set(fmi_amd.Tune.BLOCKS_ONE_PASS, 1)
         form = "" if P <= 31 or alg != Alg.SCAN else (" one-pass" if one_pass else " blocked launches")
         row(f"scan {alg.name.lower()} f32 P={P} x {n * 4 // MIB}MiB{form}", 2 * P * n * 4, med, mn,
             bucket_passes=moved, one_pass_buckets=2 * P)
