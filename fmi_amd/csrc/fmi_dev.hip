@@ -355,7 +355,7 @@ int run_tree_blocked(int op, int dtype, int alg, void* out, const void* const* i
         BlockedScanPtrs ptrs{};
         for (int p = 0; p < P; ++p) ptrs.in[p] = ins[p];
         ptrs.out[0] = out;
-        return launch_tree_blocks_one_pass(op, dtype, alg, P, ptrs, n, s);
+        return launch_tree_blocks_one_pass(op, dtype, alg, P, ptrs, n, alg == FMI_ALG_ALLREDUCE ? rank : 0, s);
     }
     TreeTemps count;
     FMI_RC_TRY(tree_blocked(op, dtype, alg, out, ins, P, rank, n, s, count));

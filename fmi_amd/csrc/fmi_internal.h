@@ -111,10 +111,11 @@ struct BlockedScanPtrs {
 };
 int launch_scan_blocks_one_pass(int op, int dtype, int B, const BlockedScanPtrs& ptrs, size_t n, hipStream_t s);
 int launch_scan_blocks_one_pass_wide(int op, int dtype, int B, const BlockedScanPtrs& ptrs, size_t n, hipStream_t s);
-// reduce_no_order over P = 16 B peers and allreduce_no_order over P = 32, 64, 128 (ops whose bits do not depend on
-// the rank) in one pass: ptrs.in[0..P) the (transformed) inputs, ptrs.out[0] the result (fmi_fused_tree_blocked.hip)
+// reduce_no_order over P = 16 B peers and allreduce_no_order over P = 32, 64, 128 in one pass: ptrs.in[0..P) the
+// (transformed) inputs, ptrs.out[0] the result of peer `rank` (allreduce) (fmi_fused_tree_blocked.hip)
 bool tree_blocks_one_pass_covers(int op, int dtype, int alg, int P);
-int launch_tree_blocks_one_pass(int op, int dtype, int alg, int P, const BlockedScanPtrs& ptrs, size_t n, hipStream_t s);
+int launch_tree_blocks_one_pass(int op, int dtype, int alg, int P, const BlockedScanPtrs& ptrs, size_t n, int rank,
+                                hipStream_t s);
 
 // Workgroups to cover `items` with `block` threads each (at least 1). Callers cap it before narrowing.
 inline size_t grid_for(size_t items, unsigned block) {

@@ -390,7 +390,7 @@ def test_one_pass_blocked_tree_matches_blocked_launches(device, P):
                         fmi_amd.reduce_tree(op, Alg.REDUCE, out, ins, rank=root)
                         assert_bit_equal(out.numpy(), want_red[root], f"reduce root {root} {what}")
                     if want_ar is not None:
-                        for rank in (0, P - 1):
+                        for rank in (0, 17, P - 1):  # float max / min: each rank keeps its own operand order
                             fmi_amd.reduce_tree(op, Alg.ALLREDUCE, out, ins, rank=rank)
                             assert_bit_equal(out.numpy(), want_ar[rank], f"allreduce rank {rank} {what}")
                         acc = [dev(x) for x in xs[:1]] + ins[1:]  # in place: out is peer 0's bucket
@@ -439,6 +439,24 @@ def test_signed_zero_max_follows_each_ranks_operand_order(device):
         out = Bucket(n, np.float32)
         fmi_amd.reduce_tree(Op.MAX, Alg.ALLREDUCE, out, ins, rank=r)
         assert_bit_equal(out.numpy(), want[r], f"rank {r}")
+
+
+@pytest.mark.parametrize("P", [32, 64, 128])
+def test_one_pass_blocked_allreduce_keeps_each_ranks_operand_order(device, P):
+    """Float max / min over ±0 ties beyond 31 peers: the one-pass blocked kernel keeps block rank r % 16 and
+    block-level rank r / 16, so every rank gets its own reference bits (data chosen so that ranks differ)."""
+    n = 4096 + 3
+    rng = np.random.default_rng(P)
+    xs = [np.where(rng.random(n) < 0.5, -0.0, 0.0).astype(np.float32) for _ in range(P)]
+    ins = [dev(x) for x in xs]
+    for op in (Op.MAX, Op.MIN):
+        want, _ = orc.allreduce(xs, orc.OPS[OPNAME[op]])
+        ranks = list(range(P)) if P <= 32 else [0, 1, 15, 16, 17, 31, 33, P // 2 + 5, P - 2, P - 1]
+        assert any(not np.array_equal(want[0].view(np.uint32), want[r].view(np.uint32)) for r in ranks)
+        for r in ranks:
+            out = Bucket(n, np.float32)
+            fmi_amd.reduce_tree(op, Alg.ALLREDUCE, out, ins, rank=r)
+            assert_bit_equal(out.numpy(), want[r], f"P={P} {op.name} rank {r}")
 
 
 def test_float_sum_tolerance_against_sequential_order(device):

@@ -94,7 +94,7 @@ def wide_tree_rows(it):
                 bucket_passes=P + 1 if len(forms) == 2 and one_pass else passes[(alg, P)], one_pass_buckets=P + 1)
         del ins, out
     # rank-aware allreduce kernels (float max/min: operand order differs per rank) against the plain ones
-    for P, op in ((16, Op.SUM), (16, Op.MAX), (24, Op.MAX)):
+    for P, op in ((16, Op.SUM), (16, Op.MAX), (24, Op.MAX), (64, Op.MAX)):
         n = 1024 * MIB // 4 // P
         ins = [Bucket(n, np.float32).fill_synthetic(7, p) for p in range(P)]
         out = Bucket(n, np.float32)
