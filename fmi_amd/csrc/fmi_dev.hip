@@ -351,6 +351,12 @@ int tree_blocked(int op, int dtype, int alg, void* out, const void* const* ins, 
 
 int run_tree_blocked(int op, int dtype, int alg, void* out, const void* const* ins, int P, int rank, size_t n,
                      hipStream_t s) {
+    if (g_tune[FMI_TUNE_BLOCKS_ONE_PASS].load() != 0 && alg == FMI_ALG_REDUCE_LTR && P <= kMaxOnePassScanBlocks * 16) {
+        BlockedScanPtrs ptrs{};
+        for (int p = 0; p < P; ++p) ptrs.in[p] = ins[p];
+        ptrs.out[0] = out;
+        return launch_chain_one_pass(op, dtype, false, P, ptrs, n, s);
+    }
     if (g_tune[FMI_TUNE_BLOCKS_ONE_PASS].load() != 0 && tree_blocks_one_pass_covers(op, dtype, alg, P)) {
         BlockedScanPtrs ptrs{};
         for (int p = 0; p < P; ++p) ptrs.in[p] = ins[p];
@@ -442,6 +448,14 @@ int run_scan_blocked(int op, int dtype, int alg, void* const* outs, const void* 
                      hipStream_t s) {
     constexpr int BL = sched::kScanBlock;
     const int B = P / BL, r = P % BL;
+    if (alg == FMI_ALG_SCAN_LTR && P <= kMaxOnePassScanBlocks * BL && g_tune[FMI_TUNE_BLOCKS_ONE_PASS].load() != 0) {
+        BlockedScanPtrs ptrs{};
+        for (int p = 0; p < P; ++p) {
+            ptrs.in[p] = ins[p];
+            ptrs.out[p] = outs[p];
+        }
+        return launch_chain_one_pass(op, dtype, true, P, ptrs, n, s);
+    }
     if (alg == FMI_ALG_SCAN && B >= 2 && B <= kMaxOnePassScanBlocks && g_tune[FMI_TUNE_BLOCKS_ONE_PASS].load() != 0) {
         // every full block in one pass (fmi_fused_scan_blocked.hip), then a ragged block as scan_blocked's
         // carry program from S_{B-1} = outs[16 B - 1]

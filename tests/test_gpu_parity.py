@@ -366,6 +366,44 @@ def test_one_pass_blocked_scan_matches_blocked_launches(device, P):
         fmi_amd.tune_set(Tune.BLOCKS_ONE_PASS, old)
 
 
+@pytest.mark.parametrize("P", [17, 32, 37, 64, 100, 128])
+def test_one_pass_chain_matches_blocked_launches(device, P):
+    """scan_ltr (32..128 peers) and reduce_ltr (17..128): the one-pass chain kernel (fmi_fused_chain.hip) and the
+    blocked launches give the oracle's left-to-right bits, every op x core dtype, ragged peer blocks, in place."""
+    n = 2 * 4096 + 7
+    old = fmi_amd.tune_get(Tune.BLOCKS_ONE_PASS)
+    try:
+        for dtype in DTYPES:
+            xs = _peer_inputs(dtype, n, P, seed=17)
+            ins = [dev(x) for x in xs]
+            for op in OPS:
+                f = orc.OPS[OPNAME[op]]
+                with np.errstate(all="ignore"):
+                    want_scan, _ = orc.scan(xs, f, commutative=False, associative=False)
+                    want_red, _ = orc.reduce(xs, f, root=0, commutative=False, associative=False)
+                for one_pass in (1, 0):
+                    fmi_amd.tune_set(Tune.BLOCKS_ONE_PASS, one_pass)
+                    what = f"P={P} {np.dtype(dtype).name} {op.name} one_pass={one_pass}"
+                    out = Bucket(n, dtype)
+                    fmi_amd.reduce_tree(op, Alg.REDUCE_LTR, out, ins, rank=P - 1)
+                    assert_bit_equal(out.numpy(), want_red, f"reduce_ltr {what}")
+                    if P > 31:
+                        outs = [Bucket(n, dtype) for _ in range(P)]
+                        fmi_amd.scan_peers(op, Alg.SCAN_LTR, outs, ins)
+                        for k in range(P):
+                            assert_bit_equal(outs[k].numpy(), want_scan[k], f"scan_ltr {what} peer {k}")
+            if dtype == np.float32:  # in place
+                for one_pass in (1, 0):
+                    fmi_amd.tune_set(Tune.BLOCKS_ONE_PASS, one_pass)
+                    bufs = [dev(x) for x in xs]
+                    fmi_amd.scan_peers(Op.SUM, Alg.SCAN_LTR, bufs, bufs)
+                    want, _ = orc.scan(xs, orc.op_sum, commutative=False, associative=False)
+                    for k in range(P):
+                        assert_bit_equal(bufs[k].numpy(), want[k], f"scan_ltr in place one_pass={one_pass} peer {k}")
+    finally:
+        fmi_amd.tune_set(Tune.BLOCKS_ONE_PASS, old)
+
+
 @pytest.mark.parametrize("P", [32, 48, 64, 128])
 def test_one_pass_blocked_tree_matches_blocked_launches(device, P):
     """reduce over 16 B peers and allreduce over 32 / 64 / 128 peers: the one-pass kernel
