@@ -357,6 +357,16 @@ int run_tree_blocked(int op, int dtype, int alg, void* out, const void* const* i
         ptrs.out[0] = out;
         return launch_chain_one_pass(op, dtype, false, P, ptrs, n, s);
     }
+    if (g_tune[FMI_TUNE_BLOCKS_ONE_PASS].load() != 0 && prefold_blocks_one_pass_covers(alg, P)) {
+        const int pow2 = 1 << sched::floor_log2(P);
+        const int r = rank < pow2 ? rank : rank - pow2;  // folded peers get their partner's value back
+        const int lo = r & 15;
+        BlockedScanPtrs ptrs{};
+        for (int p = 0; p < pow2; ++p) ptrs.in[p] = ins[(p & ~15) | ((p & 15) ^ lo)];
+        for (int p = 0; p < P - pow2; ++p) ptrs.in[pow2 + p] = ins[pow2 + ((p & ~15) | ((p & 15) ^ lo))];
+        ptrs.out[0] = out;
+        return launch_prefold_blocks_one_pass(op, dtype, P, ptrs, n, r >> 4, s);
+    }
     if (g_tune[FMI_TUNE_BLOCKS_ONE_PASS].load() != 0 && tree_blocks_one_pass_covers(op, dtype, alg, P)) {
         BlockedScanPtrs ptrs{};
         for (int p = 0; p < P; ++p) ptrs.in[p] = ins[p];

@@ -70,6 +70,60 @@ void tree_blocks_one(const BlockedScanPtrs& ptrs, size_t n, int rank, hipStream_
     tree_blocks_kernel<Op, T, ALG, B, ALL_RANKS><<<grid, kFusedBlock, lds, s>>>(ptrs, n, rank);
 }
 
+// allreduce_no_order over P = 2^k + 16 F peers (F full blocks pre-fold a partner, :100-107): block b < F is the
+// 32-input kAllreducePrefold16 program over its 16 peers and their partners 2^k + 16 b + q, the other blocks the
+// 16-peer recursive doubling; then the doubling over the B = 2^k / 16 block values. The caller permutes each
+// block's pointers by rank % 16 (the doubling is symmetric under p -> p ^ rank, partners move along), so every
+// block value is rank 0's expression; the block level keeps rank / 16's value where the bits depend on it.
+template <class Op, class T, int W, int B, bool PREFOLD>
+__device__ __forceinline__ Lanes<T, W> prefold_block_value(const BlockedScanPtrs& ptrs, int b, size_t elem) {
+    constexpr int ALG = PREFOLD ? sched::kAllreducePrefold16 : sched::kAllreduce;
+    constexpr int NIN = PREFOLD ? 2 * BL : BL;
+    Lanes<T, W> v[NIN + kNumSteps<ALG, NIN>];
+    [&]<size_t... Q>(std::index_sequence<Q...>) {
+        ((v[Q] = load_lanes<kFusedNT, T, W>(static_cast<const T*>(ptrs.in[b * BL + Q]) + elem)), ...);
+        if constexpr (PREFOLD)
+            ((v[BL + Q] = load_lanes<kFusedNT, T, W>(static_cast<const T*>(ptrs.in[B * BL + b * BL + Q]) + elem)), ...);
+    }(std::make_index_sequence<BL>{});
+    run_steps<Op, T, W, ALG, NIN>(v, std::make_index_sequence<kNumSteps<ALG, NIN>>{});
+    return v[kOut<ALG, NIN, 0>];
+}
+
+template <class Op, class T, int W, int B, int F, bool RANKED, size_t... b>
+__device__ __forceinline__ void prefold_blocks_group(const BlockedScanPtrs& ptrs, int rank_hi, size_t elem,
+                                                     std::index_sequence<b...>) {
+    using L = Lanes<T, W>;
+    L bv[B + kNumSteps<sched::kAllreduce, B>];
+    ((bv[b] = prefold_block_value<Op, T, W, B, (static_cast<int>(b) < F)>(ptrs, static_cast<int>(b), elem)), ...);
+    run_steps<Op, T, W, sched::kAllreduce, B>(bv, std::make_index_sequence<kNumSteps<sched::kAllreduce, B>>{});
+    L r;
+    if constexpr (RANKED)
+        r = pick_rank<T, W, sched::kAllreduce, B>(bv, rank_hi, std::make_index_sequence<B>{});
+    else
+        r = bv[kOut<sched::kAllreduce, B, 0>];
+    store_lanes<kFusedNT, T, W>(static_cast<T*>(ptrs.out[0]) + elem, r);
+}
+
+template <class Op, class T, int B, int F, bool RANKED>
+__global__ void __launch_bounds__(256) prefold_blocks_kernel(BlockedScanPtrs ptrs, size_t n, int rank_hi) {
+    constexpr int W = kVecLanes<T>;
+    const size_t nvec = n / W;
+    const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
+    for (size_t g = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x; g < nvec; g += stride)
+        prefold_blocks_group<Op, T, W, B, F, RANKED>(ptrs, rank_hi, g * W, std::make_index_sequence<B>{});
+    const size_t first = nvec * W;
+    if (blockIdx.x == 0 && first + threadIdx.x < n)
+        prefold_blocks_group<Op, T, 1, B, F, RANKED>(ptrs, rank_hi, first + threadIdx.x, std::make_index_sequence<B>{});
+}
+
+template <class Op, class T, int B, int F, bool RANKED>
+void prefold_blocks_one(const BlockedScanPtrs& ptrs, size_t n, int rank_hi, hipStream_t s) {
+    const size_t nvec = n / kVecLanes<T>;
+    const unsigned grid = static_cast<unsigned>(std::min<size_t>(grid_for(nvec, kFusedBlock), kFusedGridCap));
+    const size_t lds = fused_lds_bytes(2 * BL, kFusedBlock * 16);  // a pre-fold block's 32 streams at a time
+    prefold_blocks_kernel<Op, T, B, F, RANKED><<<grid, kFusedBlock, lds, s>>>(ptrs, n, rank_hi);
+}
+
 }  // namespace
 
 bool tree_blocks_one_pass_covers(int op, int dtype, int alg, int P) {
@@ -103,6 +157,34 @@ int launch_tree_blocks_one_pass(int op, int dtype, int alg, int P, const Blocked
             }
         }
         return check_launch("one-pass blocked tree launch");
+    });
+}
+
+bool prefold_blocks_one_pass_covers(int alg, int P) {
+    if (alg != FMI_ALG_ALLREDUCE || P > kMaxOnePassScanBlocks * BL) return false;
+    const int pow2 = 1 << sched::floor_log2(P);
+    const int folded = P - pow2;
+    return (pow2 == 32 || pow2 == 64) && folded > 0 && folded % BL == 0;
+}
+
+int launch_prefold_blocks_one_pass(int op, int dtype, int P, const BlockedScanPtrs& ptrs, size_t n, int rank_hi,
+                                   hipStream_t s) {
+    if (!prefold_blocks_one_pass_covers(FMI_ALG_ALLREDUCE, P))
+        return fail(FMI_ERR_INVALID, "one-pass pre-fold allreduce: unsupported P = " + std::to_string(P));
+    const int pow2 = 1 << sched::floor_log2(P);
+    const int F = (P - pow2) / BL;
+    return with_op_dtype<false>(op, dtype, [&]<class Op, class T>() -> int {
+        constexpr bool ranked = std::is_floating_point_v<T> && (std::is_same_v<Op, OpMax> || std::is_same_v<Op, OpMin>);
+        if (pow2 == 32) {
+            prefold_blocks_one<Op, T, 2, 1, ranked>(ptrs, n, rank_hi, s);
+        } else {
+            switch (F) {
+                case 1: prefold_blocks_one<Op, T, 4, 1, ranked>(ptrs, n, rank_hi, s); break;
+                case 2: prefold_blocks_one<Op, T, 4, 2, ranked>(ptrs, n, rank_hi, s); break;
+                default: prefold_blocks_one<Op, T, 4, 3, ranked>(ptrs, n, rank_hi, s); break;
+            }
+        }
+        return check_launch("one-pass pre-fold allreduce launch");
     });
 }
 

@@ -114,6 +114,11 @@ int launch_scan_blocks_one_pass_wide(int op, int dtype, int B, const BlockedScan
 // reduce_no_order over P = 16 B peers and allreduce_no_order over P = 32, 64, 128 in one pass: ptrs.in[0..P) the
 // (transformed) inputs, ptrs.out[0] the result of peer `rank` (allreduce) (fmi_fused_tree_blocked.hip)
 bool tree_blocks_one_pass_covers(int op, int dtype, int alg, int P);
+// allreduce_no_order over P = 48, 80, 96, 112 (full blocks pre-fold) in one pass: ptrs.in[0..2^k) the doubling
+// group and ptrs.in[2^k..P) the partners, each block permuted by rank % 16 by the caller; rank_hi = rank / 16
+bool prefold_blocks_one_pass_covers(int alg, int P);
+int launch_prefold_blocks_one_pass(int op, int dtype, int P, const BlockedScanPtrs& ptrs, size_t n, int rank_hi,
+                                   hipStream_t s);
 // scan_ltr (scan = true: ptrs.out[0..P)) and reduce_ltr (ptrs.out[0]) over 2..128 peers in one pass, the running
 // value carried in registers (fmi_fused_chain.hip)
 int launch_chain_one_pass(int op, int dtype, bool scan, int P, const BlockedScanPtrs& ptrs, size_t n, hipStream_t s);

@@ -260,7 +260,8 @@ typedef enum {
                                        (fewer concurrent HBM streams at large P) */
     FMI_TUNE_BLOCKS_ONE_PASS = 7 /* P-way programs beyond 31 peers in one pass over every input (default 1):
                                     scan_no_order over 32..143 peers, reduce_no_order over 16 B peers (B <= 8),
-                                    allreduce_no_order over 32 / 64 / 128 peers, scan_ltr and
+                                    allreduce_no_order over 32 / 48 / 64 / 80 / 96 / 112 / 128
+                                    peers, scan_ltr and
                                     reduce_ltr over 32..128 peers;
                                     0 = the blocked launches (block values through temps; the scan reads
                                     the inputs of blocks >= 1 twice). Same bits either way */

@@ -404,10 +404,10 @@ def test_one_pass_chain_matches_blocked_launches(device, P):
         fmi_amd.tune_set(Tune.BLOCKS_ONE_PASS, old)
 
 
-@pytest.mark.parametrize("P", [32, 48, 64, 128])
+@pytest.mark.parametrize("P", [32, 48, 64, 80, 112, 128])
 def test_one_pass_blocked_tree_matches_blocked_launches(device, P):
-    """reduce over 16 B peers and allreduce over 32 / 64 / 128 peers: the one-pass kernel
-    (fmi_fused_tree_blocked.hip) and the blocked launches (FMI_TUNE_BLOCKS_ONE_PASS = 0) give the oracle's bits
+    """reduce over 16 B peers and allreduce over 32..128 peers (pre-fold of full blocks at 48, 80, 112): the
+    one-pass kernels (fmi_fused_tree_blocked.hip) and the blocked launches (FMI_TUNE_BLOCKS_ONE_PASS = 0) give the oracle's bits
     for every op x core dtype, several roots / ranks, and in place (out = an input)."""
     n = 2 * 4096 + 3
     old = fmi_amd.tune_get(Tune.BLOCKS_ONE_PASS)
@@ -418,7 +418,7 @@ def test_one_pass_blocked_tree_matches_blocked_launches(device, P):
             for op in OPS:
                 f = orc.OPS[OPNAME[op]]
                 with np.errstate(all="ignore"):
-                    want_ar, _ = orc.allreduce(xs, f) if P & (P - 1) == 0 else (None, None)
+                    want_ar, _ = orc.allreduce(xs, f)
                     want_red = {root: orc.reduce(xs, f, root=root)[0] for root in (0, 5)}
                 for one_pass in (1, 0):
                     fmi_amd.tune_set(Tune.BLOCKS_ONE_PASS, one_pass)
@@ -427,13 +427,15 @@ def test_one_pass_blocked_tree_matches_blocked_launches(device, P):
                     for root in (0, 5):
                         fmi_amd.reduce_tree(op, Alg.REDUCE, out, ins, rank=root)
                         assert_bit_equal(out.numpy(), want_red[root], f"reduce root {root} {what}")
-                    if want_ar is not None:
-                        for rank in (0, 17, P - 1):  # float max / min: each rank keeps its own operand order
-                            fmi_amd.reduce_tree(op, Alg.ALLREDUCE, out, ins, rank=rank)
-                            assert_bit_equal(out.numpy(), want_ar[rank], f"allreduce rank {rank} {what}")
-                        acc = [dev(x) for x in xs[:1]] + ins[1:]  # in place: out is peer 0's bucket
-                        fmi_amd.reduce_tree(op, Alg.ALLREDUCE, acc[0], acc, rank=0)
-                        assert_bit_equal(acc[0].numpy(), want_ar[0], f"allreduce in place {what}")
+                    pow2 = 1 << (P.bit_length() - 1)
+                    # float max / min: each rank keeps its own operand order; folded ranks >= 2^k get their
+                    # partner's value
+                    for rank in sorted({0, 17, pow2 - 1, P - 1, min(pow2 + 3, P - 1)}):
+                        fmi_amd.reduce_tree(op, Alg.ALLREDUCE, out, ins, rank=rank)
+                        assert_bit_equal(out.numpy(), want_ar[rank], f"allreduce rank {rank} {what}")
+                    acc = [dev(x) for x in xs[:1]] + ins[1:]  # in place: out is peer 0's bucket
+                    fmi_amd.reduce_tree(op, Alg.ALLREDUCE, acc[0], acc, rank=0)
+                    assert_bit_equal(acc[0].numpy(), want_ar[0], f"allreduce in place {what}")
     finally:
         fmi_amd.tune_set(Tune.BLOCKS_ONE_PASS, old)
 
@@ -479,7 +481,7 @@ def test_signed_zero_max_follows_each_ranks_operand_order(device):
         assert_bit_equal(out.numpy(), want[r], f"rank {r}")
 
 
-@pytest.mark.parametrize("P", [32, 64, 128])
+@pytest.mark.parametrize("P", [32, 48, 64, 96, 128])
 def test_one_pass_blocked_allreduce_keeps_each_ranks_operand_order(device, P):
     """Float max / min over ±0 ties beyond 31 peers: the one-pass blocked kernel keeps block rank r % 16 and
     block-level rank r / 16, so every rank gets its own reference bits (data chosen so that ranks differ)."""

@@ -78,13 +78,13 @@ def wide_tree_rows(it):
               (Alg.ALLREDUCE, 32): 32 + 2 + 2 + 1, (Alg.ALLREDUCE, 48): 32 + 1 + 16 + 1 + 2 + 1,
               (Alg.ALLREDUCE, 64): 64 + 4 + 4 + 1, (Alg.REDUCE, 64): 64 + 4 + 4 + 1,
               (Alg.REDUCE_LTR, 64): 64 + 4 + 4 + 1}
-    # allreduce / reduce over 16 B peers (32, 64 here) run one pass by default (P + 1 buckets); the blocked
-    # launches (FMI_TUNE_BLOCKS_ONE_PASS = 0) write and re-read a temp per block
+    # allreduce / reduce over 16 B peers (32, 48, 64 here) and reduce_ltr run one pass by default (P + 1
+    # buckets); the blocked launches (FMI_TUNE_BLOCKS_ONE_PASS = 0) write and re-read a temp per block
     for alg, P in passes:
         n = 1024 * MIB // 4 // P
         ins = [Bucket(n, np.float32).fill_synthetic(7, p) for p in range(P)]
         out = Bucket(n, np.float32)
-        forms = (1, 0) if alg != Alg.REDUCE_LTR and P % 16 == 0 and (alg == Alg.REDUCE or P & (P - 1) == 0) else (1,)
+        forms = (1, 0) if P % 16 == 0 or alg == Alg.REDUCE_LTR else (1,)
         for one_pass in forms:
             fmi_amd.tune_set(fmi_amd.Tune.BLOCKS_ONE_PASS, one_pass)
             med, mn = timed(lambda k: fmi_amd.reduce_tree(Op.SUM, alg, out, ins, rank=P - 1), max(5, it // 2), 1)
