@@ -1,5 +1,6 @@
-// One-pass tree reductions over B full blocks of 16 peers (P = 16 B, 2 <= B <= kMaxOnePassScanBlocks):
-// reduce_no_order (reference src/comm/PeerToPeer.cpp:59-84) for any such P, allreduce_no_order (:96-130) for
+// One-pass tree reductions beyond the fused kernels, up to 128 peers (blocks of 16 peers):
+// reduce_no_order (reference src/comm/PeerToPeer.cpp:59-84; any 17..128 peers, ragged last block included,
+// reduce_any_kernel below), allreduce_no_order (:96-130) for
 // P = 32, 64, 128 (no pre-fold). tree_blocked (fmi_dev.hip) evaluates the same bracketing as a launch per
 // block, each writing its block value to a temp, then a launch over the B temps: P + 2 B + 1 bucket passes.
 // Here one thread computes its lane group's B block values in registers and then the block-level program:
@@ -59,8 +60,6 @@ __global__ void __launch_bounds__(256) tree_blocks_kernel(BlockedScanPtrs ptrs, 
     if (blockIdx.x == 0 && first + threadIdx.x < n)
         tree_blocks_group<Op, T, 1, ALG, B, ALL_RANKS>(ptrs, rank, first + threadIdx.x, std::make_index_sequence<B>{});
 }
-
-using TreeBlocksFn = void (*)(const BlockedScanPtrs&, size_t, int, hipStream_t);
 
 template <class Op, class T, int ALG, int B, bool ALL_RANKS = false>
 void tree_blocks_one(const BlockedScanPtrs& ptrs, size_t n, int rank, hipStream_t s) {
@@ -124,9 +123,58 @@ void prefold_blocks_one(const BlockedScanPtrs& ptrs, size_t n, int rank_hi, hipS
     prefold_blocks_kernel<Op, T, B, F, RANKED><<<grid, kFusedBlock, lds, s>>>(ptrs, n, rank_hi);
 }
 
+// reduce_no_order over any 17..128 peers in one kernel: the binomial rounds with compile-time operand indices
+// and a uniform runtime guard `t + span < m`, which is exactly the m-peer program's step list (the fused
+// kReduce program restricted to the steps whose right operand exists). Block b (m_b = min(16, P - 16 b)
+// peers) is reduced that way, then the ceil(P / 16) block values likewise: tree_blocked's bracketing,
+// ragged last block included.
+template <class Op, class T, int W, int N>
+__device__ __forceinline__ void binomial_reduce(Lanes<T, W>* v, int m) {
+#pragma unroll
+    for (int span = 1; span < N; span *= 2) {
+#pragma unroll
+        for (int t = 0; t + span < N; t += 2 * span)
+            if (t + span < m) v[t] = combine<Op, T, W>(v[t], v[t + span]);
+    }
+}
+
+template <class Op, class T, int W>
+__device__ __forceinline__ void reduce_any_group(const BlockedScanPtrs& ptrs, int P, size_t elem) {
+    using L = Lanes<T, W>;
+    constexpr int NB = kMaxOnePassScanBlocks;
+    const int nb = (P + BL - 1) / BL;
+    L bv[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        if (b < nb) {
+            const int m = P - b * BL < BL ? P - b * BL : BL;
+            L v[BL];
+#pragma unroll
+            for (int q = 0; q < BL; ++q)
+                if (q < m) v[q] = load_lanes<kFusedNT, T, W>(static_cast<const T*>(ptrs.in[b * BL + q]) + elem);
+            binomial_reduce<Op, T, W, BL>(v, m);
+            bv[b] = v[0];
+        }
+    }
+    binomial_reduce<Op, T, W, NB>(bv, nb);
+    store_lanes<kFusedNT, T, W>(static_cast<T*>(ptrs.out[0]) + elem, bv[0]);
+}
+
+template <class Op, class T>
+__global__ void __launch_bounds__(256) reduce_any_kernel(BlockedScanPtrs ptrs, int P, size_t n) {
+    constexpr int W = kVecLanes<T>;
+    const size_t nvec = n / W;
+    const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
+    for (size_t g = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x; g < nvec; g += stride)
+        reduce_any_group<Op, T, W>(ptrs, P, g * W);
+    const size_t first = nvec * W;
+    if (blockIdx.x == 0 && first + threadIdx.x < n) reduce_any_group<Op, T, 1>(ptrs, P, first + threadIdx.x);
+}
+
 }  // namespace
 
 bool tree_blocks_one_pass_covers(int op, int dtype, int alg, int P) {
+    if (alg == FMI_ALG_REDUCE) return P > sched::kMaxFusedPeers && P <= kMaxOnePassScanBlocks * BL;
     if (P % BL != 0) return false;
     const int B = P / BL;
     if (B < 2 || B > kMaxOnePassScanBlocks) return false;
@@ -140,15 +188,12 @@ int launch_tree_blocks_one_pass(int op, int dtype, int alg, int P, const Blocked
         return fail(FMI_ERR_INVALID, "one-pass blocked tree: unsupported (alg, P, op, dtype)");
     const int B = P / BL;
     return with_op_dtype<false>(op, dtype, [&]<class Op, class T>() -> int {
-        static constexpr TreeBlocksFn reduce_table[] = {
-            &tree_blocks_one<Op, T, sched::kReduce, 2>, &tree_blocks_one<Op, T, sched::kReduce, 3>,
-            &tree_blocks_one<Op, T, sched::kReduce, 4>, &tree_blocks_one<Op, T, sched::kReduce, 5>,
-            &tree_blocks_one<Op, T, sched::kReduce, 6>, &tree_blocks_one<Op, T, sched::kReduce, 7>,
-            &tree_blocks_one<Op, T, sched::kReduce, 8>};
-        static_assert(kMaxOnePassScanBlocks == 8, "tables cover B = 2..8");
+        static_assert(kMaxOnePassScanBlocks == 8, "allreduce covers B = 2, 4, 8");
         constexpr bool ranked = std::is_floating_point_v<T> && (std::is_same_v<Op, OpMax> || std::is_same_v<Op, OpMin>);
         if (alg == FMI_ALG_REDUCE) {
-            reduce_table[B - 2](ptrs, n, 0, s);
+            const size_t nvec = n / kVecLanes<T>;
+            const unsigned grid = static_cast<unsigned>(std::min<size_t>(grid_for(nvec, kFusedBlock), kFusedGridCap));
+            reduce_any_kernel<Op, T><<<grid, kFusedBlock, fused_lds_bytes(BL, kFusedBlock * 16), s>>>(ptrs, P, n);
         } else {
             switch (B) {
                 case 2: tree_blocks_one<Op, T, sched::kAllreduce, 2, ranked>(ptrs, n, rank, s); break;

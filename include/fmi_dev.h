@@ -259,7 +259,7 @@ typedef enum {
                                        resident per CU (an LDS reservation enforces it); 0 = no cap. Default 64
                                        (fewer concurrent HBM streams at large P) */
     FMI_TUNE_BLOCKS_ONE_PASS = 7 /* P-way programs beyond 31 peers in one pass over every input (default 1):
-                                    scan_no_order over 32..143 peers, reduce_no_order over 16 B peers (B <= 8),
+                                    scan_no_order over 32..143 peers, reduce_no_order over 17..128 peers,
                                     allreduce_no_order over 32 / 48 / 64 / 80 / 96 / 112 / 128
                                     peers, scan_ltr and
                                     reduce_ltr over 32..128 peers;

@@ -404,11 +404,12 @@ def test_one_pass_chain_matches_blocked_launches(device, P):
         fmi_amd.tune_set(Tune.BLOCKS_ONE_PASS, old)
 
 
-@pytest.mark.parametrize("P", [32, 48, 64, 80, 112, 128])
+@pytest.mark.parametrize("P", [17, 32, 33, 48, 64, 80, 100, 112, 128])
 def test_one_pass_blocked_tree_matches_blocked_launches(device, P):
-    """reduce over 16 B peers and allreduce over 32..128 peers (pre-fold of full blocks at 48, 80, 112): the
-    one-pass kernels (fmi_fused_tree_blocked.hip) and the blocked launches (FMI_TUNE_BLOCKS_ONE_PASS = 0) give the oracle's bits
-    for every op x core dtype, several roots / ranks, and in place (out = an input)."""
+    """reduce over 17..128 peers (ragged last blocks at 17, 33, 100) and allreduce over 32..128 peers (pre-fold of
+    full blocks at 48, 80, 112; other P take the launches): the one-pass kernels (fmi_fused_tree_blocked.hip) and
+    the blocked launches (FMI_TUNE_BLOCKS_ONE_PASS = 0) give the oracle's bits for every op x core dtype, several
+    roots / ranks, and in place (out = an input)."""
     n = 2 * 4096 + 3
     old = fmi_amd.tune_get(Tune.BLOCKS_ONE_PASS)
     try:
@@ -430,7 +431,7 @@ def test_one_pass_blocked_tree_matches_blocked_launches(device, P):
                     pow2 = 1 << (P.bit_length() - 1)
                     # float max / min: each rank keeps its own operand order; folded ranks >= 2^k get their
                     # partner's value
-                    for rank in sorted({0, 17, pow2 - 1, P - 1, min(pow2 + 3, P - 1)}):
+                    for rank in sorted(r for r in {0, 17, pow2 - 1, P - 1, min(pow2 + 3, P - 1)} if r < P):
                         fmi_amd.reduce_tree(op, Alg.ALLREDUCE, out, ins, rank=rank)
                         assert_bit_equal(out.numpy(), want_ar[rank], f"allreduce rank {rank} {what}")
                     acc = [dev(x) for x in xs[:1]] + ins[1:]  # in place: out is peer 0's bucket
