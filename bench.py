@@ -2,24 +2,34 @@
 """Benchmark of FMI's bucket reduction on MI355X (BASELINE.json metric:
 "GiB/s device-resident float32 sum-reduce, 256 MiB buckets, 1/2/4/8 GPU").
 
-One *step* = one pass of the hot path over one batch of synthetic, HBM-resident buckets: every GPU holds
-two peers' 256 MiB float32 buckets and performs the pairwise combine a = a + b — the reference's
-`f.f(a, b)` (include/Communicator.h:180-189) on the device (config C2). The combine is element-wise and
-pairs are independent, so at N > 1 the pairs shard over the GPUs with no data-path collective (weak
-scaling, 2N peers); only the barrier + max-over-ranks timing crosses GPUs.
-value = (N × 256 MiB of reduced bucket) / (wall time per step, max over ranks), in GiB/s.
+N = 1 (config C2). One *step* = one pairwise combine a = a + b of two 256 MiB float32 peer buckets
+resident in HBM — the reference's `f.f(a, b)` (include/Communicator.h:180-189) on the device, rotating over
+4 buffer sets (2 GiB, beyond the 256 MiB Infinity Cache). value = 256 MiB / (wall time per step).
+
+N > 1 (config C4's shape at the metric's bucket size). One *step* = the N-peer float32 sum-allreduce of
+256 MiB buckets, ONE FMI peer per GPU (one process per GPU), through the product C-ABI communicator
+fmi_comm_allreduce: all-to-all of N shards over RCCL/xGMI -> the fused N-way kernel in the reference's
+allreduce_no_order order (src/comm/PeerToPeer.cpp:96-130) on every GPU's shard -> all-gather (path TREE,
+bit-identical to the reference's N-peer allreduce). value = N x 256 MiB / (wall time per step, max over
+ranks): reduced bucket bytes delivered per second, summed over the GPUs (weak scaling: 256 MiB per GPU).
+The result of the last timed step is checked on every rank against the single-GPU fused kernel over the same
+synthetic buckets rebuilt locally (`self_check`); a mismatch prints the line and exits 1.
 
 Also reported (one JSON line on rank 0):
-  roofline      — the pairwise kernel: algorithmic bytes 3·n·4 per launch ÷ its mean duration from HIP
-                  events on the stream it runs on; peak = 8000 GB/s HBM3E; traffic from the committed
-                  rocprofv3 PMC summary of the same kernel (profiles/).
-  cpu_baseline  — (N = 1) oracle/cpu_baseline (a C++ port of the reference's CPU path) on this host: the
-                  reference-faithful 6-copy adapter around std::transform, 1 thread, same 256 MiB buckets.
-  config.allreduce, xgmi_roofline — (N > 1) the path with a real exchange step, measured after `value`:
-                  the 2N-peer allreduce of 256 MiB buckets (config C4's shape) — local pairwise round, then
-                  all-to-all of shards over RCCL/xGMI + the fused P-way kernel in allreduce_no_order order +
-                  all-gather (fmi_amd/collectives.py), bit-identical to the reference's 2N-peer allreduce;
-                  its step time, and its egress bytes per GPU against the N-1 xGMI links' peak.
+  roofline      — the dominant HBM kernel: N = 1 the pairwise kernel (3·n·4 bytes per launch), N > 1 the
+                  fused N-way shard kernel ((N+1)·shard·4 bytes), duration from HIP events on the library
+                  stream it runs on; peak = 8000 GB/s HBM3E; traffic from the committed rocprofv3 PMC summary.
+  xgmi_roofline — (N > 1) egress bytes per GPU per step, 2·(N−1)/N·S, over the step time, against the N−1
+                  xGMI links' peak.
+  c4            — (N > 1) config C4 itself: N peers × 1 GiB f32, paths TREE and RCCL, algbw / busbw, each
+                  self-checked (TREE bit-exact, RCCL within (N−1)·2^-24·Σ|x|).
+  c5            — config C5: the 1 GiB page-locked host bucket through fmi_comm_allreduce_host (H2D +
+                  allreduce + D2H pipelined), N = 1 one rank, N > 1 every rank.
+  cpu_baseline  — (N = 1) oracle/cpu_baseline (a C++ port of the reference's CPU path) on this host.
+  diagnostics   — (N > 1) the replicated-pair rate (C2 on every GPU, no exchange), the per-phase breakdown
+                  of the exchange and, opt-in, path DIRECT.
+Everything after `value` runs under a per-rank deadline (--diag-deadline); if it expires, rank 0 prints the
+line with a top-level "incomplete" field and every rank exits.
 """
 from __future__ import annotations
 
@@ -47,24 +57,25 @@ def parse():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--bucket-mib", type=int, default=256)
+    ap.add_argument("--c4-mib", type=int, default=1024, help="N>1: bucket per peer of the c4 block (config C4)")
     ap.add_argument("--sets", type=int, default=4, help="rotating bucket sets (defeats the 256 MiB MALL)")
     ap.add_argument("--path", default="tree", choices=["tree", "rccl", "direct"],
-                    help="N>1 exchange: tree = all-to-all + fused kernel (bit-exact), rccl = reduce-scatter, "
-                         "direct = fused kernel over IPC-mapped peer windows (bit-exact, fmi backend only)")
-    ap.add_argument("--backend", default="fmi", choices=["fmi", "torch"],
-                    help="N>1 exchange driver: fmi = the C-ABI communicator fmi_comm_* (RCCL transport), "
-                         "torch = torch.distributed collectives + our kernels on torch's stream")
-    ap.add_argument("--overlap-steps", action="store_true",
-                    help="N>1, fmi backend: run step k+1's local round on a second stream during step k's exchange")
+                    help="N>1 headline exchange: tree = all-to-all + fused kernel (bit-exact), rccl = "
+                         "reduce-scatter + all-gather, direct = fused kernel over IPC-mapped peer windows")
+    ap.add_argument("--transport", default="rccl", choices=["rccl", "proc"],
+                    help="N>1: rccl = one process per GPU over RCCL/xGMI (torch backend nccl); proc = processes "
+                         "of one node sharing GPUs through shared-memory staging (torch backend gloo) — runs this "
+                         "exact N>1 code with several ranks on one GPU (tests)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-diagnostics", action="store_true", help="skip the untimed N>1 phase breakdown")
+    ap.add_argument("--no-c5", action="store_true", help="skip the host-bucket (C5) measurement")
+    ap.add_argument("--c5-mib", type=int, default=1024, help="host bucket per rank of the c5 block (config C5)")
+    ap.add_argument("--no-diagnostics", action="store_true", help="N>1: skip the untimed diagnostics")
     ap.add_argument("--diag-deadline", type=float, default=240.0,
-                    help="seconds the N>1 allreduce measurement + diagnostics (run after `value`) may take before "
-                         "the line is printed without the rest of them")
-    ap.add_argument("--diag-direct", action="store_true",
-                    help="N>1 diagnostics: also check and time path DIRECT (IPC-mapped peer windows)")
+                    help="seconds everything after `value` (c4, c5, diagnostics) may take before the line is "
+                         "printed without the rest of it")
+    ap.add_argument("--diag-direct", action="store_true", help="N>1 diagnostics: also check and time path DIRECT")
     ap.add_argument("--force-dist", action="store_true",
-                    help="run the N>1 code path (RCCL exchange) even at world size 1 — plumbing check only")
+                    help="run the N>1 code path (fmi_comm over RCCL) even at world size 1 — plumbing check")
     ap.add_argument("--cpu-reps", type=int, default=30, help="adapter combines timed (≈10 s of CPU work)")
     return ap.parse_args()
 
@@ -141,149 +152,9 @@ def c1_host():
         return {"error": str(e)}
 
 
-def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        if args.gpus > 1 and world == 1:
-            raise SystemExit(f"--gpus {args.gpus} needs torch.distributed.run with {args.gpus} processes")
-        args.gpus = world
-
-    import numpy as np
-
-    dist = None
-    use_dist = world > 1 or args.force_dist
-    if use_dist:
-        # torch first: libfmi_dev.so then binds to the HIP runtime torch already loaded (one runtime
-        # per process, shared streams/pointers with RCCL) — see DESIGN.md §Runtime.
-        import torch
-        import torch.distributed as dist
-
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-
-    import fmi_amd
-    from fmi_amd import Bucket, Event, Op
-
-    fmi_amd.init(local_rank)
-    n = args.bucket_mib * MIB // 4
-    nbytes = n * 4
-
-    # ---- the timed measurement: every rank combines its own peer pairs (C2's unit of work) -------------
-    sets = [tuple(Bucket(n, np.float32).fill_synthetic(42 + s, 2 * rank + j) for j in range(2))
-            for s in range(args.sets)]
-    fmi_amd.sync()
-
-    def step(k):
-        a, b = sets[k % len(sets)]
-        fmi_amd.reduce_pair(Op.SUM, a, b)
-
-    def bracket():  # barrier + device sync (both sides of the timed region)
-        fmi_amd.sync()
-        if dist is not None:
-            dist.barrier()
-            torch.cuda.synchronize()
-
-    for k in range(args.warmup):
-        step(k)
-    bracket()
-    # Timed region: exactly K back-to-back launches on the library stream; two HIP events on that stream
-    # bracket them (no markers between launches).
-    ev0, ev1 = Event(), Event()
-    t0 = time.perf_counter()
-    ev0.record()
-    for k in range(args.steps):
-        step(k)
-    ev1.record()
-    bracket()
-    t1 = time.perf_counter()
-    step_ms = (t1 - t0) * 1e3 / args.steps
-    # mean launch duration over the timed region (includes the ~1-2 us dispatch gaps between launches)
-    kernel_avg_ms = ev0.elapsed_ms(ev1) / args.steps
-    if dist is not None:  # max over ranks
-        step_ms, kernel_avg_ms = _max_over_ranks(dist, step_ms, kernel_avg_ms)
-    # diagnostic, untimed: per-launch event pairs give the launch duration without the gaps
-    probe = min(args.steps, 32)
-    pairs = [(Event(), Event()) for _ in range(probe)]
-    for k in range(probe):
-        pairs[k][0].record()
-        step(k)
-        pairs[k][1].record()
-    fmi_amd.sync()
-    isolated_us = 1e3 * sum(a.elapsed_ms(b) for a, b in pairs) / probe
-    for a, b in sets:
-        a.free()
-        b.free()
-    dominant = "pair_tile"
-    algo_bytes = 3 * nbytes
-    if world == 1:
-        workload = "C2: 1-GPU pairwise float32 sum-reduce of two 256 MiB device-resident peer buckets"
-        parallelism = "single GPU (2 peers resident)"
-    else:
-        workload = (f"C2 on every GPU: {world} GPUs each combine their own pair of 256 MiB device-resident "
-                    f"peer buckets ({2 * world} peers)")
-        parallelism = f"dp{world}: pairs sharded over GPUs, no data-path collective (barrier + max-over-ranks timing)"
-    roofline_extra = {"kernel_avg_us_isolated": round(isolated_us, 2),
-                      "kernel_avg_source": "HIP events bracketing the K timed launches on the library stream"
-                                           + (", max over ranks" if dist is not None else "")}
-    value = args.gpus * (nbytes / GIB) / (step_ms * 1e-3)
-    achieved = algo_bytes / (kernel_avg_ms * 1e-3) / 1e9
-    traffic, traffic_src = pmc_traffic(dominant)
-    line = {
-        "metric": METRIC,
-        "value": round(value, 2),
-        "unit": "GiB/s",
-        "n_gpus": args.gpus,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(step_ms, 5),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "f32",
-        "data": "synthetic (splitmix64 counter generator, SURVEY.md §8d), device-resident in HBM",
-        "config": {"workload": workload, "bucket_mib": args.bucket_mib, "elements": n,
-                   "peers": 2 * args.gpus, "parallelism": parallelism, "rotating_sets": args.sets},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "kernel": dominant, "kernel_avg_us": round(kernel_avg_ms * 1e3, 2),
-                     "algorithmic_bytes_per_launch": algo_bytes,
-                     "traffic_source": traffic_src},
-    }
-    line["roofline"].update(roofline_extra)
-    if rank == 0 and not use_dist and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(args)
-    emit = _Emitter(line, rank)
-    watchdog = None
-    if use_dist:
-        # The timed measurement is complete and `line` holds it. The sharded allreduce and the diagnostics
-        # below run other paths; a per-rank deadline (kept until teardown is done, since a rank that failed
-        # alone would leave its peers waiting in a collective) guarantees that a hang there cannot cost
-        # the measured line.
-        state = line["config"]["allreduce"] = {}
-        watchdog = threading.Timer(args.diag_deadline, emit.deadline, args=(state,))
-        watchdog.daemon = True
-        watchdog.start()
-        try:
-            ar = measure_allreduce(args, n, world, dist, line, state)
-            if not args.no_diagnostics:
-                state["diagnostics"] = {}
-                run_diagnostics(args, ar, n, dist, state["diagnostics"])
-        except Exception as e:  # never fails the measured line
-            state["failed"] = f"{type(e).__name__}: {e}"
-    emit.emit()
-    if dist is not None:
-        dist.barrier()
-        dist.destroy_process_group()
-    if watchdog is not None:
-        watchdog.cancel()
-
-
 class _Emitter:
-    """Prints the one JSON line exactly once (rank 0), from the main thread or from the diagnostics
-    deadline — whichever comes first."""
+    """Prints the one JSON line exactly once (rank 0), from the main thread or from the deadline —
+    whichever comes first."""
 
     def __init__(self, line, rank):
         self.line, self.rank = line, rank
@@ -299,122 +170,315 @@ class _Emitter:
                 try:
                     text = json.dumps(self.line)
                 except RuntimeError:  # the main thread was still writing the after-`value` section
-                    self.line["config"]["allreduce"] = {"incomplete": "deadline reached while recording"}
+                    self.line = {k: v for k, v in self.line.items() if k in _HEADLINE_KEYS}
+                    self.line["incomplete"] = "deadline reached while recording the after-value section"
                     text = json.dumps(self.line)
                 print(text, flush=True)
 
     def deadline(self, state):
-        state["incomplete"] = "deadline reached; the timed measurement (value, roofline) is unaffected"
+        msg = "deadline reached; the timed measurement (value, roofline, self_check) is unaffected"
+        state["incomplete"] = msg
+        self.line["incomplete"] = msg
         self.emit()
-        print("bench: diagnostics deadline reached, exiting", file=sys.stderr, flush=True)
+        print("bench: deadline reached, exiting", file=sys.stderr, flush=True)
         os._exit(0)
 
 
-def _max_over_ranks(dist, *vals):
-    import torch
-
-    t = torch.tensor(vals, dtype=torch.float64, device=torch.cuda.current_device())
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return [float(v) for v in t.tolist()]
+_HEADLINE_KEYS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+                  "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "xgmi_roofline", "self_check",
+                  "cpu_baseline")
 
 
-def measure_allreduce(args, n, world, dist, line, state):
-    """Config C4's shape at this node size: the 2N-peer float32 sum-allreduce of 256 MiB buckets, two peers
-    per GPU (the local pairwise round, then the exchange over xGMI: all-to-all of shards + fused kernel in
-    allreduce_no_order order + all-gather, bit-exact with the reference's 2N-peer bracketing). K steps,
-    barrier + sync on both sides, max over ranks. Reported beside `value`, with its xGMI roofline: per step
-    every GPU sends (N-1)/N of its bucket in the all-to-all (or reduce-scatter) and (N-1)/N in the
-    all-gather over its N-1 direct links to the other GPUs (fully connected node)."""
-    from fmi_amd.collectives import CommAllreduce, ShardedAllreduce
-
-    ar = None
-    backend = args.backend
-    if backend == "fmi":
-        try:  # the product C-ABI communicator (fmi_comm_*, RCCL transport)
-            ar = CommAllreduce(dist.group.WORLD, path=args.path)
-        except Exception as e:  # setup only: every rank fails alike, before any timed work
-            print(f"fmi_comm setup failed ({e}); using the torch.distributed exchange", file=sys.stderr)
-            backend = "torch"
-    if ar is None:
-        ar = ShardedAllreduce(dist.group.WORLD, path=args.path, force_exchange=args.force_dist)
-    if isinstance(ar, CommAllreduce):
-        step_ms, kernel_ms, extra = ar.bench(n, steps=args.steps, warmup=args.warmup, sets=args.sets,
-                                             overlap=args.overlap_steps)
-    else:
-        step_ms, kernel_ms, extra = ar.bench(n, steps=args.steps, warmup=args.warmup, sets=args.sets)
-    extra.pop("kernel_algo_bytes", None)
-    state.update({
-        "workload": f"C4-shaped: {2 * world}-peer float32 sum-allreduce of 256 MiB buckets, 2 peers per GPU",
-        "path": {"tree": "all-to-all + fused tree kernel + all-gather over RCCL (bit-exact)",
-                 "rccl": "RCCL reduce-scatter + all-gather",
-                 "direct": "fused tree over IPC-mapped peer windows + direct gather (bit-exact)"}[args.path],
-        "backend": backend,
+def _headline(args, value, step_ms, workload, parallelism, n, roofline):
+    return {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "GiB/s",
+        "n_gpus": args.gpus,
+        "steps": args.steps,
+        "warmup": args.warmup,
         "ms_per_step": round(step_ms, 5),
-        "GiB_s_reduced_buckets": round(world * (n * 4 / GIB) / (step_ms * 1e-3), 2),
-        "local_pair_kernel_ms": round(sum(kernel_ms) / len(kernel_ms), 5),
-    })
-    state.update(extra)
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (splitmix64 counter generator, SURVEY.md §8d), device-resident in HBM",
+        "config": {"workload": workload, "bucket_mib": args.bucket_mib, "elements": n, "parallelism": parallelism,
+                   "rotating_sets": args.sets},
+        "roofline": roofline,
+    }
+
+
+def _roofline(kernel, algo_bytes, kernel_avg_ms, source, extra=None):
+    achieved = algo_bytes / (kernel_avg_ms * 1e-3) / 1e9
+    traffic, traffic_src = pmc_traffic(kernel)
+    r = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kernel,
+         "kernel_avg_us": round(kernel_avg_ms * 1e3, 2), "algorithmic_bytes_per_launch": algo_bytes,
+         "kernel_avg_source": source, "traffic_source": traffic_src}
+    r.update(extra or {})
+    return r
+
+
+# ------------------------------------------------------------------------------------------------------
+# N = 1: config C2
+# ------------------------------------------------------------------------------------------------------
+def run_single(args):
+    import numpy as np
+
+    import fmi_amd
+    from fmi_amd import Bucket, Event, Op
+
+    fmi_amd.init(0)
+    n = args.bucket_mib * MIB // 4
+    nbytes = n * 4
+    sets = [tuple(Bucket(n, np.float32).fill_synthetic(42 + s, j) for j in range(2)) for s in range(args.sets)]
+    fmi_amd.sync()
+
+    def step(k):
+        a, b = sets[k % len(sets)]
+        fmi_amd.reduce_pair(Op.SUM, a, b)
+
+    for k in range(args.warmup):
+        step(k)
+    fmi_amd.sync()
+    # Timed region: exactly K back-to-back launches on the library stream; two HIP events on that stream
+    # bracket them (no markers between launches).
+    ev0, ev1 = Event(), Event()
+    t0 = time.perf_counter()
+    ev0.record()
+    for k in range(args.steps):
+        step(k)
+    ev1.record()
+    fmi_amd.sync()
+    t1 = time.perf_counter()
+    step_ms = (t1 - t0) * 1e3 / args.steps
+    kernel_avg_ms = ev0.elapsed_ms(ev1) / args.steps  # includes the ~1-2 us dispatch gaps between launches
+    # diagnostic, untimed: per-launch event pairs give the launch duration without the gaps
+    probe = min(args.steps, 32)
+    pairs = [(Event(), Event()) for _ in range(probe)]
+    for k in range(probe):
+        pairs[k][0].record()
+        step(k)
+        pairs[k][1].record()
+    fmi_amd.sync()
+    isolated_us = 1e3 * sum(a.elapsed_ms(b) for a, b in pairs) / probe
+    for a, b in sets:
+        a.free()
+        b.free()
+    roof = _roofline("pair_tile", 3 * nbytes, kernel_avg_ms,
+                     "HIP events bracketing the K timed launches on the library stream",
+                     {"kernel_avg_us_isolated": round(isolated_us, 2)})
+    line = _headline(args, (nbytes / GIB) / (step_ms * 1e-3), step_ms,
+                     "C2: 1-GPU pairwise float32 sum-reduce of two 256 MiB device-resident peer buckets",
+                     "single GPU (2 peers resident)", n, roof)
+    line["config"]["peers"] = 2
+    if not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(args)
+    if not args.no_c5:
+        try:
+            line["c5"] = c5_single(args.c5_mib)
+        except Exception as e:  # reported, never fails the measured line
+            line["c5"] = f"failed: {type(e).__name__}: {e}"
+    print(json.dumps(line), flush=True)
+
+
+def c5_single(mib: int, iters: int = 3) -> dict:
+    """Config C5 at N = 1: a `mib` (1 GiB) f32 bucket in page-locked host memory (a channel recv buffer) through
+    fmi_comm_allreduce_host on a one-rank communicator — H2D, the (one-peer) allreduce and D2H pipelined in
+    64 MiB chunks. Median wall time of `iters` after one warm-up; the result must equal the input bit for
+    bit (a one-peer allreduce is a copy, reference PeerToPeer.cpp:96-130 with P = 1)."""
+    import statistics
+
+    import numpy as np
+
+    from fmi_amd import Op, PinnedArray
+    from fmi_amd.comm import Comm, Transport, unique_id
+
+    n = mib * MIB // 4
+    comm = Comm(unique_id(Transport.LOCAL), 1, 0)
+    send, recv = PinnedArray(n, np.float32), PinnedArray(n, np.float32)
+    try:
+        send.array[:] = np.random.default_rng(5).random(n, dtype=np.float32)
+        times = []
+        for k in range(iters + 1):
+            recv.array[:1] = np.float32(-1.0)
+            t0 = time.perf_counter()
+            comm.allreduce_host(Op.SUM, send.array, recv.array, chunk=64 * MIB // 4)
+            if k:
+                times.append(time.perf_counter() - t0)
+        ok = bool(np.array_equal(send.array.view(np.uint32), recv.array.view(np.uint32)))
+    finally:
+        send.free()
+        recv.free()
+        comm.destroy()
+    ms = statistics.median(times) * 1e3
+    return {"workload": f"C5 at N = 1: {mib} MiB f32 page-locked host bucket, H2D + allreduce + D2H, 64 MiB chunks",
+            "ms": round(ms, 3), "host_bucket_GiB_s": round(n * 4 / GIB / (ms * 1e-3), 2),
+            "pcie_GB_s_both_directions": round(2 * n * 4 / (ms * 1e-3) / 1e9, 1), "result_bit_exact": ok,
+            "iters": iters}
+
+
+# ------------------------------------------------------------------------------------------------------
+# N > 1: the sharded allreduce, one peer per GPU
+# ------------------------------------------------------------------------------------------------------
+def run_dist(args, world, rank, local_rank):
+    # torch first: libfmi_dev.so then binds to the HIP runtime torch already loaded (one runtime per process,
+    # shared streams/pointers with RCCL) — see DESIGN.md §Runtime.
+    import torch
+    import torch.distributed as dist
+
+    proc = args.transport == "proc"
+    dev = local_rank % max(1, torch.cuda.device_count()) if proc else local_rank
+    torch.cuda.set_device(dev)
+    if proc:
+        dist.init_process_group("gloo")
+    else:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+
+    import fmi_amd
+    from fmi_amd.collectives import CommAllreduce
+
+    fmi_amd.init(dev)
+    ar = CommAllreduce(dist.group.WORLD, path=args.path, transport=args.transport)
+    n = args.bucket_mib * MIB // 4
+    S = n * 4
+    step_ms, _, extra = ar.bench(n, steps=args.steps, warmup=args.warmup, sets=args.sets, peers_per_gpu=1)
+    out, seed = extra.pop("result")
+    value = world * (S / GIB) / (step_ms * 1e-3)
+    check = ar.self_check(out, n, seed, tolerance=args.path == "rccl")
+    out.free()
+    kern = ar.shard_kernel(n, launches=max(10, min(args.steps, 50)))
+    roof = _roofline("tree_kernel", kern["algorithmic_bytes_per_launch"], kern["kernel_avg_us"] * 1e-3,
+                     "HIP events around back-to-back launches of the same fused shard kernel on the library "
+                     "stream, right after the timed region (rotating shard sets), max over ranks",
+                     {"launch_shape": kern["kernel"],
+                      "note": "the allreduce step is xGMI-bound (xgmi_roofline); this is its HBM-bound kernel"})
+    path_desc = {"tree": "all-to-all + fused tree kernel + all-gather (bit-exact)",
+                 "rccl": "RCCL reduce-scatter + all-gather", "direct": "fused tree over IPC-mapped peer windows"}
+    line = _headline(args, value, step_ms,
+                     f"C4-shaped at the metric's bucket size: {world}-peer float32 sum-allreduce, one FMI peer "
+                     f"(a {args.bucket_mib} MiB device-resident bucket) per GPU, through fmi_comm_allreduce",
+                     f"{world} GPUs, one peer per GPU, buckets sharded {world} ways; path {args.path}: "
+                     f"{path_desc[args.path]}; transport {args.transport}", n, roof)
+    line["config"].update({"peers": world, "path": args.path, "transport": args.transport,
+                           "algbw_GiB_s": extra["algbw_GiB_s"], "busbw_GiB_s": extra["busbw_GiB_s"],
+                           "shard_elems": extra["shard_elems"]})
+    line["self_check"] = check
     if world > 1:
-        egress = 2 * (world - 1) * n * 4 / world
+        egress = 2 * (world - 1) * S / world
         xg = egress / (step_ms * 1e-3) / 1e9
         xpeak = (world - 1) * XGMI_LINK_GBS_PER_DIR
         line["xgmi_roofline"] = {"bound": "xgmi", "achieved": round(xg, 1), "peak": round(xpeak, 1), "unit": "GB/s",
                                  "frac": round(xg / xpeak, 4), "bytes_per_step_per_gpu": int(egress),
-                                 "kernel": "sharded allreduce step (config.allreduce)",
-                                 "note": "egress bytes per GPU / allreduce step time (local round included); "
-                                         "peak = N-1 links x 76.8 GB/s per direction"}
-    return ar
-
-
-def run_diagnostics(args, ar, n, dist, diag):
-    """Untimed N>1 diagnostics for the next optimisation round, each max over ranks: the other exchange
-    path's step time, the per-phase breakdown, the other step schedule, config C5 (host-resident buckets)
-    and, last and only with --diag-direct, path DIRECT (xGMI reads of IPC-mapped peer windows). Results are
-    written into `diag` as they complete."""
-    from fmi_amd.collectives import CommAllreduce, phase_breakdown
-
-    other = "rccl" if args.path == "tree" else "tree"
-    short = dict(steps=max(10, args.steps // 4), warmup=3, sets=min(2, args.sets))
-    if isinstance(ar, CommAllreduce):
-        from fmi_amd.comm import Path
-
-        saved = ar._path
-        ar._path = Path.RCCL if other == "rccl" else Path.TREE
-        alt_ms, _, _ = ar.bench(n, **short)
-        ar._path = saved
-    else:
-        saved = ar.path
-        ar.path = other
-        alt_ms, _, _ = ar.bench(n, **short)
-        ar.path = saved
-    diag[f"ms_per_step_path_{other}"] = round(alt_ms, 5)
-    diag["phase_ms"] = phase_breakdown(n, dist.group.WORLD)
-    if not isinstance(ar, CommAllreduce):
-        return
-    # the other step schedule: local round of step k+1 overlapped with step k's exchange, or not
-    ov_ms, _, _ = ar.bench(n, steps=short["steps"], warmup=3, sets=args.sets, overlap=not args.overlap_steps)
-    diag["ms_per_step_no_overlap" if args.overlap_steps else "ms_per_step_overlap_steps"] = round(ov_ms, 5)
-    # config C5: 1 GiB host (pinned) bucket per rank, H2D + allreduce + D2H pipelined
+                                 "note": "egress bytes per GPU (all-to-all + all-gather, (N-1)/N of the bucket "
+                                         "each) / step time; peak = N-1 links x 76.8 GB/s per direction"
+                                         + ("; PROC transport stages through host memory" if proc else "")}
+    emit = _Emitter(line, rank)
+    state = {}
+    watchdog = threading.Timer(args.diag_deadline, emit.deadline, args=(state,))
+    watchdog.daemon = True
+    watchdog.start()
     try:
-        diag["c5_host_allreduce_1GiB"] = ar.host_bench(GIB // 4)
-    except Exception as e:  # diagnostic only; never fails the bench line
-        diag["c5_host_allreduce_1GiB"] = f"failed: {e}"
-    # path DIRECT: bit-identical to TREE on this node? and its step time. Opt-in (--diag-direct): its
-    # cross-process IPC mappings have only run on the LOCAL transport so far, and a fault there would take
-    # the whole line with it.
-    if not args.diag_direct:
-        diag["path_direct"] = "not run (opt-in: --diag-direct)"
-    elif args.path != "direct":
-        saved = ar._path
+        after_value(args, ar, world, dist, line, proc)
+    except Exception as e:  # never fails the measured line
+        line["after_value_failed"] = f"{type(e).__name__}: {e}"
+    emit.emit()
+    ar.destroy()
+    dist.barrier()
+    dist.destroy_process_group()
+    watchdog.cancel()
+    if not check["ok"]:
+        print("bench: self-check FAILED: the sharded allreduce differs from the single-GPU kernel", file=sys.stderr,
+              flush=True)
+        sys.exit(1)
+
+
+def after_value(args, ar, world, dist, line, proc):
+    """Config C4 at its own size, config C5, then the diagnostics — each max over ranks, recorded into
+    `line` as it completes (a deadline prints whatever is there)."""
+    n4 = args.c4_mib * MIB // 4
+    steps4, warm4 = max(5, args.steps // 10), 2
+    c4 = line["c4"] = {"workload": f"C4: {world} peers x {args.c4_mib} MiB f32 sum-allreduce, one peer per GPU",
+                       "elements": n4, "steps": steps4, "warmup": warm4, "rotating_sets": 2}
+    for path in ("tree", "rccl"):
+        if proc and path == "rccl":
+            c4[path] = "not run (path RCCL needs the RCCL transport)"
+            continue
+        ms, _, ex = ar.bench(n4, steps=steps4, warmup=warm4, sets=2, peers_per_gpu=1, seed=1000, path=path)
+        out, seed = ex.pop("result")
+        chk = ar.self_check(out, n4, seed, tolerance=path == "rccl")
+        out.free()
+        c4[path] = {"ms_per_step": round(ms, 4), "algbw_GiB_s": ex["algbw_GiB_s"], "busbw_GiB_s": ex["busbw_GiB_s"],
+                    "GiB_s_reduced_buckets": round(world * (n4 * 4 / GIB) / (ms * 1e-3), 2), "self_check": chk}
+        if not chk["ok"]:
+            line["self_check"] = dict(line["self_check"], ok=False, failed_in=f"c4 path {path}")
+    if not args.no_c5:
+        line["c5"] = dict(ar.host_bench(args.c5_mib * MIB // 4),
+                          workload=f"C5: {args.c5_mib} MiB f32 page-locked host bucket per rank, H2D + sharded "
+                                   f"allreduce + D2H pipelined")
+    if args.no_diagnostics:
+        return
+    diag = line["diagnostics"] = {}
+    diag["replicated_pairs"] = replicated_pairs(args, ar)
+    if not proc:
+        from fmi_amd.collectives import phase_breakdown
+
+        diag["phase_ms"] = phase_breakdown(args.bucket_mib * MIB // 4, dist.group.WORLD)
+    if args.diag_direct:
         try:
             ok = ar.check_direct(1 << 20)
-            ar._path = Path.DIRECT
-            d_ms, _, _ = ar.bench(n, **short)
-            diag["path_direct"] = {"bit_identical_to_tree": ok, "ms_per_step": round(d_ms, 5)}
+            ms, _, _ = ar.bench(args.bucket_mib * MIB // 4, steps=max(10, args.steps // 4), warmup=3, sets=2,
+                                path="direct")
+            diag["path_direct"] = {"bit_identical_to_tree": ok, "ms_per_step": round(ms, 5)}
         except Exception as e:  # window setup fails on every rank alike (all-or-nothing)
             diag["path_direct"] = f"unavailable: {e}"
-        finally:
-            ar._path = saved
+    else:
+        diag["path_direct"] = "not run (opt-in: --diag-direct)"
+
+
+def replicated_pairs(args, ar) -> dict:
+    """C2 on every GPU at once (each combines its own pair of 256 MiB buckets, no data-path collective):
+    what round 1 reported as value at N > 1. Max over ranks."""
+    import numpy as np
+
+    import fmi_amd
+    from fmi_amd import Bucket, Event, Op
+
+    n = args.bucket_mib * MIB // 4
+    sets = [tuple(Bucket(n, np.float32).fill_synthetic(42 + s, 2 * ar.rank + j) for j in range(2))
+            for s in range(args.sets)]
+    steps = max(20, args.steps // 4)
+    for k in range(5):
+        fmi_amd.reduce_pair(Op.SUM, *sets[k % len(sets)])
+    fmi_amd.sync()
+    e0, e1 = Event(), Event()
+    e0.record()
+    for k in range(steps):
+        fmi_amd.reduce_pair(Op.SUM, *sets[k % len(sets)])
+    e1.record()
+    e1.sync()
+    ms = ar.max_over_ranks(e0.elapsed_ms(e1) / steps)[0]
+    for a, b in sets:
+        a.free()
+        b.free()
+    return {"ms_per_step": round(ms, 5), "GiB_s_all_gpus": round(ar.world * (n * 4 / GIB) / (ms * 1e-3), 2),
+            "steps": steps}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if args.gpus > 1 and world == 1:
+            raise SystemExit(f"--gpus {args.gpus} needs torch.distributed.run with {args.gpus} processes")
+        args.gpus = world
+    if world > 1 or args.force_dist:
+        run_dist(args, world, rank, local_rank)
+    else:
+        run_single(args)
 
 
 if __name__ == "__main__":

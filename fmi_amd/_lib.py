@@ -95,6 +95,7 @@ SIGNATURES = {
     "fmi_comm_recv": (_i, [_vp, _vp, _sz, _i, _vp]),
     "fmi_comm_barrier": (_i, [_vp, _vp]),
     "fmi_dev_fill_synthetic": (_i, [_i, _vp, _sz, _c.c_uint64, _c.c_uint32, _vp]),
+    "fmi_dev_fill_synthetic_at": (_i, [_i, _vp, _sz, _c.c_uint64, _c.c_uint32, _c.c_uint64, _vp]),
     "fmi_schedule_expr": (_i, [_i, _i, _i, _c.c_char_p, _sz]),
     "fmi_tune_set": (_i, [_i, _c.c_longlong]),
     "fmi_tune_get": (_i, [_i, _c.POINTER(_c.c_longlong)]),

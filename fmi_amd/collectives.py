@@ -24,7 +24,7 @@ RCCL and our kernels share one runtime, one set of streams and one address space
 """
 from __future__ import annotations
 
-from typing import List, Sequence
+from typing import List, Optional, Sequence
 
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
@@ -119,8 +119,14 @@ class ShardedAllreduce:
                 raise RuntimeError("Dimensions of send and receive data must match")
         if out.numel() != n:
             raise RuntimeError("Dimensions of send and receive data must match")
-        for b in buckets[1:]:  # local rounds of recursive doubling
-            self.engine.reduce_pair(op, x, b)
+        L = len(buckets)
+        if L & (L - 1):
+            # recursive doubling pairs the local peers among themselves only for a power-of-two count
+            raise ValueError(f"{L} local peer buckets: a GPU must host a power-of-two number of peers")
+        if L == 2:  # local round 0 of recursive doubling: pairs (2g, 2g+1)
+            self.engine.reduce_pair(op, x, buckets[1])
+        elif L > 2:  # local rounds 0..k-1: the 2^k-peer allreduce program over this GPU's peers
+            self.engine.reduce_tree(op, Alg.ALLREDUCE, x, buckets, rank=0)
         N = self.world
         if N == 1 and not self.force_exchange:
             out.copy_(x)
@@ -224,13 +230,17 @@ class ShardedAllreduce:
 
 
 class CommAllreduce:
-    """The same 2-peers-per-GPU sharded allreduce through the product C-ABI (fmi_comm_*, RCCL transport):
-    pairwise kernel for the local round, then fmi_comm_allreduce (all-to-all of shards + fused kernel in
-    the reference's order + all-gather, or RCCL reduce-scatter + all-gather) — everything on the
-    library's stream. torch.distributed only bootstraps: it broadcasts the 128-byte communicator id and
-    provides the bracketing barriers of the timed region."""
+    """The sharded allreduce through the product C-ABI (fmi_comm_*): one FMI peer per GPU (or 2^k peers,
+    folded by a local round first), then fmi_comm_allreduce — all-to-all of shards + the fused kernel in
+    the reference's order + all-gather (path TREE), RCCL reduce-scatter + all-gather (path RCCL), or the
+    fused kernel over IPC-mapped peer windows (path DIRECT) — everything on the library's stream.
 
-    def __init__(self, group=None, path: str = "tree"):
+    torch.distributed only bootstraps: it broadcasts the 128-byte communicator id and provides the barriers
+    and max-over-ranks of the timed region. `transport`: "rccl" (one process per GPU, torch's backend
+    "nccl") or "proc" (processes of one node on the same or different GPUs, data staged through
+    shared memory; with the "gloo" backend this runs the exact bench.py N>1 code on a single GPU)."""
+
+    def __init__(self, group=None, path: str = "tree", transport: str = "rccl"):
         from .comm import Comm, Path, Transport, unique_id
 
         self.group = group if group is not None else dist.group.WORLD
@@ -238,17 +248,38 @@ class CommAllreduce:
         self.rank = dist.get_rank(self.group)
         self.path = path
         self._path = {"tree": Path.TREE, "rccl": Path.RCCL, "direct": Path.DIRECT}[path]
+        self.transport = transport
+        tr = {"rccl": Transport.RCCL, "proc": Transport.PROC}[transport]
+        # max-over-ranks and flags travel on the process group's own device: GPU for nccl, host for gloo
+        self._red_dev = (torch.device("cuda", torch.cuda.current_device())
+                         if dist.get_backend(self.group) == "nccl" else torch.device("cpu"))
         _lib.load()
         _lib.call("fmi_dev_init", torch.cuda.current_device())
-        box = [unique_id(Transport.RCCL) if self.rank == 0 else None]
+        box = [unique_id(tr) if self.rank == 0 else None]
         dist.broadcast_object_list(box, src=0, group=self.group)
         self.comm = Comm(box[0], self.world, self.rank)
 
-    def bench(self, n: int, steps: int, warmup: int, sets: int = 2, peers_per_gpu: int = 2,
-              overlap: bool = False):
-        """overlap=True: the local round of step k+1 runs on a second stream while step k's exchange is
-        in flight (steps are independent: each reduces its own buffer set). Events order the reuse of a
-        set: its local round waits until the exchange that last read it has finished."""
+    def max_over_ranks(self, *vals: float) -> List[float]:
+        t = torch.tensor(vals, dtype=torch.float64, device=self._red_dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        return [float(v) for v in t.tolist()]
+
+    def shard_elems(self, n: int) -> int:
+        per = -(-n // self.world)
+        return -(-per // SHARD_ALIGN) * SHARD_ALIGN
+
+    def bench(self, n: int, steps: int, warmup: int, sets: int = 2, peers_per_gpu: int = 1,
+              overlap: bool = False, seed: int = 42, path: Optional[str] = None):
+        """Timed loop: exactly `steps` allreduces of n-element f32 buckets, bracketed by barrier + device
+        sync on both sides; returns (ms_per_step max over ranks, per-step local-round ms, extras). Step k
+        reduces buffer set k % sets, whose peer buckets are the synthetic buckets (seed + set, peer).
+
+        peers_per_gpu = 1: FMI's one peer per process, the bucket goes straight into fmi_comm_allreduce and
+        is never modified, so extras["result"] = (out bucket, seed of the last step's set) can be checked
+        against the same synthetic buckets (self_check). peers_per_gpu = 2: a local pairwise round first
+        (round 0 of recursive doubling); it folds in place, so repeated steps drift and no check applies.
+        overlap=True: the local round of step k+1 runs on a second stream while step k's exchange is in
+        flight (steps are independent: each reduces its own buffer set); events order set reuse."""
         import time
 
         import numpy as np
@@ -257,13 +288,15 @@ class CommAllreduce:
 
         from .comm import Path
 
-        direct = self._path == Path.DIRECT  # the reduced bucket must live in a symmetric window
+        path_name = self.path if path is None else path
+        path_id = {"tree": Path.TREE, "rccl": Path.RCCL, "direct": Path.DIRECT}[path_name]
+        direct = path_id == Path.DIRECT  # the reduced bucket must live in a symmetric window
 
         def first(s):
             b = self.comm.window(n, np.float32) if direct else fdev.Bucket(n, np.float32)
-            return b.fill_synthetic(42 + s, peers_per_gpu * self.rank)
+            return b.fill_synthetic(seed + s, peers_per_gpu * self.rank)
 
-        bufs = [[first(s)] + [fdev.Bucket(n, np.float32).fill_synthetic(42 + s, peers_per_gpu * self.rank + j)
+        bufs = [[first(s)] + [fdev.Bucket(n, np.float32).fill_synthetic(seed + s, peers_per_gpu * self.rank + j)
                               for j in range(1, peers_per_gpu)] for s in range(sets)]
         out = fdev.Bucket(n, np.float32)
         side = fdev.Stream() if overlap else None
@@ -284,7 +317,7 @@ class CommAllreduce:
             if overlap:
                 ready[s].record(side)
                 ready[s].wait_on(None)
-            self.comm.allreduce(Op.SUM, pair[0], out, path=self._path)
+            self.comm.allreduce(Op.SUM, pair[0], out, path=path_id)
             if overlap:
                 freed[s].record(None)
 
@@ -300,28 +333,124 @@ class CommAllreduce:
         fdev.sync()
         dist.barrier(group=self.group)
         t1 = time.perf_counter()
-        local = torch.tensor([(t1 - t0) * 1e3 / steps], dtype=torch.float64, device=torch.cuda.current_device())
-        dist.all_reduce(local, op=dist.ReduceOp.MAX, group=self.group)
-        step_ms = float(local.item())
+        step_ms = self.max_over_ranks((t1 - t0) * 1e3 / steps)[0]
         kernel_ms = [a.elapsed_ms(b) for a, b in evs]
-        per = -(-n // self.world)
+        for a, b in evs:
+            a.destroy()
+            b.destroy()
+        gib = n * 4 / 2 ** 30
         extra = {
-            "kernel_algo_bytes": 3 * n * 4,
-            "exchange": f"fmi_comm/{self.path}",
-            "shard_elems": -(-per // SHARD_ALIGN) * SHARD_ALIGN,
-            "algbw_GiB_s": round((n * 4 / 2 ** 30) / (step_ms * 1e-3), 2),
-            "busbw_GiB_s": round((n * 4 / 2 ** 30) / (step_ms * 1e-3) * 2 * (self.world - 1) / self.world, 2),
+            "exchange": f"fmi_comm/{path_name}",
+            "transport": self.transport,
+            "shard_elems": self.shard_elems(n),
+            "algbw_GiB_s": round(gib / (step_ms * 1e-3), 2),
+            "busbw_GiB_s": round(gib / (step_ms * 1e-3) * 2 * (self.world - 1) / self.world, 2),
         }
         if overlap:
             extra["overlap_steps"] = True
             side.destroy()
         for e in ready + freed:
             e.destroy()
-        if direct:
-            fdev.sync()
-            for pair in bufs:
+        fdev.sync()
+        for s, pair in enumerate(bufs):
+            if direct:
                 self.comm.window_free(pair[0])
+            else:
+                pair[0].free()
+            for b in pair[1:]:
+                b.free()
+        if peers_per_gpu == 1 and steps > 0:
+            extra["result"] = (out, seed + (steps - 1) % sets)
+        else:
+            out.free()
         return step_ms, kernel_ms, extra
+
+    def self_check(self, out, n: int, seed: int, width: int = 4096, tolerance: bool = False) -> dict:
+        """Check a one-peer-per-GPU f32 sum allreduce result on sampled windows, on every rank: for each
+        window (the head, the tail and a random interior range of every shard) this rank regenerates every
+        peer's synthetic bucket over that range (fmi_dev_fill_synthetic_at) and reduces them on its own GPU
+        with the single-GPU fused kernel in allreduce_no_order order for its own rank (fmi_dev_reduce_tree).
+        The sharded result must equal it bit for bit (tolerance=False: paths TREE and DIRECT, the reference's
+        bracketing) or lie within (N-1)·2^-24·Σ|x_p| of it (tolerance=True: path RCCL, RCCL's order).
+        Returns the counts, max over ranks; "ok" is the verdict every rank agrees on."""
+        import numpy as np
+
+        from . import device as fdev
+
+        N, r = self.world, self.rank
+        shard = self.shard_elems(n)
+        rng = np.random.default_rng(977 + r)
+        starts = set()
+        for j in range(N):
+            lo = j * shard
+            if lo >= n:
+                break
+            hi = min(n, lo + shard)
+            starts.update({lo, max(lo, hi - width), int(rng.integers(lo, max(lo + 1, hi - width)))})
+        peers = [fdev.Bucket(width, np.float32) for _ in range(N)]
+        ref = fdev.Bucket(width, np.float32)
+        mismatches = checked = 0
+        worst = 0.0
+        for st in sorted(starts):
+            w = min(width, n - st)
+            pv = [p.view(0, w) for p in peers]
+            for p in range(N):
+                pv[p].fill_synthetic(seed, p, first=st)
+            rv = ref.view(0, w)
+            fdev.reduce_tree(Op.SUM, Alg.ALLREDUCE, rv, pv, rank=r)
+            got, want = out.view(st, w).numpy(), rv.numpy()
+            if tolerance:
+                xs = np.stack([v.numpy() for v in pv]).astype(np.float64)
+                bound = (N - 1) * 2.0 ** -24 * np.abs(xs).sum(axis=0)
+                err = np.abs(got.astype(np.float64) - want.astype(np.float64))
+                mismatches += int(np.count_nonzero(err > bound))
+                worst = max(worst, float(np.max(err / np.maximum(bound, 1e-300))) if w else 0.0)
+            else:
+                mismatches += int(np.count_nonzero(got.view(np.uint32) != want.view(np.uint32)))
+            checked += w
+        for b in peers + [ref]:
+            b.free()
+        mism, chk = self.max_over_ranks(float(mismatches), float(checked))
+        res = {"ok": mism == 0, "mismatches": int(mism), "elements_checked_per_rank": int(chk),
+               "windows_per_rank": len(starts),
+               "against": ("single-GPU fused reduce_tree (allreduce_no_order order, own rank) of the same "
+                           "synthetic buckets rebuilt on this GPU, " +
+                           ("within (N-1)*2^-24*sum|x|" if tolerance else "bit-exact"))}
+        if tolerance:
+            res["max_err_over_bound"] = round(self.max_over_ranks(worst)[0], 4)
+        return res
+
+    def shard_kernel(self, n: int, launches: int = 20, sets: int = 2) -> dict:
+        """The dominant kernel of path TREE on this GPU: the fused N-way tree over n/N-element shards
+        (what fmi_comm_allreduce launches between its all-to-all and all-gather), timed with events on the
+        library stream over `launches` back-to-back launches on rotating input sets. Algorithmic HBM bytes
+        per launch: (N + 1) · shard · 4 (N shard reads + 1 write)."""
+        import numpy as np
+
+        from . import device as fdev
+
+        N = self.world
+        shard = self.shard_elems(n)
+        ins = [[fdev.Bucket(shard, np.float32).fill_synthetic(3 + s, p) for p in range(N)] for s in range(sets)]
+        out = fdev.Bucket(shard, np.float32)
+        for s in range(sets):
+            fdev.reduce_tree(Op.SUM, Alg.ALLREDUCE, out, ins[s])
+        fdev.sync()
+        e0, e1 = fdev.Event(), fdev.Event()
+        e0.record()
+        for k in range(launches):
+            fdev.reduce_tree(Op.SUM, Alg.ALLREDUCE, out, ins[k % sets])
+        e1.record()
+        e1.sync()
+        ms = e0.elapsed_ms(e1) / launches
+        e0.destroy()
+        e1.destroy()
+        for b in [out] + [x for s in ins for x in s]:
+            b.free()
+        ms = self.max_over_ranks(ms)[0]
+        return {"kernel": f"tree_kernel<OpSum,float,kAllreduce,P={N}>" if N > 1 else "P=1: device copy",
+                "kernel_avg_us": round(ms * 1e3, 2), "algorithmic_bytes_per_launch": (N + 1) * shard * 4,
+                "launches": launches, "rotating_sets": sets}
 
     def check_direct(self, n: int) -> bool:
         """Path DIRECT against path TREE on the same window bucket: bit-identical on every rank?"""
@@ -337,15 +466,16 @@ class CommAllreduce:
         fdev.sync()
         same = bool(np.array_equal(a.numpy().view(np.uint32), b.numpy().view(np.uint32)))
         self.comm.window_free(w)
-        flag = torch.tensor([1 if same else 0], dtype=torch.int32, device=torch.cuda.current_device())
-        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)
-        return bool(flag.item())
+        a.free()
+        b.free()
+        return self.max_over_ranks(0.0 if same else 1.0)[0] == 0.0
 
     def host_bench(self, n: int, iters: int = 3, chunk: int = 64 << 18) -> dict:
-        """Config C5 (untimed diagnostic): fmi_comm_allreduce_host of an n-element f32 bucket in page-locked
-        host memory on every rank — H2D, sharded allreduce and D2H pipelined in `chunk`-element pieces.
-        Returns the median wall time (max over ranks) and the per-rank host-bucket rate. 64 MiB chunks: 16 MiB
-        chunks measured up to 2x slower on some boxes."""
+        """Config C5: fmi_comm_allreduce_host of an n-element f32 bucket in page-locked host memory on every
+        rank — H2D, sharded allreduce and D2H pipelined in `chunk`-element pieces. Returns the median wall
+        time (max over ranks), the per-rank host-bucket rate and whether the result is right (every rank
+        holds rank + 1, so every element must be N (N + 1) / 2, exact in f32). 64 MiB chunks: 16 MiB chunks
+        measured up to 2x slower on some boxes."""
         import statistics
         import time
 
@@ -364,16 +494,17 @@ class CommAllreduce:
                 dist.barrier(group=self.group)
                 if k:
                     times.append(time.perf_counter() - t0)
-            local = torch.tensor([statistics.median(times) * 1e3], dtype=torch.float64,
-                                 device=torch.cuda.current_device())
-            dist.all_reduce(local, op=dist.ReduceOp.MAX, group=self.group)
-            ms = float(local.item())
+            ms = self.max_over_ranks(statistics.median(times) * 1e3)[0]
             ok = bool(np.all(recv.array == np.float32(self.world * (self.world + 1) // 2)))
+            ok = self.max_over_ranks(0.0 if ok else 1.0)[0] == 0.0
         finally:
             send.free()
             recv.free()
         return {"bucket_mib": n * 4 // (1 << 20), "chunk_mib": chunk * 4 / (1 << 20), "ms": round(ms, 3),
                 "per_rank_GiB_s": round(n * 4 / 2 ** 30 / (ms * 1e-3), 2), "result_ok": ok}
+
+    def destroy(self) -> None:
+        self.comm.destroy()
 
 
 def phase_breakdown(n: int, group=None, iters: int = 5) -> dict:

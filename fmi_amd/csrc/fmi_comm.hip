@@ -152,6 +152,10 @@ public:
     // every rank returns FMI_OK only if every rank could export and map, so no rank is left waiting.
     virtual int map_window(char* base, bool ok, std::vector<char*>& peers, hipStream_t s) = 0;
     virtual void unmap_window(const std::vector<char*>& peers) = 0;
+    // Blocking element-wise max over ranks of k <= kAgreeMax host int64 values (in place): used to check
+    // that every rank passed the same arguments (FMI_CHECK_DIRECT).
+    static constexpr int kAgreeMax = 4;
+    virtual int agree_max(int64_t* vals, int k, hipStream_t s) = 0;
     virtual int reduce_scatter(int, int, const void*, void*, size_t, hipStream_t) {
         return fail(FMI_ERR_UNSUPPORTED, "path RCCL needs the RCCL transport");
     }
@@ -312,6 +316,19 @@ public:
         for (int j = 0; j < static_cast<int>(peers.size()); ++j)
             if (j != rank_ && peers[j]) (void)hipIpcCloseMemHandle(peers[j]);
     }
+    int agree_max(int64_t* vals, int k, hipStream_t s) override {
+        int64_t* d = nullptr;
+        FMI_COMM_HIP(hipMalloc(&d, kAgreeMax * sizeof(int64_t)));
+        const int rc = [&]() -> int {
+            FMI_COMM_HIP(hipMemcpyAsync(d, vals, k * sizeof(int64_t), hipMemcpyHostToDevice, s));
+            FMI_NCCL(api_, AllReduce(d, d, k, ncclInt64, ncclMax, comm_, s));
+            FMI_COMM_HIP(hipMemcpyAsync(vals, d, k * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+            FMI_COMM_HIP(hipStreamSynchronize(s));
+            return FMI_OK;
+        }();
+        (void)hipFree(d);
+        return rc;
+    }
 
 private:
     const RcclApi* api_;
@@ -448,6 +465,18 @@ public:
         return FMI_OK;
     }
     void unmap_window(const std::vector<char*>&) override {}
+    int agree_max(int64_t* vals, int k, hipStream_t s) override {
+        int64_t out[kAgreeMax];
+        const int rc = exchange(reinterpret_cast<const char*>(vals), s, [&](const std::vector<const char*>& all) -> int {
+            for (int i = 0; i < k; ++i) {
+                out[i] = reinterpret_cast<const int64_t*>(all[0])[i];
+                for (int j = 1; j < n_; ++j) out[i] = std::max(out[i], reinterpret_cast<const int64_t*>(all[j])[i]);
+            }
+            return FMI_OK;
+        });
+        if (rc == FMI_OK) std::copy(out, out + k, vals);  // after the closing barrier: every rank has read
+        return rc;
+    }
 
 private:
     // Publish my buffer, wait for everyone, run `work` over all ranks' buffers, wait until everyone's
@@ -496,6 +525,7 @@ struct ProcCtrl {  // lives in the shared segment; all-zero is the initial state
     } mail[kProcMaxRanks];
     hipIpcMemHandle_t handle[kProcMaxRanks];
     std::atomic<int> ok[kProcMaxRanks];
+    int64_t agree[kProcMaxRanks][4];  // Transport::agree_max inputs, one row per rank
 };
 static_assert(sizeof(ProcCtrl) <= kProcCtrlBytes, "control block");
 
@@ -666,6 +696,14 @@ public:
         for (int j = 0; j < static_cast<int>(peers.size()); ++j)
             if (j != rank_ && peers[j]) (void)hipIpcCloseMemHandle(peers[j]);
     }
+    int agree_max(int64_t* vals, int k, hipStream_t s) override {
+        FMI_COMM_HIP(hipStreamSynchronize(s));
+        std::copy(vals, vals + k, ctrl_->agree[rank_]);
+        FMI_COMM_RC(host_barrier("agree (published)"));
+        for (int i = 0; i < k; ++i)
+            for (int j = 0; j < n_; ++j) vals[i] = std::max(vals[i], ctrl_->agree[j][i]);
+        return host_barrier("agree (read)");
+    }
 
 private:
     char* slot(int r) const { return base_ + kProcCtrlBytes + static_cast<size_t>(r) * kProcSlot; }
@@ -794,11 +832,16 @@ struct Comm {
 
     ~Comm() {
         if (pipe.cs) (void)hipStreamSynchronize(pipe.cs);
+        // Windows are read by the peers: wait until every rank is done with them (communicators are torn
+        // down collectively, as the reference's Communicator destructor finalizes every channel). A path
+        // DIRECT collective may have run on any stream of this process and still be reading a peer's window
+        // through its mapping, so drain the whole device before the barrier releases the peers.
+        if (!windows.empty()) {
+            (void)hipDeviceSynchronize();
+            (void)t->barrier(library_stream());
+        }
         for (void* b : buf)
             if (b) (void)hipFree(b);
-        // Windows are read by the peers: wait until every rank is done with them (communicators are torn
-        // down collectively, as the reference's Communicator destructor finalizes every channel).
-        if (!windows.empty()) (void)t->barrier(library_stream());
         for (auto& [base, w] : windows) {
             t->unmap_window(w.peers);
             (void)hipFree(base);
@@ -904,6 +947,19 @@ int allreduce_direct(Comm* c, const Window& w, size_t off, int op, int dtype, in
     if (N > sched::kMaxPeers)
         return fail(FMI_ERR_UNSUPPORTED, "path DIRECT supports up to " + std::to_string(sched::kMaxPeers) + " ranks");
     const size_t shard = shard_elems(n, N);
+    static const bool check = [] {
+        const char* e = std::getenv("FMI_CHECK_DIRECT");
+        return e && e[0] == '1';
+    }();
+    if (check) {  // every rank must read the peers' windows at the offset and length it uses itself
+        int64_t v[4] = {static_cast<int64_t>(off), -static_cast<int64_t>(off), static_cast<int64_t>(n),
+                        -static_cast<int64_t>(n)};
+        FMI_COMM_RC(c->t->agree_max(v, 4, s));
+        if (v[0] != -v[1] || v[2] != -v[3])
+            return fail(FMI_ERR_INVALID, "path DIRECT: ranks passed different window offsets or lengths (offset " +
+                                             std::to_string(-v[1]) + ".." + std::to_string(v[0]) + ", n " +
+                                             std::to_string(-v[3]) + ".." + std::to_string(v[2]) + ")");
+    }
     FMI_COMM_RC(c->t->barrier_async(s));
     const size_t lo = std::min(n, static_cast<size_t>(k) * shard);
     const size_t len = std::min(shard, n - lo);
@@ -1112,7 +1168,10 @@ int fmi_comm_window_free(fmi_comm_t comm, void* ptr) {
     std::lock_guard<std::mutex> lk(c->mu);
     auto it = c->windows.find(static_cast<char*>(ptr));
     if (it == c->windows.end()) return fail(FMI_ERR_INVALID, "not a window of this communicator");
-    // no peer may still be reading it
+    // No peer may still be reading it, and this rank must be done reading the peers' windows: a path
+    // DIRECT collective on any stream (not only the library's) reads them through the mappings that are
+    // closed below, so the whole device drains before the barrier.
+    FMI_COMM_HIP(hipDeviceSynchronize());
     FMI_COMM_RC(c->t->barrier(library_stream()));
     c->t->unmap_window(it->second.peers);
     FMI_COMM_HIP(hipFree(it->first));

@@ -894,20 +894,25 @@ int fmi_host_reduce_pair(int op, int dtype, void* inout, const void* in, size_t 
     return rc;
 }
 
-int fmi_dev_fill_synthetic(int dtype, void* buf, size_t n, uint64_t seed, uint32_t peer, fmi_stream_t stream) {
+int fmi_dev_fill_synthetic_at(int dtype, void* buf, size_t n, uint64_t seed, uint32_t peer, uint64_t first,
+                              fmi_stream_t stream) {
     if (n == 0) return FMI_OK;
     if (!buf) return fail(FMI_ERR_INVALID, "null buffer");
     if (int rc = require_device()) return rc;
     hipStream_t s = resolve(stream);
     const unsigned grid = static_cast<unsigned>(std::min<size_t>(grid_for(n, 256), 16384));
     if (int rc = with_dtype<true>(dtype, [&]<class T>() -> int {
-            synth_kernel<T><<<grid, 256, 0, s>>>(static_cast<T*>(buf), n, seed, peer);
+            synth_kernel<T><<<grid, 256, 0, s>>>(static_cast<T*>(buf), n, seed, peer, first);
             return FMI_OK;
         }))
         return rc;
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail("synthetic fill launch", e);
     return FMI_OK;
+}
+
+int fmi_dev_fill_synthetic(int dtype, void* buf, size_t n, uint64_t seed, uint32_t peer, fmi_stream_t stream) {
+    return fmi_dev_fill_synthetic_at(dtype, buf, n, seed, peer, 0, stream);
 }
 
 int fmi_schedule_expr(int alg, int P, int rank, char* buf, size_t len) {

@@ -1,10 +1,11 @@
 // One-pass tree reductions beyond the fused kernels, up to 128 peers (blocks of 16 peers):
 // reduce_no_order (reference src/comm/PeerToPeer.cpp:59-84; any 17..128 peers, ragged last block included,
 // reduce_any_kernel below), allreduce_no_order (:96-130) for
-// P = 32, 64, 128 (no pre-fold). tree_blocked (fmi_dev.hip) evaluates the same bracketing as a launch per
-// block, each writing its block value to a temp, then a launch over the B temps: P + 2 B + 1 bucket passes.
-// Here one thread computes its lane group's B block values in registers and then the block-level program:
-// P + 1 passes. Same programs, same operand order, so the same bits.
+// P = 32, 64, 128 (no pre-fold) and, in prefold_blocks_kernel, P = 48, 80, 96, 112 (whole blocks pre-fold).
+// tree_blocked (fmi_dev.hip) evaluates the same bracketing as a launch per block, each writing its block value
+// to a temp, then a launch over the B temps: P + 2 B + 1 bucket passes. Here one thread computes its lane
+// group's block values in registers and then the block-level program: P + 1 passes. Same programs, same
+// operand order, so the same bits.
 //   reduce:     binomial rounds 0..3 stay inside each block (the block's 16-peer reduce program); rounds 4..
 //               combine the block values at spans 16, 32, ..: the reduce program over the B values.
 //   allreduce:  recursive-doubling rounds 0..3 give position p the block's 16-peer allreduce for rank p % 16;
@@ -175,11 +176,9 @@ __global__ void __launch_bounds__(256) reduce_any_kernel(BlockedScanPtrs ptrs, i
 
 bool tree_blocks_one_pass_covers(int op, int dtype, int alg, int P) {
     if (alg == FMI_ALG_REDUCE) return P > sched::kMaxFusedPeers && P <= kMaxOnePassScanBlocks * BL;
-    if (P % BL != 0) return false;
+    if (alg != FMI_ALG_ALLREDUCE || P % BL != 0) return false;
     const int B = P / BL;
-    if (B < 2 || B > kMaxOnePassScanBlocks) return false;
-    if (alg == FMI_ALG_REDUCE) return true;
-    return alg == FMI_ALG_ALLREDUCE && (B & (B - 1)) == 0;
+    return B >= 2 && B <= kMaxOnePassScanBlocks && (B & (B - 1)) == 0;
 }
 
 int launch_tree_blocks_one_pass(int op, int dtype, int alg, int P, const BlockedScanPtrs& ptrs, size_t n, int rank,

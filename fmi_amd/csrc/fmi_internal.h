@@ -111,8 +111,9 @@ struct BlockedScanPtrs {
 };
 int launch_scan_blocks_one_pass(int op, int dtype, int B, const BlockedScanPtrs& ptrs, size_t n, hipStream_t s);
 int launch_scan_blocks_one_pass_wide(int op, int dtype, int B, const BlockedScanPtrs& ptrs, size_t n, hipStream_t s);
-// reduce_no_order over P = 16 B peers and allreduce_no_order over P = 32, 64, 128 in one pass: ptrs.in[0..P) the
-// (transformed) inputs, ptrs.out[0] the result of peer `rank` (allreduce) (fmi_fused_tree_blocked.hip)
+// reduce_no_order over any 17..128 peers (ragged last block included) and allreduce_no_order over P = 32, 64, 128
+// in one pass: ptrs.in[0..P) the (transformed) inputs, ptrs.out[0] the result of peer `rank` (allreduce)
+// (fmi_fused_tree_blocked.hip)
 bool tree_blocks_one_pass_covers(int op, int dtype, int alg, int P);
 // allreduce_no_order over P = 48, 80, 96, 112 (full blocks pre-fold) in one pass: ptrs.in[0..2^k) the doubling
 // group and ptrs.in[2^k..P) the partners, each block permuted by rank % 16 by the caller; rank_hi = rank / 16

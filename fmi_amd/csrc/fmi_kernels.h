@@ -411,11 +411,11 @@ __host__ __device__ __forceinline__ T synth_value(uint64_t h) {
 }
 
 template <class T>
-__global__ void __launch_bounds__(256) synth_kernel(T* buf, size_t n, uint64_t seed, uint32_t peer) {
+__global__ void __launch_bounds__(256) synth_kernel(T* buf, size_t n, uint64_t seed, uint32_t peer, uint64_t first) {
     const uint64_t key = seed ^ (static_cast<uint64_t>(peer) << 40);
     for (size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
          i += static_cast<size_t>(gridDim.x) * blockDim.x)
-        buf[i] = synth_value<T>(splitmix64(key ^ i));
+        buf[i] = synth_value<T>(splitmix64(key ^ (first + i)));
 }
 
 }  // namespace fmi::dev

@@ -165,8 +165,10 @@ class Bucket:
         _lib.call("fmi_stream_sync", _sptr(stream))
         return out
 
-    def fill_synthetic(self, seed: int, peer: int, stream=None) -> "Bucket":
-        _lib.call("fmi_dev_fill_synthetic", int(self.dtype), self.ptr, self.n, seed, peer, _sptr(stream))
+    def fill_synthetic(self, seed: int, peer: int, stream=None, first: int = 0) -> "Bucket":
+        """Elements [first, first + n) of peer `peer`'s synthetic bucket (SURVEY.md §8d generator)."""
+        _lib.call("fmi_dev_fill_synthetic_at", int(self.dtype), self.ptr, self.n, seed, peer, int(first),
+                  _sptr(stream))
         return self
 
     def copy_from(self, other: "Bucket", stream=None) -> None:

@@ -171,7 +171,9 @@ int fmi_host_reduce_pair(int op, int dtype, void* inout, const void* in, size_t 
  * order:
  *   allreduce (path TREE): all-to-all of N shards -> fused P-way kernel over the N partials of this
  *       GPU's shard (allreduce_no_order / reduce_ltr order) -> all-gather. Bit-identical to the
- *       reference's N-peer allreduce (rank 0's operand order for float max/min ties).
+ *       reference's N-peer allreduce on every rank, each rank with its OWN operand order: for float
+ *       max/min (whose ±0 ties and NaNs depend on it) the shard owner computes its shard in every rank's
+ *       order and an all-to-all replaces the all-gather, so rank r receives what reference peer r holds.
  *   allreduce (path RCCL): RCCL reduce-scatter + all-gather (RCCL's order; within (N-1)*u*sum|x|).
  *   reduce: all-to-all -> fused kernel in reduce_no_order / reduce_ltr order for `root` -> gather.
  *   scan:   all-to-all -> fused peer-axis scan -> all-to-all back.
@@ -183,14 +185,23 @@ int fmi_host_reduce_pair(int op, int dtype, void* inout, const void* in, size_t 
  * POSIX shared-memory segment, windows mapped with HIP IPC — the same schedules again, so multi-process
  * runs, FMI_PATH_DIRECT's cross-process mappings included, are testable on a single GPU).
  * All calls enqueue on `stream` (NULL = library stream); results are valid after fmi_stream_sync.
- * Buckets are device pointers; `send` is never modified; recv may alias send. */
+ * Buckets are device pointers; recv may alias send.
+ * Side effect on `send` — a deliberate divergence from the reference: the reference's commutative
+ * allreduce / scan leave the result in the caller's sendbuf and its reduce leaves partials in interior
+ * peers' sendbufs (src/comm/PeerToPeer.cpp:72,103,119,160,179). Here `send` is never modified by
+ * allreduce, reduce or scan, so a C-ABI caller that relied on the clobber passes recv == send (allreduce,
+ * scan) to get it. The C++ channel FMI::Comm::Rccl (fmi_amd/cpp/include/fmi/comm/Rccl.h) restores the
+ * reference's side effects itself, so Communicator callers see the reference behaviour. */
 #define FMI_COMM_ID_BYTES 128
 typedef void* fmi_comm_t;
 typedef enum { FMI_TRANSPORT_RCCL = 0, FMI_TRANSPORT_LOCAL = 1, FMI_TRANSPORT_PROC = 2 } fmi_transport_t;
-/* FMI_PATH_DIRECT: no RCCL data movement. `send` must lie in a window (fmi_comm_window_alloc, same offset on
- * every rank); rank k's fused kernel reads shard k of every rank's window over xGMI (IPC-mapped peer
+/* FMI_PATH_DIRECT: no RCCL data movement. `send` must lie in a window (fmi_comm_window_alloc) at the SAME
+ * byte offset and with the same n on every rank: rank k reads every peer's window at its own offset (windows
+ * are equal-sized, so a mismatch reads wrong data, never outside a window). With FMI_CHECK_DIRECT=1 in the
+ * environment every call first compares the (offset, n) pairs across ranks (a blocking all-reduce) and a
+ * mismatch fails the call on every rank with FMI_ERR_INVALID. Rank k's fused kernel reads shard k of every rank's window over xGMI (IPC-mapped peer
  * memory) and reduces it in the reference's order, then every rank reads the N reduced shards from the
- * peers' windows. Bit-identical to FMI_PATH_TREE; up to 256 ranks. */
+ * peers' windows. Bit-identical to FMI_PATH_TREE. */
 typedef enum { FMI_PATH_TREE = 0, FMI_PATH_RCCL = 1, FMI_PATH_DIRECT = 2 } fmi_path_t;
 
 /* A fresh communicator id (FMI_COMM_ID_BYTES) made by one rank and handed to the others by any host
@@ -203,7 +214,8 @@ int fmi_comm_size(fmi_comm_t comm, int* nranks, int* rank);
  * device bucket of `bytes` that every peer of the communicator can read directly (RCCL transport: HIP IPC
  * handles exchanged by all-gather, mapped with peer access over xGMI). All-or-nothing: if any rank cannot
  * allocate, export or map, every rank gets an error. Freed (collectively) by fmi_comm_window_free or with
- * the communicator. */
+ * the communicator: both first wait for all work on this rank's device (any stream may still be reading
+ * a peer's window through its mapping), then barrier with the peers, then unmap and free. */
 int fmi_comm_window_alloc(fmi_comm_t comm, size_t bytes, void** ptr);
 int fmi_comm_window_free(fmi_comm_t comm, void* ptr);
 /* alg: FMI_ALG_ALLREDUCE (commutative+associative) or FMI_ALG_REDUCE_LTR (ordered) */
@@ -237,6 +249,10 @@ int fmi_comm_barrier(fmi_comm_t comm, fmi_stream_t stream);
  * f64 = (double)((h >> 11) * 2^-53) * 2 - 1,  i32 = (int32)(h >> 32),  i64 = (int64)h. */
 int fmi_dev_fill_synthetic(int dtype, void* buf, size_t n, uint64_t seed, uint32_t peer,
                            fmi_stream_t stream);
+/* Elements [first, first + n) of the same synthetic bucket (i runs from `first`): lets a rank rebuild any
+ * window of every peer's bucket locally, e.g. to check a sharded collective's result on sampled ranges. */
+int fmi_dev_fill_synthetic_at(int dtype, void* buf, size_t n, uint64_t seed, uint32_t peer, uint64_t first,
+                              fmi_stream_t stream);
 
 /* ---- schedule introspection (host-only logic, no device needed) --------------------------------
  * Writes the symbolic combine expression peer `rank` ends with, e.g. "((x0+x1)+(x2+x3))", as the

@@ -1,6 +1,6 @@
 """bench.py's host-side contract (CPU): the JSON line is printed exactly once, and the per-rank deadline
-over the after-`value` section (the N>1 allreduce measurement and diagnostics) prints the measured line and
-exits cleanly when that section hangs."""
+over the after-`value` section (C4, C5 and the diagnostics) prints the measured line, marked "incomplete" at
+top level, and exits when that section hangs."""
 import json
 import os
 import subprocess
@@ -32,7 +32,7 @@ def test_deadline_prints_measured_line_and_exits():
         sys.path.insert(0, {ROOT!r})
         import bench
         line = {{"metric": "m", "value": 2.5, "config": {{}}}}
-        state = line["config"]["allreduce"] = {{}}
+        state = line["c4"] = {{}}
         e = bench._Emitter(line, 0)
         t = threading.Timer(0.2, e.deadline, args=(state,))
         t.daemon = True
@@ -45,10 +45,11 @@ def test_deadline_prints_measured_line_and_exits():
     lines = r.stdout.strip().splitlines()
     assert len(lines) == 1
     got = json.loads(lines[0])
-    assert got["value"] == 2.5 and "incomplete" in got["config"]["allreduce"]
+    assert got["value"] == 2.5 and "incomplete" in got and "incomplete" in got["c4"]
 
 
 def test_defaults_are_the_contract(monkeypatch):
     monkeypatch.setattr(sys, "argv", ["bench.py"])
     a = bench.parse()
     assert a.gpus == 1 and a.bucket_mib == 256 and a.steps > 0 and a.warmup > 0 and a.path == "tree"
+    assert a.c4_mib == 1024 and a.transport == "rccl"  # C4: 1 GiB per peer, one process per GPU over RCCL

@@ -109,6 +109,28 @@ def test_single_peer_per_gpu():
         assert _bits_equal(outs[r], want[r])
 
 
+def test_four_peers_per_gpu_bit_exact():
+    """2^k local peers fold as the 2^k-peer allreduce program (recursive doubling's local rounds), so the
+    sharded result is still the reference's bracketing: here 8 peers on 2 processes."""
+    world, n = 2, 2053
+    outs, _, xs = _run(world, n, "float32", 0, "tree", peers_per_gpu=4)
+    want, _ = orc.allreduce(xs, orc.op_sum)
+    for r in range(world):
+        assert _bits_equal(outs[r], want[4 * r]), f"rank {r}"
+
+
+def test_non_power_of_two_local_peers_rejected():
+    from fmi_amd import collectives
+
+    class _Stub(collectives.ShardedAllreduce):
+        def __init__(self):  # no process group needed: the check precedes any exchange
+            pass
+
+    x = [torch.zeros(8) for _ in range(3)]
+    with pytest.raises(ValueError, match="power-of-two"):
+        _Stub().allreduce(0, x, torch.zeros(8))
+
+
 @pytest.mark.parametrize("path", ["tree", "rccl"])
 def test_bench_loop_runs_multi_process(path):
     import json
