@@ -819,6 +819,7 @@ struct HostPipe {
 struct Window {
     size_t bytes = 0;
     std::vector<char*> peers;  // peers[j] = rank j's window base, as seen from this rank
+    char** shards = nullptr;   // device table: peers[j] + bytes (rank j's reduced-shard area), any N
 };
 
 struct Comm {
@@ -844,6 +845,7 @@ struct Comm {
             if (b) (void)hipFree(b);
         for (auto& [base, w] : windows) {
             t->unmap_window(w.peers);
+            if (w.shards) (void)hipFree(w.shards);
             (void)hipFree(base);
         }
     }
@@ -905,30 +907,31 @@ int padded_source(Comm* c, size_t n, size_t padded, size_t esz, const void* send
     return FMI_OK;
 }
 
-// recv[i] = (reduced-shard area of the rank owning element i)[i], for the byte range [0, nbytes): 16-B
-// nontemporal accesses over xGMI when every pointer is 16-B aligned, bytes otherwise. Shards are whole
-// multiples of 256 B, so a 16-B group never straddles two owners.
-struct WindowPtrs {  // every rank's reduced-shard area (kernel argument: 2 KiB at the 256-rank cap)
-    const void* in[sched::kMaxPeers];
-};
-
+// recv[i] = (reduced-shard area of the rank owning element i)[i], for the byte range [0, nbytes). The owners'
+// reduced-shard areas come from a device table (`shards`, one pointer per rank: no limit on the number of
+// ranks); blockIdx.y strides over the owners, so each block copies from one owner through a uniform (scalar)
+// pointer, and blockIdx.x over that owner's 16-B groups: nontemporal accesses over xGMI when every pointer is
+// 16-B aligned, bytes otherwise. Shards are whole multiples of 256 B: only the last owner has a ragged tail.
 template <bool VEC>
-__global__ void __launch_bounds__(256) gather_shards(WindowPtrs src, char* dst, size_t nbytes, size_t shard_bytes) {
+__global__ void __launch_bounds__(256) gather_shards(const char* const* shards, size_t off, char* dst, size_t nbytes,
+                                                     size_t shard_bytes, int nranks) {
     const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
     const size_t first = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-    if constexpr (VEC) {
-        const size_t nvec = nbytes / 16;
-        for (size_t g = first; g < nvec; g += stride) {
-            const size_t b = g * 16;
-            const auto* from = reinterpret_cast<const u32x4*>(static_cast<const char*>(src.in[b / shard_bytes]) + b);
-            __builtin_nontemporal_store(__builtin_nontemporal_load(from), reinterpret_cast<u32x4*>(dst + b));
+    for (int j = blockIdx.y; j < nranks; j += gridDim.y) {
+        const size_t lo = static_cast<size_t>(j) * shard_bytes;
+        if (lo >= nbytes) break;
+        const size_t len = nbytes - lo < shard_bytes ? nbytes - lo : shard_bytes;
+        const char* src = shards[j] + off + lo;
+        char* out = dst + lo;
+        if constexpr (VEC) {
+            const size_t nvec = len / 16;
+            for (size_t g = first; g < nvec; g += stride)
+                __builtin_nontemporal_store(__builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src) + g),
+                                            reinterpret_cast<u32x4*>(out) + g);
+            if (blockIdx.x == 0 && nvec * 16 + threadIdx.x < len) out[nvec * 16 + threadIdx.x] = src[nvec * 16 + threadIdx.x];
+        } else {
+            for (size_t b = first; b < len; b += stride) out[b] = src[b];
         }
-        if (blockIdx.x == 0 && nvec * 16 + threadIdx.x < nbytes) {
-            const size_t b = nvec * 16 + threadIdx.x;
-            dst[b] = static_cast<const char*>(src.in[b / shard_bytes])[b];
-        }
-    } else {
-        for (size_t b = first; b < nbytes; b += stride) dst[b] = static_cast<const char*>(src.in[b / shard_bytes])[b];
     }
 }
 
@@ -944,8 +947,6 @@ int allreduce_direct(Comm* c, const Window& w, size_t off, int op, int dtype, in
     const int N = c->t->n();
     const int k = c->t->rank();
     const size_t esz = dtype_size(dtype);
-    if (N > sched::kMaxPeers)
-        return fail(FMI_ERR_UNSUPPORTED, "path DIRECT supports up to " + std::to_string(sched::kMaxPeers) + " ranks");
     const size_t shard = shard_elems(n, N);
     static const bool check = [] {
         const char* e = std::getenv("FMI_CHECK_DIRECT");
@@ -970,18 +971,19 @@ int allreduce_direct(Comm* c, const Window& w, size_t off, int op, int dtype, in
         FMI_COMM_RC(fmi_dev_reduce_tree(op, dtype, alg, out, ins.data(), N, 0, len, s));
     }
     FMI_COMM_RC(c->t->barrier_async(s));
-    WindowPtrs src{};
-    bool vec = aligned16(recv);
-    for (int j = 0; j < N; ++j) {
-        src.in[j] = w.peers[j] + w.bytes + off;
-        vec = vec && aligned16(src.in[j]);
-    }
+    // Window bases are allocation starts (256-B aligned) and w.bytes is a multiple of 256, so every owner's
+    // source is 16-B aligned exactly when the common offset is.
+    const bool vec = aligned16(recv) && off % 16 == 0;
     const size_t nbytes = n * esz;
-    const unsigned grid = static_cast<unsigned>(std::min<size_t>(grid_for(vec ? nbytes / 16 : nbytes, 256), 1u << 20));
+    const size_t shard_bytes = shard * esz;
+    const unsigned gy = static_cast<unsigned>(std::min(N, 65535));
+    const size_t per_owner = std::max<size_t>(1, 16384 / gy);
+    const unsigned gx = static_cast<unsigned>(std::min(grid_for(vec ? shard_bytes / 16 : shard_bytes, 256), per_owner));
+    const dim3 grid(gx, gy);
     if (vec)
-        gather_shards<true><<<grid, 256, 0, s>>>(src, static_cast<char*>(recv), nbytes, shard * esz);
+        gather_shards<true><<<grid, 256, 0, s>>>(w.shards, off, static_cast<char*>(recv), nbytes, shard_bytes, N);
     else
-        gather_shards<false><<<grid, 256, 0, s>>>(src, static_cast<char*>(recv), nbytes, shard * esz);
+        gather_shards<false><<<grid, 256, 0, s>>>(w.shards, off, static_cast<char*>(recv), nbytes, shard_bytes, N);
     FMI_COMM_HIP(hipGetLastError());
     return FMI_OK;
 }
@@ -1095,7 +1097,7 @@ int fmi_comm_unique_id(int transport, void* id, size_t len) {
 int fmi_comm_init(fmi_comm_t* comm, const void* id, int nranks, int rank) {
     if (!comm || !id) return fail(FMI_ERR_INVALID, "null argument");
     if (nranks < 1 || rank < 0 || rank >= nranks) return fail(FMI_ERR_INVALID, "rank out of range");
-    if (nranks > fmi::sched::kMaxPeers)  // every shard program is one P = nranks program
+    if (nranks > fmi::sched::kMaxPeers)  // value ids of a P = nranks program must fit 31 bits
         return fail(FMI_ERR_INVALID, "at most " + std::to_string(fmi::sched::kMaxPeers) + " ranks per communicator");
     auto c = std::make_unique<Comm>();
     if (std::memcmp(id, kLocalMagic, 8) == 0) {
@@ -1157,6 +1159,18 @@ int fmi_comm_window_alloc(fmi_comm_t comm, size_t bytes, void** ptr) {
         if (base) (void)hipFree(base);
         return rc;
     }
+    // The gather's table of reduced-shard areas (any number of ranks). A failure here is local, after the
+    // collective mapping succeeded everywhere: this rank fails; the peers still hold a usable window.
+    std::vector<char*> table(w.peers.size());
+    for (size_t j = 0; j < table.size(); ++j) table[j] = w.peers[j] + bytes;
+    hipError_t e = hipMalloc(&w.shards, table.size() * sizeof(char*));
+    if (e == hipSuccess) e = hipMemcpy(w.shards, table.data(), table.size() * sizeof(char*), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        if (w.shards) (void)hipFree(w.shards);
+        c->t->unmap_window(w.peers);
+        (void)hipFree(base);
+        return fail(FMI_ERR_ALLOC, std::string("window shard table: ") + hipGetErrorString(e));
+    }
     c->windows[base] = std::move(w);
     *ptr = base;
     return FMI_OK;
@@ -1174,6 +1188,7 @@ int fmi_comm_window_free(fmi_comm_t comm, void* ptr) {
     FMI_COMM_HIP(hipDeviceSynchronize());
     FMI_COMM_RC(c->t->barrier(library_stream()));
     c->t->unmap_window(it->second.peers);
+    if (it->second.shards) FMI_COMM_HIP(hipFree(it->second.shards));
     FMI_COMM_HIP(hipFree(it->first));
     c->windows.erase(it);
     return FMI_OK;

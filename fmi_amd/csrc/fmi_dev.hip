@@ -506,10 +506,27 @@ int check_peer_args(int op, int dtype, int P) {
 }
 
 // Symbolic evaluation of a program, for fmi_schedule_expr.
+// Iterative (an LTR chain over P peers nests P deep): a stack of pending tokens, written left to right.
 std::string expr_of(const sched::HostProgram& prog, int v) {
-    if (v < prog.peers) return "x" + std::to_string(v);
-    const sched::Step& st = prog.step[v - prog.peers];
-    return "(" + expr_of(prog, st.a) + "+" + expr_of(prog, st.b) + ")";
+    std::string e;
+    std::vector<int> todo{v};  // >= 0: a value id to expand; -1: "+"; -2: ")"
+    while (!todo.empty()) {
+        const int t = todo.back();
+        todo.pop_back();
+        if (t == -1) {
+            e += '+';
+        } else if (t == -2) {
+            e += ')';
+        } else if (t < prog.peers) {
+            e += 'x';
+            e += std::to_string(t);
+        } else {
+            const auto& st = prog.step[t - prog.peers];
+            e += '(';
+            todo.insert(todo.end(), {-2, st.b, -1, st.a});
+        }
+    }
+    return e;
 }
 
 }  // namespace

@@ -19,6 +19,8 @@
 #pragma once
 
 #include <cstdint>
+#include <type_traits>
+#include <vector>
 
 namespace fmi::sched {
 
@@ -54,16 +56,20 @@ constexpr int max_fused_peers(int alg) {
            : alg == 7 /*kAllreducePrefold16*/         ? 32
                                                       : kMaxFusedPeers;
 }
-inline constexpr int kMaxPeers = 256;       // P-way programs beyond the fused kernels, up to this P
-inline constexpr int kHostStepCap = 2560;   // >= max steps for P <= 256 (allreduce P=256: 2048)
+// No cap on the number of peers, as in the reference (src/comm/PeerToPeer.cpp:59-184 take any num_peers):
+// host programs (HostProgram below) are sized at run time; only the value ids must fit 31 bits.
+inline constexpr int kMaxPeers = 1 << 24;
 
 struct Step {
     uint16_t a;  // left operand (the buffer f.f overwrites)
     uint16_t b;  // right operand (the received buffer)
 };
 
+// Fixed-capacity program: the fused kernels' compile-time programs (value ids < 2^16).
 template <int CapSteps, int CapPeers>
 struct Program {
+    using Id = uint16_t;
+    using Ids = Id[CapPeers];
     int peers = 0;
     int nsteps = 0;
     bool ok = true;  // false if the capacity was exceeded or arguments were invalid
@@ -71,6 +77,7 @@ struct Program {
     uint16_t out[CapPeers] = {};
 
     constexpr int nvalues() const { return peers + nsteps; }
+    constexpr bool fits(int P) const { return P >= 1 && P <= CapPeers; }
 
     constexpr uint16_t emit(uint16_t a, uint16_t b) {
         if (nsteps >= CapSteps) {
@@ -79,6 +86,28 @@ struct Program {
         }
         step[nsteps] = Step{a, b};
         return static_cast<uint16_t>(peers + nsteps++);
+    }
+};
+
+// Run-time program for any P (host side: fmi_schedule_expr, the pairwise-pass execution, the oracle
+// checks). Same member names as Program, so host code indexes either alike.
+struct HostStep {
+    int32_t a;
+    int32_t b;
+};
+struct HostProgram {
+    using Id = int32_t;
+    int peers = 0;
+    int nsteps = 0;
+    bool ok = true;
+    std::vector<HostStep> step;
+    std::vector<int32_t> out;
+
+    int nvalues() const { return peers + nsteps; }
+    bool fits(int P) const { return P >= 1 && P <= kMaxPeers; }
+    int32_t emit(int32_t a, int32_t b) {
+        step.push_back(HostStep{a, b});
+        return peers + nsteps++;
     }
 };
 
@@ -94,19 +123,35 @@ constexpr int ceil_log2(int v) {
     return r;
 }
 
-// Build the program of `alg` for P peers. Ids are *transformed* ids for kReduce (root -> 0, reference
-// PeerToPeer::transform_peer_id, src/comm/PeerToPeer.cpp:287-293): the caller rotates its inputs so
+// The peers' current value ids: a fixed array for Program (constexpr), a vector for HostProgram.
+template <class Prog>
+struct IdVec {
+    typename Prog::Ids v = {};
+    constexpr explicit IdVec(int) {}
+    constexpr auto& operator[](int i) { return v[i]; }
+    constexpr const auto& operator[](int i) const { return v[i]; }
+};
+template <>
+struct IdVec<HostProgram> {
+    std::vector<int32_t> v;
+    explicit IdVec(int P) : v(static_cast<size_t>(P)) {}
+    int32_t& operator[](int i) { return v[static_cast<size_t>(i)]; }
+    const int32_t& operator[](int i) const { return v[static_cast<size_t>(i)]; }
+};
+
+// Build the program of `alg` for P peers into `prog`. Ids are *transformed* ids for kReduce (root -> 0,
+// reference PeerToPeer::transform_peer_id, src/comm/PeerToPeer.cpp:287-293): the caller rotates its inputs so
 // that input t is real peer (t + root) % P; out[0] is then the root's result.
-template <int CapSteps, int CapPeers>
-constexpr Program<CapSteps, CapPeers> build(int alg, int P) {
-    Program<CapSteps, CapPeers> prog{};
-    if (P < 1 || P > CapPeers) {
+template <class Prog>
+constexpr void build_into(Prog& prog, int alg, int P) {
+    using Id = typename Prog::Id;
+    if (!prog.fits(P)) {
         prog.ok = false;
-        return prog;
+        return;
     }
     prog.peers = P;
-    uint16_t cur[CapPeers] = {};
-    for (int p = 0; p < P; ++p) cur[p] = static_cast<uint16_t>(p);
+    IdVec<Prog> cur(P);
+    for (int p = 0; p < P; ++p) cur[p] = static_cast<Id>(p);
 
     switch (alg) {
         case kAllreduce: {
@@ -118,8 +163,7 @@ constexpr Program<CapSteps, CapPeers> build(int alg, int P) {
             const int pow2 = 1 << rounds;
             for (int p = pow2; p < P; ++p) cur[p - pow2] = prog.emit(cur[p - pow2], cur[p]);
             for (int i = 0; i < rounds; ++i) {
-                uint16_t prev[CapPeers] = {};
-                for (int p = 0; p < pow2; ++p) prev[p] = cur[p];
+                IdVec<Prog> prev = cur;
                 for (int p = 0; p < pow2; ++p) cur[p] = prog.emit(prev[p], prev[p ^ (1 << i)]);
             }
             for (int p = pow2; p < P; ++p) cur[p] = cur[p - pow2];
@@ -133,14 +177,13 @@ constexpr Program<CapSteps, CapPeers> build(int alg, int P) {
                 const int span = 1 << i;
                 for (int t = 0; t + span < P; t += 2 * span) cur[t] = prog.emit(cur[t], cur[t + span]);
             }
-            break;  // out[t != 0] is a non-root's partial; only out[0] (the root) is meaningful
-
+            break;  // out[t != 0] is a non-root's partial (its sendbuf after the call, :72); out[0] the root's
         }
         case kReduceLtr: {
             // Root gathers all buckets by real id and folds left to right: ((x0 + x1) + x2) + ... (:49-52).
             // The allreduce variant broadcasts the root's result, so every peer ends with it.
-            uint16_t acc = 0;
-            for (int p = 1; p < P; ++p) acc = prog.emit(acc, static_cast<uint16_t>(p));
+            Id acc = 0;
+            for (int p = 1; p < P; ++p) acc = prog.emit(acc, static_cast<Id>(p));
             for (int p = 0; p < P; ++p) cur[p] = acc;
             break;
         }
@@ -170,7 +213,7 @@ constexpr Program<CapSteps, CapPeers> build(int alg, int P) {
         case kScanLtr:
         case kScanLtrCarry: {
             // Linear chain: peer k receives the prefix of k-1 and combines f(prefix, own) (:146-147).
-            for (int p = 1; p < P; ++p) cur[p] = prog.emit(cur[p - 1], static_cast<uint16_t>(p));
+            for (int p = 1; p < P; ++p) cur[p] = prog.emit(cur[p - 1], static_cast<Id>(p));
             break;
         }
         case kAllreducePrefold16: {
@@ -178,12 +221,11 @@ constexpr Program<CapSteps, CapPeers> build(int alg, int P) {
             // (:108-121) over them: the program of a block whose peers all have a partner >= 2^k.
             if (P != 32) {
                 prog.ok = false;
-                return prog;
+                return;
             }
             for (int j = 0; j < 16; ++j) cur[j] = prog.emit(cur[j], cur[16 + j]);
             for (int i = 0; i < 4; ++i) {
-                uint16_t prev[CapPeers] = {};
-                for (int p = 0; p < 16; ++p) prev[p] = cur[p];
+                IdVec<Prog> prev = cur;
                 for (int p = 0; p < 16; ++p) cur[p] = prog.emit(prev[p], prev[p ^ (1 << i)]);
             }
             for (int p = 16; p < 32; ++p) cur[p] = cur[p - 16];
@@ -199,7 +241,7 @@ constexpr Program<CapSteps, CapPeers> build(int alg, int P) {
             // its result is the block-level prefix, computed separately, so P - 1 <= 15 inputs.
             if (P - 1 > kScanBlock - 1) {
                 prog.ok = false;
-                return prog;
+                return;
             }
             const int m = P - 1;
             for (int i = 0; i < 4; ++i) {
@@ -220,9 +262,16 @@ constexpr Program<CapSteps, CapPeers> build(int alg, int P) {
         }
         default:
             prog.ok = false;
-            return prog;
+            return;
     }
+    if constexpr (std::is_same_v<Prog, HostProgram>) prog.out.assign(static_cast<size_t>(P), 0);
     for (int p = 0; p < P; ++p) prog.out[p] = cur[p];
+}
+
+template <int CapSteps, int CapPeers>
+constexpr Program<CapSteps, CapPeers> build(int alg, int P) {
+    Program<CapSteps, CapPeers> prog{};
+    build_into(prog, alg, P);
     return prog;
 }
 
@@ -232,8 +281,10 @@ struct Fused {
     static_assert(prog.ok, "fused schedule exceeds capacity");
 };
 
-using HostProgram = Program<kHostStepCap, kMaxPeers>;
-
-inline HostProgram build_host(int alg, int P) { return build<kHostStepCap, kMaxPeers>(alg, P); }
+inline HostProgram build_host(int alg, int P) {
+    HostProgram prog;
+    build_into(prog, alg, P);
+    return prog;
+}
 
 }  // namespace fmi::sched

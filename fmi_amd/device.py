@@ -345,9 +345,16 @@ def _check_peers(out: Bucket, ins: Sequence[Bucket]) -> None:
 
 
 def schedule_expr(alg: Alg, P: int, rank: int) -> str:
-    buf = ctypes.create_string_buffer(1 << 16)
-    _lib.call("fmi_schedule_expr", int(alg), P, rank, buf, len(buf))
-    return buf.value.decode()
+    size = 1 << 16
+    while True:
+        buf = ctypes.create_string_buffer(size)
+        status = _lib.load().fmi_schedule_expr(int(alg), P, rank, buf, len(buf))
+        msg = _lib.last_error() if status else ""
+        if status and "buffer too small" in msg:  # "(<bytes> needed)"
+            size = int(msg.split("(")[1].split()[0])
+            continue
+        _lib.check(status)
+        return buf.value.decode()
 
 
 def tune_set(key: Tune, value: int) -> None:

@@ -149,6 +149,38 @@ def test_comm_more_ranks_than_a_fused_kernel_holds(device):
     assert_bit_equal(res[3][1], want_red, "reduce root 3")
 
 
+def test_comm_300_ranks(device):
+    """No rank cap (the reference's collectives take any num_peers, src/comm/PeerToPeer.cpp:59-184): a
+    300-rank communicator (LOCAL transport, 300 threads on the one GPU). Every shard reduction is a 300-peer
+    program (three levels of fused 16-peer blocks); path DIRECT gathers through its device pointer table.
+    Bit-exact vs the oracle for allreduce (TREE, DIRECT), reduce at a non-zero root and scan."""
+    N, n = 300, 1027
+    xs = [inputs(np.float32, n, r, seed=43) for r in range(N)]
+
+    def body(c, r):
+        s, out, red, sc = Bucket.from_numpy(xs[r]), Bucket(n, np.float32), Bucket(n, np.float32), Bucket(n, np.float32)
+        c.allreduce(Op.SUM, s, out)
+        c.reduce(Op.SUM, s, red if r == 37 else None, 37)
+        c.scan(Op.SUM, s, sc)
+        w, direct = c.window(n, np.float32), Bucket(n, np.float32)
+        w.upload(xs[r])
+        c.allreduce(Op.SUM, w, direct, path=Path.DIRECT)
+        fmi_amd.sync()
+        got = out.numpy(), red.numpy() if r == 37 else None, sc.numpy(), direct.numpy()
+        c.window_free(w)
+        return got
+
+    res = run_ranks(N, body)
+    want_ar, _ = orc.allreduce(xs, orc.op_sum)
+    want_red, _ = orc.reduce(xs, orc.op_sum, root=37)
+    want_sc, _ = orc.scan(xs, orc.op_sum)
+    for r in range(N):
+        assert_bit_equal(res[r][0], want_ar[r], f"allreduce rank {r}")
+        assert_bit_equal(res[r][2], want_sc[r], f"scan rank {r}")
+        assert_bit_equal(res[r][3], want_ar[r], f"allreduce DIRECT rank {r}")
+    assert_bit_equal(res[37][1], want_red, "reduce root 37")
+
+
 def _host_allreduce(c, r, x, op, ordered, pinned, chunk):
     n, dtype = x.size, x.dtype
     if pinned:

@@ -263,6 +263,42 @@ def test_many_peers_blocked_programs(device, P):
                         assert_bit_equal(outs[k].numpy(), want[k], f"{what} {alg.name} P={P} peer {k}")
 
 
+@pytest.mark.parametrize("P", [257, 512, 1000])
+def test_beyond_256_peers(device, P):
+    """No peer cap, as in the reference (src/comm/PeerToPeer.cpp:59-184 take any num_peers): P = 257, 512,
+    1000 — three levels of 16-peer blocks, ragged blocks — every algorithm, every rank kind, aligned (fused
+    blocks) and unaligned (pairwise passes over run-time-sized programs) buckets, bit-exact vs the oracle."""
+    n = 131
+    for dtype, op in ((np.float32, Op.SUM), (np.int64, Op.MAX)):
+        xs = _peer_inputs(dtype, n + 1, P, seed=41)
+        big = [dev(x) for x in xs]
+        fn = orc.OPS[OPNAME[op]]
+        for ins, sl, what in (([b.view(0, n) for b in big], slice(0, n), "aligned"),
+                              ([b.view(1, n) for b in big], slice(1, n + 1), "unaligned")):
+            ys = [x[sl] for x in xs]
+            with np.errstate(all="ignore"):
+                want, _ = orc.allreduce(ys, fn)
+                for rank in (0, 257 % P, P - 1):
+                    out = Bucket(n, dtype)
+                    fmi_amd.reduce_tree(op, Alg.ALLREDUCE, out, ins, rank=rank)
+                    assert_bit_equal(out.numpy(), want[rank], f"{what} allreduce P={P} rank {rank}")
+                for root in (0, P - 3):
+                    want, _ = orc.reduce(ys, fn, root=root)
+                    out = Bucket(n, dtype)
+                    fmi_amd.reduce_tree(op, Alg.REDUCE, out, ins, rank=root)
+                    assert_bit_equal(out.numpy(), want, f"{what} reduce P={P} root {root}")
+                want, _ = orc.reduce(ys, fn, root=0, commutative=False, associative=False)
+                out = Bucket(n, dtype)
+                fmi_amd.reduce_tree(op, Alg.REDUCE_LTR, out, ins)
+                assert_bit_equal(out.numpy(), want, f"{what} reduce_ltr P={P}")
+                for alg, ordered in ((Alg.SCAN, False), (Alg.SCAN_LTR, True)):
+                    want, _ = orc.scan(ys, fn, commutative=not ordered, associative=not ordered)
+                    outs = [Bucket(n, dtype) for _ in range(P)]
+                    fmi_amd.scan_peers(op, alg, outs, ins)
+                    for k in range(P):
+                        assert_bit_equal(outs[k].numpy(), want[k], f"{what} {alg.name} P={P} peer {k}")
+
+
 _FIRST_CALL = """
 import numpy as np, fmi_amd
 from fmi_amd import Alg, Bucket, Op
