@@ -87,6 +87,7 @@ SIGNATURES = {
     "fmi_comm_allreduce": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _sz, _vp]),
     "fmi_comm_allreduce_host": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _sz, _sz]),
     "fmi_comm_reduce": (_i, [_vp, _i, _i, _i, _vp, _vp, _sz, _i, _vp]),
+    "fmi_comm_reduce_sendbuf": (_i, [_vp, _i, _i, _i, _vp, _vp, _sz, _i, _vp]),
     "fmi_comm_scan": (_i, [_vp, _i, _i, _i, _vp, _vp, _sz, _vp]),
     "fmi_comm_bcast": (_i, [_vp, _vp, _sz, _i, _vp]),
     "fmi_comm_gather": (_i, [_vp, _vp, _vp, _sz, _i, _vp]),

@@ -99,10 +99,12 @@ class Comm:
                   send.ctypes.data, recv.ctypes.data, send.size, int(chunk))
 
     def reduce(self, op: Op, send: Bucket, recv: Optional[Bucket], root: int, ordered: bool = False,
-               stream=None) -> None:
+               stream=None, sendbuf_partials: bool = False) -> None:
+        """sendbuf_partials=True: `send` ends as the reference leaves peer `rank`'s sendbuf (the partial it
+        forwarded up the binomial tree, reference src/comm/PeerToPeer.cpp:72) — fmi_comm_reduce_sendbuf."""
         alg = Alg.REDUCE_LTR if ordered else Alg.REDUCE
-        _lib.call("fmi_comm_reduce", self.handle, int(op), int(send.dtype), int(alg), _p(send), _p(recv), send.n, root,
-                  _sptr(stream))
+        fn = "fmi_comm_reduce_sendbuf" if sendbuf_partials else "fmi_comm_reduce"
+        _lib.call(fn, self.handle, int(op), int(send.dtype), int(alg), _p(send), _p(recv), send.n, root, _sptr(stream))
 
     def scan(self, op: Op, send: Bucket, recv: Bucket, ordered: bool = False, stream=None) -> None:
         alg = Alg.SCAN_LTR if ordered else Alg.SCAN

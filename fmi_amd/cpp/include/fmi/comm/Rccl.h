@@ -6,10 +6,11 @@
 //
 // The collectives are the C-ABI's sharded schedules (fmi_comm_*): all-to-all of shards, one pass of the
 // fused kernel in the reference's order, all-gather / gather / all-to-all back — so every result has the
-// reference's bracketing (float max/min ties: rank 0's operand order on every rank).
-// Side effects mirrored from the reference: commutative allreduce and scan leave sendbuf = result
-// (reference src/comm/PeerToPeer.cpp:129,183), reduce leaves the root's sendbuf = result (:80); the
-// non-root partials of the reference's reduce are intermediate values and are not reproduced.
+// reference's bracketing, each peer with its own operand order (float max/min ties and NaNs included).
+// Side effects reproduced from the reference: commutative allreduce and scan leave sendbuf = result
+// (reference src/comm/PeerToPeer.cpp:129,183); commutative reduce leaves every peer's sendbuf as the
+// reference does (:72): the partial it forwarded up the binomial tree, the root's = the result
+// (fmi_comm_reduce_sendbuf); the ordered (LTR) collectives leave it intact.
 //
 // Host ingress (config C5), opt-in with set_host_ingress(): the channel then also
 // carries host buckets — the recv buffers FMI's transports fill (reference src/comm/Direct.cpp:36-45).
@@ -98,12 +99,17 @@ public:
         const bool is_root = peer_id == root;
         Staged s(this, sendbuf, true);
         Staged r(this, is_root ? recvbuf : channel_data{nullptr, 0, true}, false);
-        run(fmi_comm_reduce(comm_, d.op, d.dtype, alg, s.ptr(), is_root ? r.ptr() : nullptr, d.count,
-                            static_cast<int>(root), nullptr),
-            "fmi_comm_reduce");
-        if (!is_root) return;
-        r.store();
-        if (!ordered(f)) mirror(sendbuf, recvbuf);
+        if (ordered(f)) {
+            run(fmi_comm_reduce(comm_, d.op, d.dtype, alg, s.ptr(), is_root ? r.ptr() : nullptr, d.count,
+                                static_cast<int>(root), nullptr),
+                "fmi_comm_reduce");
+        } else {  // every sendbuf ends as the reference leaves it
+            run(fmi_comm_reduce_sendbuf(comm_, d.op, d.dtype, alg, s.ptr(), is_root ? r.ptr() : nullptr, d.count,
+                                        static_cast<int>(root), nullptr),
+                "fmi_comm_reduce_sendbuf");
+            s.store();
+        }
+        if (is_root) r.store();
     }
 
     void allreduce(channel_data sendbuf, channel_data recvbuf, raw_function f) override {

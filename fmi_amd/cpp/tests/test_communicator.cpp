@@ -716,9 +716,10 @@ GPU_TEST(host_offload_matches_host_path) {
 // Loopback host channel, selected by the policy for device buckets, results equal to the host path.
 GPU_TEST(rccl_channel_collectives_local_transport) {
     Dev::init(0);
-    for (peer_num P : {2u, 3u, 4u, 8u}) {
+    for (peer_num P : {2u, 3u, 4u, 5u, 8u}) {
         const std::size_t n = 300007;
         std::vector<std::vector<float>> host_ar(P), dev_ar(P), dev_send(P), host_sc(P), dev_sc(P);
+        std::vector<std::vector<float>> host_red_send(P), dev_red_send(P);  // reduce partials (PeerToPeer.cpp:72)
         std::vector<float> host_red, dev_red;
         std::vector<std::string> picked(P);
         with_peers(P, [&](Communicator& c, peer_num p) {
@@ -731,6 +732,7 @@ GPU_TEST(rccl_channel_collectives_local_transport) {
             Data<std::vector<float>> d(synth_f32(n, 5, p)), dr(n);
             c.reduce(d, dr, 1 % P, Function<std::vector<float>>(Op::sum));
             if (p == 1 % P) host_red = dr.get();
+            host_red_send[p] = d.get();
         });
         auto mailbox = std::make_shared<FMI::Comm::Mailbox>();
         std::vector<std::thread> ts;
@@ -752,6 +754,7 @@ GPU_TEST(rccl_channel_collectives_local_transport) {
                     Data<Dev::Bucket<float>> d(synth_f32(n, 5, p)), dr(n);
                     c.reduce(d, dr, 1 % P, Function<Dev::Bucket<float>>(Op::sum));
                     if (p == 1 % P) dev_red = dr.get();
+                    dev_red_send[p] = d.get();
                     Data<Dev::Bucket<int64_t>> b(std::vector<int64_t>{static_cast<int64_t>(p), 9});
                     c.bcast(b, P - 1);
                     if (b.get()[0] != static_cast<int64_t>(P - 1)) throw std::runtime_error("bcast over Rccl");
@@ -770,6 +773,8 @@ GPU_TEST(rccl_channel_collectives_local_transport) {
             CHECK(std::memcmp(host_ar[p].data(), dev_ar[p].data(), n * 4) == 0);
             CHECK(std::memcmp(dev_send[p].data(), dev_ar[p].data(), n * 4) == 0);  // sendbuf = result
             CHECK(std::memcmp(host_sc[p].data(), dev_sc[p].data(), n * 4) == 0);
+            // every peer's sendbuf after reduce: the reference's partial (interior), own bucket (leaf), result (root)
+            CHECK(std::memcmp(host_red_send[p].data(), dev_red_send[p].data(), n * 4) == 0);
         }
         CHECK(host_red.size() == n && dev_red.size() == n && std::memcmp(host_red.data(), dev_red.data(), n * 4) == 0);
     }

@@ -1298,6 +1298,58 @@ int fmi_comm_reduce(fmi_comm_t comm, int op, int dtype, int alg, const void* sen
     return FMI_OK;
 }
 
+// The reference's reduce with its side effect on every sendbuf (PeerToPeer.cpp:59-84): all-to-all of shards
+// -> on every shard owner, the reduce_no_order program with ALL N peers' final values as outputs (fused
+// kReducePartials kernel: N reads, N writes) -> all-to-all back into each rank's `send`; the root then
+// copies its value (the result) into recv. reduce_ltr leaves every sendbuf intact (:44-57), so it is the
+// plain reduce.
+int fmi_comm_reduce_sendbuf(fmi_comm_t comm, int op, int dtype, int alg, void* send, void* recv, size_t n, int root,
+                            fmi_stream_t stream) {
+    if (alg == FMI_ALG_REDUCE_LTR) return fmi_comm_reduce(comm, op, dtype, alg, send, recv, n, root, stream);
+    FMI_COMM_RC(check_common(comm, op, dtype));
+    if (alg != FMI_ALG_REDUCE) return fail(FMI_ERR_INVALID, "reduce: alg must be REDUCE or REDUCE_LTR");
+    Comm* c = static_cast<Comm*>(comm);
+    const int N = c->t->n();
+    if (root < 0 || root >= N) return fail(FMI_ERR_INVALID, "root out of range");
+    if (n == 0) return FMI_OK;
+    if (!send || (c->t->rank() == root && !recv)) return fail(FMI_ERR_INVALID, "null bucket");
+    std::lock_guard<std::mutex> lk(c->mu);
+    hipStream_t s = resolve_stream(stream);
+    const size_t esz = dtype_size(dtype);
+    const bool is_root = c->t->rank() == root;
+    if (N > 1) {
+        const size_t shard = shard_elems(n, N);
+        const size_t padded = shard * N;
+        const char* src = nullptr;
+        FMI_COMM_RC(padded_source(c, n, padded, esz, send, s, &src));
+        char* staging = nullptr;
+        char* partial = nullptr;
+        FMI_COMM_RC(c->scratch(1, padded * esz, s, &staging));
+        FMI_COMM_RC(c->scratch(2, padded * esz, s, &partial));
+        FMI_COMM_RC(c->t->all_to_all(src, staging, shard * esz, s));
+        // transformed id t = (rank - root) mod N (PeerToPeer.cpp:287-293): input t is real rank (t + root) % N,
+        // and output t goes to the block of that real rank (the all-to-all back delivers block j to rank j)
+        std::vector<const void*> ins(N);
+        std::vector<void*> outs(N);
+        for (int t = 0; t < N; ++t) {
+            const int real = (t + root) % N;
+            ins[t] = staging + real * shard * esz;
+            outs[t] = partial + real * shard * esz;
+        }
+        FMI_COMM_RC(reduce_partials(op, dtype, outs.data(), ins.data(), N, shard, s));
+        if (padded == n) {
+            FMI_COMM_RC(c->t->all_to_all(partial, static_cast<char*>(send), shard * esz, s));
+        } else {
+            char* out = nullptr;
+            FMI_COMM_RC(c->scratch(3, padded * esz, s, &out));
+            FMI_COMM_RC(c->t->all_to_all(partial, out, shard * esz, s));
+            FMI_COMM_HIP(hipMemcpyAsync(send, out, n * esz, hipMemcpyDeviceToDevice, s));
+        }
+    }
+    if (is_root && recv != send) FMI_COMM_HIP(hipMemcpyAsync(recv, send, n * esz, hipMemcpyDeviceToDevice, s));
+    return FMI_OK;
+}
+
 int fmi_comm_scan(fmi_comm_t comm, int op, int dtype, int alg, const void* send, void* recv, size_t n,
                   fmi_stream_t stream) {
     FMI_COMM_RC(check_common(comm, op, dtype));

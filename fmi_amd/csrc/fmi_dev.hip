@@ -531,6 +531,24 @@ std::string expr_of(const sched::HostProgram& prog, int v) {
 
 }  // namespace
 
+int reduce_partials(int op, int dtype, void* const* outs, const void* const* ins, int P, size_t n, hipStream_t s) {
+    if (n == 0) return FMI_OK;
+    bool aligned = true;
+    for (int p = 0; p < P; ++p) aligned = aligned && aligned16(ins[p]) && aligned16(outs[p]);
+    if (P >= 2 && P <= sched::kMaxFusedPeers && aligned && is_core_dtype(dtype)) {
+        PeerPtrs ptrs{};
+        for (int p = 0; p < P; ++p) {
+            ptrs.in[p] = ins[p];
+            ptrs.out[p] = outs[p];
+        }
+        return launch_fused_reduce_partials(op, dtype, P, ptrs, n, s);
+    }
+    const sched::HostProgram prog = sched::build_host(sched::kReducePartials, P);
+    if (!prog.ok) return fail(FMI_ERR_INVALID, "schedule construction failed");
+    std::vector<int> values(prog.out.begin(), prog.out.end());
+    return run_program_stepwise(op, dtype, prog, outs, P, values.data(), ins, n, s);
+}
+
 int fail(int code, const std::string& msg) {
     t_last_error = msg;
     return code;

@@ -24,7 +24,7 @@ void fused_one(const PeerPtrs& ptrs, size_t n, int rank, hipStream_t s) {
     const size_t nvec = n / kVecLanes<T>;
     const unsigned grid = static_cast<unsigned>(std::min<size_t>(grid_for(nvec, kFusedBlock), kFusedGridCap));
     const size_t lds = fused_lds_bytes(P, kFusedBlock * 16);
-    if constexpr (ALG == sched::kScan || ALG == sched::kScanLtr || sched::is_carry_alg(ALG))
+    if constexpr (sched::stores_all_outputs(ALG))
         scan_kernel<Op, T, ALG, P><<<grid, kFusedBlock, lds, s>>>(ptrs, n);
     else
         tree_kernel<Op, T, ALG, P, ALL_RANKS><<<grid, kFusedBlock, lds, s>>>(ptrs, n, rank);

@@ -94,6 +94,12 @@ inline bool order_sensitive(int op, int dtype) { return is_float(dtype) && (op =
 int launch_fused_allreduce_wide(int op, int dtype, int P, const PeerPtrs& ptrs, size_t n, int rank, hipStream_t s);
 int launch_fused_reduce(int op, int dtype, int P, const PeerPtrs& ptrs, size_t n, hipStream_t s);
 int launch_fused_reduce_ltr(int op, int dtype, int P, const PeerPtrs& ptrs, size_t n, hipStream_t s);
+// reduce_no_order with every (transformed) peer's final sendbuf stored: ptrs.out[t] for t < P
+int launch_fused_reduce_partials(int op, int dtype, int P, const PeerPtrs& ptrs, size_t n, hipStream_t s);
+// The same for any P and any alignment / dtype (fused kernel where it applies, pairwise passes otherwise):
+// outs[t] = the value transformed peer t of reduce_no_order holds in its sendbuf at the end
+// (src/comm/PeerToPeer.cpp:66-78); ins in transformed order. Defined in fmi_dev.hip.
+int reduce_partials(int op, int dtype, void* const* outs, const void* const* ins, int P, size_t n, hipStream_t s);
 int launch_fused_scan(int op, int dtype, int P, const PeerPtrs& ptrs, size_t n, hipStream_t s);
 int launch_fused_scan_ltr(int op, int dtype, int P, const PeerPtrs& ptrs, size_t n, hipStream_t s);
 // scans for P = 17..31 (alg = sched::kScan or kScanLtr), reached through the two launches above

@@ -37,9 +37,16 @@ enum Alg : int {
     // One 16-peer block of allreduce_no_order (P_all > 32) whose 16 peers all take a pre-fold: 32 inputs,
     // values 16 + j are the partners peer j folds in first; then the 16-peer recursive doubling.
     kAllreducePrefold16 = 7,
+    // reduce_no_order's program with every peer's final value as an output: out[t] is the value transformed
+    // peer t leaves in its sendbuf (the partial it forwarded; a leaf's own bucket; the root's result).
+    kReducePartials = 8,
 };
 
 inline constexpr bool is_carry_alg(int alg) { return alg == kScanCarry || alg == kScanLtrCarry; }
+// Programs whose kernels store every peer's output (not one peer's).
+inline constexpr bool stores_all_outputs(int alg) {
+    return alg == kScan || alg == kScanLtr || is_carry_alg(alg) || alg == kReducePartials;
+}
 inline constexpr int kScanBlock = 16;  // kScanCarry's block: P - 1 <= 15 of its 16 peers are inputs
 
 inline constexpr int kMaxFusedPeers = 16;   // fused single-pass kernels are instantiated for P <= 16
@@ -169,7 +176,8 @@ constexpr void build_into(Prog& prog, int alg, int P) {
             for (int p = pow2; p < P; ++p) cur[p] = cur[p - pow2];
             break;
         }
-        case kReduce: {
+        case kReduce:
+        case kReducePartials: {
             // Binomial tree on transformed ids: in round i every t that is a multiple of 2^(i+1)
             // receives from t + 2^i (if it exists) and combines f(own, received) (:66-78).
             const int rounds = ceil_log2(P);

@@ -233,6 +233,13 @@ int fmi_comm_allreduce_host(fmi_comm_t comm, int op, int dtype, int alg, int pat
 /* alg: FMI_ALG_REDUCE or FMI_ALG_REDUCE_LTR; recv is used on root only (may be NULL elsewhere) */
 int fmi_comm_reduce(fmi_comm_t comm, int op, int dtype, int alg, const void* send, void* recv, size_t n, int root,
                     fmi_stream_t stream);
+/* fmi_comm_reduce with the reference's side effect on every rank's sendbuf (src/comm/PeerToPeer.cpp:59-84,
+ * combine site :72): after the call rank r's `send` holds what reference peer r leaves in its sendbuf —
+ * for FMI_ALG_REDUCE the partial it forwarded up the binomial tree (a leaf's own bucket, the root's
+ * result), for FMI_ALG_REDUCE_LTR its own bucket unchanged (:44-57). recv (root only) gets the result, as
+ * with fmi_comm_reduce. Costs N shard writes on each owner and an all-to-all back instead of a gather. */
+int fmi_comm_reduce_sendbuf(fmi_comm_t comm, int op, int dtype, int alg, void* send, void* recv, size_t n, int root,
+                            fmi_stream_t stream);
 /* alg: FMI_ALG_SCAN or FMI_ALG_SCAN_LTR; rank k receives x0 (+) ... (+) xk */
 int fmi_comm_scan(fmi_comm_t comm, int op, int dtype, int alg, const void* send, void* recv, size_t n,
                   fmi_stream_t stream);

@@ -149,6 +149,37 @@ def test_comm_more_ranks_than_a_fused_kernel_holds(device):
     assert_bit_equal(res[3][1], want_red, "reduce root 3")
 
 
+@pytest.mark.parametrize("N", [2, 3, 5, 8, 20])
+def test_comm_reduce_sendbuf_partials(device, N):
+    """fmi_comm_reduce_sendbuf: every rank's send ends as the reference leaves that peer's sendbuf
+    (src/comm/PeerToPeer.cpp:72 — the partial an interior peer forwarded, a leaf's own bucket, the root's
+    result), i.e. the oracle's second return value; recv on the root is the result. Plain fmi_comm_reduce
+    leaves send untouched (include/fmi_dev.h: the documented divergence), and the ordered reduce_ltr leaves it
+    intact in both (reference :44-57)."""
+    n = 4099
+    for dtype, op in ((np.float32, Op.SUM), (np.int64, Op.MAX), (np.float64, Op.MIN)):
+        xs = [inputs(dtype, n, r, seed=47) for r in range(N)]
+        for root in sorted({0, 1 % N, N - 1}):
+            def body(c, r):
+                s, out = Bucket.from_numpy(xs[r]), Bucket(n, dtype)
+                c.reduce(op, s, out if r == root else None, root, sendbuf_partials=True)
+                plain = Bucket.from_numpy(xs[r])
+                c.reduce(op, plain, None if r != root else Bucket(n, dtype), root)
+                ltr = Bucket.from_numpy(xs[r])
+                c.reduce(op, ltr, None if r != root else Bucket(n, dtype), root, ordered=True, sendbuf_partials=True)
+                fmi_amd.sync()
+                return s.numpy(), out.numpy() if r == root else None, plain.numpy(), ltr.numpy()
+
+            res = run_ranks(N, body)
+            with np.errstate(all="ignore"):
+                want, sends = orc.reduce(xs, orc.OPS[OPNAME[op]], root=root)
+            for r in range(N):
+                assert_bit_equal(res[r][0], sends[r], f"N={N} {op.name} root {root}: sendbuf of rank {r}")
+                assert_bit_equal(res[r][2], xs[r], "plain reduce leaves send untouched")
+                assert_bit_equal(res[r][3], xs[r], "reduce_ltr leaves sendbuf intact")
+            assert_bit_equal(res[root][1], want, f"N={N} {op.name} root {root} result")
+
+
 def test_comm_300_ranks(device):
     """No rank cap (the reference's collectives take any num_peers, src/comm/PeerToPeer.cpp:59-184): a
     300-rank communicator (LOCAL transport, 300 threads on the one GPU). Every shard reduction is a 300-peer
@@ -380,6 +411,48 @@ def test_c4_8peer_1gib_allreduce_full_size(device):
 
     assert all(run_ranks(N, body))
     idx = np.sort(np.random.default_rng(0).choice(n, size=1 << 16, replace=False)).astype(np.uint64)
+    xs = [orc.synthetic_at(np.float32, idx, 42, r) for r in range(N)]
+    want, _ = orc.allreduce(xs, orc.op_sum)
+    assert_bit_equal(want_full[idx.astype(np.int64)], want[0], "sampled oracle check")
+    for b in ins:
+        b.free()
+
+
+def test_c5_host_allreduce_full_size(device):
+    """BASELINE config C5 at the largest size the one-GPU box takes comfortably: 8 LOCAL ranks, each with a
+    256 MiB f32 bucket in page-locked host memory (2 GiB in, 2 GiB out), fmi_comm_allreduce_host with the
+    default 64 MiB chunks (H2D, sharded allreduce and D2H of successive chunks overlapped). Every rank's host
+    result must equal, bit for bit, the single-GPU fused kernel over the same 8 buckets, and the oracle's
+    simulation of the reference's 8-peer allreduce on 2^16 sampled indices."""
+    from fmi_amd import Alg, _lib
+
+    N, n = 8, (256 << 20) // 4
+    ins = [Bucket(n, np.float32).fill_synthetic(42, r) for r in range(N)]
+    ref = Bucket(n, np.float32)
+    fmi_amd.reduce_tree(Op.SUM, Alg.ALLREDUCE, ref, ins)
+    fmi_amd.sync()
+    want_full = ref.numpy()
+    ref.free()
+
+    def body(c, r):
+        s, out = PinnedArray(n, np.float32), PinnedArray(n, np.float32)
+        try:
+            _lib.call("fmi_dev_d2h_async", s.ptr, ins[r].ptr, n * 4, None)
+            _lib.call("fmi_stream_sync", None)
+            out.array[:] = np.float32(np.nan)
+            c.allreduce_host(Op.SUM, s.array, out.array)  # chunk 0 = FMI_TUNE_HOST_CHUNK (64 MiB)
+            same = bool(np.array_equal(out.array.view(np.uint32), want_full.view(np.uint32)))
+            kept = bool(np.array_equal(s.array[:4096], ins[r].view(0, 4096).numpy()))
+        finally:
+            s.free()
+            out.free()
+        return same, kept
+
+    res = run_ranks(N, body)
+    for r, (same, kept) in enumerate(res):
+        assert same, f"rank {r}: host allreduce differs from the single-GPU fused kernel"
+        assert kept, f"rank {r}: send host bucket modified"
+    idx = np.sort(np.random.default_rng(1).choice(n, size=1 << 16, replace=False)).astype(np.uint64)
     xs = [orc.synthetic_at(np.float32, idx, 42, r) for r in range(N)]
     want, _ = orc.allreduce(xs, orc.op_sum)
     assert_bit_equal(want_full[idx.astype(np.int64)], want[0], "sampled oracle check")
