@@ -12,7 +12,8 @@
 //   bare     — the std::transform loop alone, single thread.
 //   omp      — the same loop over all host cores (a CPU roofline, not something FMI does).
 // Inputs: the counter-based generator of SURVEY.md §8d (identical to fmi_dev_fill_synthetic).
-// Output: one JSON object on stdout.
+// Output: one JSON object on stdout; with --dump PATH also the combined bucket as raw bytes (for
+// tests/test_oracle.py, which checks the port's bits against the numpy oracle).
 #include <omp.h>
 
 #include <algorithm>
@@ -82,7 +83,7 @@ double now_ms() {
 }
 
 template <class A, class Elem>
-int run(const std::string& mode, const std::string& op, size_t n, int reps) {
+int run(const std::string& mode, const std::string& op, size_t n, int reps, const std::string& dump) {
     std::vector<A> a(n), b(n), a0;
     fill(a, 42, 0);
     fill(b, 42, 1);
@@ -116,6 +117,11 @@ int run(const std::string& mode, const std::string& op, size_t n, int reps) {
         const A w = elem(a0[i], b[i]);
         bad += std::memcmp(&w, &a[i], sizeof(A)) != 0;
     }
+    if (!dump.empty()) {
+        FILE* f = std::fopen(dump.c_str(), "wb");
+        if (!f || std::fwrite(a.data(), 1, bytes, f) != bytes) return 4;
+        std::fclose(f);
+    }
     std::sort(times.begin(), times.end());
     const double med = times[times.size() / 2];
     const int threads = mode == "omp" ? omp_get_max_threads() : 1;
@@ -130,7 +136,7 @@ int run(const std::string& mode, const std::string& op, size_t n, int reps) {
 }  // namespace
 
 int main(int argc, char** argv) {
-    std::string mode = "adapter", dtype = "f32", op = "sum";
+    std::string mode = "adapter", dtype = "f32", op = "sum", dump;
     double mib = 256;
     int reps = 5;
     for (int i = 1; i + 1 < argc; i += 2) {
@@ -140,6 +146,7 @@ int main(int argc, char** argv) {
         else if (k == "--op") op = v;
         else if (k == "--mib") mib = std::atof(v.c_str());
         else if (k == "--reps") reps = std::atoi(v.c_str());
+        else if (k == "--dump") dump = v;
         else {
             std::fprintf(stderr, "unknown option %s\n", k.c_str());
             return 2;
@@ -149,9 +156,9 @@ int main(int argc, char** argv) {
     const size_t bytes = static_cast<size_t>(mib * (1 << 20));
     const bool mx = op == "max";
     if (op != "sum" && op != "max") return 2;
-    if (dtype == "f32") return mx ? run<float, MaxOf<float>>(mode, op, bytes / 4, reps) : run<float, std::plus<float>>(mode, op, bytes / 4, reps);
-    if (dtype == "f64") return mx ? run<double, MaxOf<double>>(mode, op, bytes / 8, reps) : run<double, std::plus<double>>(mode, op, bytes / 8, reps);
-    if (dtype == "i32") return mx ? run<int32_t, MaxOf<int32_t>>(mode, op, bytes / 4, reps) : run<int32_t, std::plus<int32_t>>(mode, op, bytes / 4, reps);
-    if (dtype == "i64") return mx ? run<int64_t, MaxOf<int64_t>>(mode, op, bytes / 8, reps) : run<int64_t, std::plus<int64_t>>(mode, op, bytes / 8, reps);
+    if (dtype == "f32") return mx ? run<float, MaxOf<float>>(mode, op, bytes / 4, reps, dump) : run<float, std::plus<float>>(mode, op, bytes / 4, reps, dump);
+    if (dtype == "f64") return mx ? run<double, MaxOf<double>>(mode, op, bytes / 8, reps, dump) : run<double, std::plus<double>>(mode, op, bytes / 8, reps, dump);
+    if (dtype == "i32") return mx ? run<int32_t, MaxOf<int32_t>>(mode, op, bytes / 4, reps, dump) : run<int32_t, std::plus<int32_t>>(mode, op, bytes / 4, reps, dump);
+    if (dtype == "i64") return mx ? run<int64_t, MaxOf<int64_t>>(mode, op, bytes / 8, reps, dump) : run<int64_t, std::plus<int64_t>>(mode, op, bytes / 8, reps, dump);
     return 2;
 }

@@ -55,6 +55,18 @@ def run(c, N, r):
         fmi_amd.sync()
         out["direct_" + np.dtype(dtype).name] = o.numpy()
         c.window_free(w)
+    # a DIRECT allreduce on a user stream, its window freed right away (no sync): fmi_comm_window_free must
+    # drain the device before the barrier that lets the peers free the memory this rank is still reading
+    st = fmi_amd.Stream()
+    n = 3 * 65536 + 5
+    w = c.window(n, np.float32)
+    w.upload(inputs(np.float32, n, r, seed=37))
+    o = Bucket(n, np.float32)
+    c.allreduce(Op.SUM, w, o, path=Path.DIRECT, stream=st)
+    c.window_free(w)
+    st.sync()
+    out["direct_stream_free"] = o.numpy()
+    st.destroy()
     # host buckets through the GPU (config C5's shape), pageable, several chunks
     x = inputs(np.float64, 3 * 4099 + 17, r, seed=36)
     got = np.zeros_like(x)

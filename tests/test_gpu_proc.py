@@ -63,6 +63,9 @@ def test_proc_transport_collectives(device, N, tmp_path):
             want, _ = orc.allreduce([inputs(dtype, n, r, seed=35) for r in range(N)], orc.OPS[op])
             for r in range(N):
                 assert_bit_equal(res[r]["direct_" + np.dtype(dtype).name], want[r], f"direct {op} rank {r}")
+        want, _ = orc.allreduce([inputs(np.float32, 3 * 65536 + 5, r, seed=37) for r in range(N)], orc.op_sum)
+        for r in range(N):
+            assert_bit_equal(res[r]["direct_stream_free"], want[r], f"direct on a user stream, rank {r}")
     assert np.array_equal(res[0]["gather"], np.concatenate([np.arange(1000) + 1000 * j for j in range(N)]))
     for r in range(N):
         assert res[r]["bcast_ok"][0] and res[r]["ring_ok"][0], f"rank {r}"

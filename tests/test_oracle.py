@@ -177,3 +177,32 @@ def test_splitmix64_known_values():
     # whose state is incremented by the golden gamma before mixing, as here).
     assert int(orc.splitmix64(np.array([0], dtype=np.uint64))[0]) == 0xE220A8397B1DCDAF
     assert int(orc.splitmix64(np.array([1234567], dtype=np.uint64))[0]) == 6457827717110365317
+
+
+@pytest.fixture(scope="module")
+def cpu_baseline_exe(tmp_path_factory):
+    import subprocess
+
+    exe = tmp_path_factory.mktemp("cpu_baseline") / "cpu_baseline"
+    src = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle", "cpu_baseline.cpp")
+    subprocess.run(["g++", "-std=c++17", "-O2", "-fopenmp", "-o", str(exe), src], check=True)
+    return exe
+
+
+@pytest.mark.parametrize("mode", ["adapter", "bare", "omp"])
+@pytest.mark.parametrize("dtype,op", [("f32", "sum"), ("i64", "max"), ("f64", "sum"), ("i32", "max")])
+def test_cpu_baseline_port_matches_oracle(cpu_baseline_exe, tmp_path, mode, dtype, op):
+    """bench.py's cpu_baseline leg times oracle/cpu_baseline.cpp (a port of the reference's CPU combine);
+    its combined bucket must equal the numpy oracle's pairwise op on the same synthetic buckets."""
+    import subprocess
+
+    dump = tmp_path / "out.bin"
+    subprocess.run([str(cpu_baseline_exe), "--mode", mode, "--dtype", dtype, "--op", op, "--mib", "1", "--reps", "1",
+                    "--dump", str(dump)], check=True, capture_output=True)
+    dt = {"f32": np.float32, "f64": np.float64, "i32": np.int32, "i64": np.int64}[dtype]
+    got = np.fromfile(dump, dtype=dt)
+    n = (1 << 20) // np.dtype(dt).itemsize
+    a, b = orc.synthetic(dt, n, seed=42, peer=0), orc.synthetic(dt, n, seed=42, peer=1)
+    want = orc.pairwise(op, a, b)
+    u = {4: np.uint32, 8: np.uint64}[np.dtype(dt).itemsize]
+    assert np.array_equal(got.view(u), want.view(u))
