@@ -19,9 +19,14 @@ This restatement is pinned instead by
   (1) the reference's own known-answer tests (reference tests/communicator.cpp:94-254,
       tests/channels.cpp:419-690), including the non-commutative LTR subtraction cases that fix the
       left-to-right order — tests/golden/reference_kats.json;
-  (2) the evaluation-order table traced from the compiled reference in SURVEY.md Appendix B —
-      tests/golden/bracketing.json.
-Both are checked by tests/test_oracle.py.
+  (2) the evaluation-order table of SURVEY.md Appendix B — tests/golden/bracketing.json. The survey traced it
+      from a reference build that needed stand-ins, which by this task's rules pins nothing: it is a third
+      restatement that agrees, not a reference output.
+Both are checked by tests/test_oracle.py. Every reference-held vector is integer, and the commutative
+collectives' integer results do not depend on the order, so the FLOAT EVALUATION ORDER of the commutative
+allreduce / reduce / scan is PARITY UNPINNED: it rests on this restatement's line-by-line reading of
+src/comm/PeerToPeer.cpp:59-184, checked against two independent in-repo restatements (the kernels' programs
+and the C++ channel algorithms). Integer results and the left-to-right (LTR) order are pinned.
 
 Floating point: numpy float32/float64 arithmetic is IEEE round-to-nearest-even with denormals kept,
 the same as the reference's libstdc++ loop compiled without fast-math. Integer arrays wrap modulo 2^bits

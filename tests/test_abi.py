@@ -216,3 +216,20 @@ def test_no_kernel_spills_to_scratch(tmp_path):
         kernels += len(sizes)
         spilled += sum(1 for v in sizes if v != "0")
     assert kernels > 2000 and spilled == 0, f"{spilled} of {kernels} kernels use scratch"
+
+
+def test_header_contract_matches_the_tests():
+    """The C-ABI header states the contract the GPU tests assert (it once said 'rank 0's
+    operand order' while the tests assert each rank's own order): each rank keeps its own operand order;
+    `send` is left untouched by allreduce / reduce / scan (tests/test_gpu_comm.py "send bucket untouched"),
+    and fmi_comm_reduce_sendbuf reproduces the reference's sendbuf partials
+    (test_comm_reduce_sendbuf_partials)."""
+    hdr = open(os.path.join(ROOT, "include", "fmi_dev.h")).read()
+    rccl = open(os.path.join(ROOT, "fmi_amd", "cpp", "include", "fmi", "comm", "Rccl.h")).read()
+    flat = " ".join(re.sub(r"^\s*\*\s?", "", hdr, flags=re.M).split())
+    assert "rank 0's operand order" not in hdr and "rank 0's operand order" not in rccl
+    assert "each rank with its OWN operand order" in flat
+    assert "`send` is never modified by allreduce, reduce or scan" in flat
+    assert "fmi_comm_reduce_sendbuf" in hdr and "fmi_comm_reduce_sendbuf" in rccl
+    gpu_tests = open(os.path.join(ROOT, "tests", "test_gpu_comm.py")).read()
+    assert "send bucket untouched" in gpu_tests and "plain reduce leaves send untouched" in gpu_tests
