@@ -425,6 +425,7 @@ def after_value(args, ar, world, dist, line, proc):
         from fmi_amd.collectives import phase_breakdown
 
         diag["phase_ms"] = phase_breakdown(args.bucket_mib * MIB // 4, dist.group.WORLD)
+        diag["exchange_variants"] = exchange_variants(args, ar)
     if args.diag_direct:
         try:
             ok = ar.check_direct(1 << 20)
@@ -435,6 +436,34 @@ def after_value(args, ar, world, dist, line, proc):
             diag["path_direct"] = f"unavailable: {e}"
     else:
         diag["path_direct"] = "not run (opt-in: --diag-direct)"
+
+
+def exchange_variants(args, ar) -> dict:
+    """The headline step (path TREE, 256 MiB per peer) with each RCCL realisation of its two exchanges:
+    ncclAllToAll or grouped send/recv for the all-to-all (FMI_TUNE_COMM_A2A), ncclAllGather or grouped
+    send/recv of the shard to every peer for the all-gather (FMI_TUNE_COMM_GATHER). Same bytes, same
+    result bits (self-checked); the step time decides the default. Max over ranks."""
+    import fmi_amd
+    from fmi_amd import Tune
+
+    n = args.bucket_mib * MIB // 4
+    steps = max(10, args.steps // 10)
+    out = {}
+    try:
+        for a2a in (0, 1):
+            for gather in (0, 1):
+                fmi_amd.tune_set(Tune.COMM_A2A, a2a)
+                fmi_amd.tune_set(Tune.COMM_GATHER, gather)
+                ms, _, ex = ar.bench(n, steps=steps, warmup=2, sets=2, peers_per_gpu=1, seed=77)
+                res, seed = ex.pop("result")
+                ok = ar.self_check(res, n, seed, width=1024)["ok"]
+                res.free()
+                out[f"a2a_{'grouped' if a2a else 'nccl'}+gather_{'grouped' if gather else 'nccl'}"] = {
+                    "ms_per_step": round(ms, 4), "self_check_ok": ok}
+    finally:
+        fmi_amd.tune_set(Tune.COMM_A2A, 0)
+        fmi_amd.tune_set(Tune.COMM_GATHER, 0)
+    return out
 
 
 def replicated_pairs(args, ar) -> dict:

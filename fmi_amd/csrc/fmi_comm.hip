@@ -45,6 +45,12 @@ constexpr size_t kShardAlign = 64;  // elements: shards stay 256-B aligned for t
 
 int hip_err(const char* what, hipError_t e) { return fail(FMI_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e)); }
 
+long long tune(int key) {
+    long long v = 0;
+    (void)fmi_tune_get(key, &v);
+    return v;
+}
+
 #define FMI_COMM_HIP(call)                                 \
     do {                                                   \
         const hipError_t e_ = (call);                      \
@@ -108,7 +114,6 @@ const RcclApi* rccl_api() {
         FMI_RCCL_SYM(AllReduce)
 #undef FMI_RCCL_SYM
         api.AllToAll = reinterpret_cast<decltype(api.AllToAll)>(dlsym(h, "ncclAllToAll"));
-        if (const char* g = std::getenv("FMI_A2A_GROUPED"); g && g[0] == '1') api.AllToAll = nullptr;
         ok = true;
     });
     if (!ok) {
@@ -200,7 +205,7 @@ public:
     }
 
     int all_to_all(const char* send, char* recv, size_t bytes, hipStream_t s) override {
-        if (api_->AllToAll) {
+        if (api_->AllToAll && tune(FMI_TUNE_COMM_A2A) == 0) {
             FMI_NCCL(api_, AllToAll(send, recv, bytes, ncclUint8, comm_, s));
             return FMI_OK;
         }
@@ -213,7 +218,20 @@ public:
         return FMI_OK;
     }
     int all_gather(const char* send, char* recv, size_t bytes, hipStream_t s) override {
-        FMI_NCCL(api_, AllGather(send, recv, bytes, ncclUint8, comm_, s));
+        if (tune(FMI_TUNE_COMM_GATHER) == 0) {
+            FMI_NCCL(api_, AllGather(send, recv, bytes, ncclUint8, comm_, s));
+            return FMI_OK;
+        }
+        // this rank's shard straight to every peer, one link each (no ring); the local copy on the stream
+        FMI_NCCL(api_, GroupStart());
+        for (int j = 0; j < n_; ++j) {
+            if (j == rank_) continue;
+            FMI_NCCL(api_, Send(send, bytes, ncclUint8, j, comm_, s));
+            FMI_NCCL(api_, Recv(recv + j * bytes, bytes, ncclUint8, j, comm_, s));
+        }
+        FMI_NCCL(api_, GroupEnd());
+        if (bytes && recv + rank_ * bytes != send)
+            FMI_COMM_HIP(hipMemcpyAsync(recv + rank_ * bytes, send, bytes, hipMemcpyDeviceToDevice, s));
         return FMI_OK;
     }
     int gather(const char* send, char* recv, size_t bytes, int root, hipStream_t s) override {

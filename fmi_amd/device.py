@@ -57,6 +57,8 @@ class Tune(enum.IntEnum):
     HOST_ZERO_COPY = 5
     FUSED_INFLIGHT_KIB = 6
     BLOCKS_ONE_PASS = 7
+    COMM_A2A = 8
+    COMM_GATHER = 9
 
 
 NP_DTYPE = {DType.F32: np.float32, DType.F64: np.float64, DType.I32: np.int32, DType.I64: np.int64,

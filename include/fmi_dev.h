@@ -281,13 +281,18 @@ typedef enum {
                                        4 KiB x P, so at most max(2, ceil(budget / (4 P))) workgroups stay
                                        resident per CU (an LDS reservation enforces it); 0 = no cap. Default 64
                                        (fewer concurrent HBM streams at large P) */
-    FMI_TUNE_BLOCKS_ONE_PASS = 7 /* P-way programs beyond 31 peers in one pass over every input (default 1):
+    FMI_TUNE_BLOCKS_ONE_PASS = 7, /* P-way programs beyond 31 peers in one pass over every input (default 1):
                                     scan_no_order over 32..143 peers, reduce_no_order over 17..128 peers,
                                     allreduce_no_order over 32 / 48 / 64 / 80 / 96 / 112 / 128
                                     peers, scan_ltr and
                                     reduce_ltr over 32..128 peers;
                                     0 = the blocked launches (block values through temps; the scan reads
                                     the inputs of blocks >= 1 twice). Same bits either way */
+    FMI_TUNE_COMM_A2A = 8,        /* RCCL transport all-to-all: 0 = ncclAllToAll where librccl has it (default),
+                                    1 = grouped ncclSend / ncclRecv to every peer. Same bytes either way */
+    FMI_TUNE_COMM_GATHER = 9      /* RCCL transport all-gather: 0 = ncclAllGather (default), 1 = grouped
+                                    ncclSend / ncclRecv of this rank's shard to every peer (each peer link
+                                    carries one shard, no ring). Same bytes either way */
 } fmi_tune_key_t;
 int fmi_tune_set(int key, long long value);
 int fmi_tune_get(int key, long long* value);

@@ -139,6 +139,13 @@ def test_tuning_knobs_validate():
     fmi_amd.tune_set(fmi_amd.Tune.BLOCKS_ONE_PASS, 1)
     with pytest.raises(fmi_amd.FmiError):
         fmi_amd.tune_set(fmi_amd.Tune.BLOCKS_ONE_PASS, 2)
+    for key in (fmi_amd.Tune.COMM_A2A, fmi_amd.Tune.COMM_GATHER):  # RCCL exchange realisations
+        assert fmi_amd.tune_get(key) == 0
+        fmi_amd.tune_set(key, 1)
+        assert fmi_amd.tune_get(key) == 1
+        fmi_amd.tune_set(key, 0)
+        with pytest.raises(fmi_amd.FmiError):
+            fmi_amd.tune_set(key, 2)
 
 
 @pytest.mark.parametrize("P", list(range(1, 34)) + [48, 64, 100, 129, 256])

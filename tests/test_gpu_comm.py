@@ -373,10 +373,18 @@ def test_comm_rccl_transport_single_rank(device):
     c = Comm(uid, 1, 0)
     x = inputs(np.float32, 4099, 0)
     s, out = Bucket.from_numpy(x), Bucket(4099, np.float32)
-    for path in (Path.TREE, Path.RCCL):
-        c.allreduce(Op.SUM, s, out, path=path)
-        fmi_amd.sync()
-        assert_bit_equal(out.numpy(), x)
+    try:
+        for a2a in (0, 1):  # ncclAllToAll / grouped send-recv, ncclAllGather / grouped send-recv
+            for gather in (0, 1):
+                fmi_amd.tune_set(fmi_amd.Tune.COMM_A2A, a2a)
+                fmi_amd.tune_set(fmi_amd.Tune.COMM_GATHER, gather)
+                for path in (Path.TREE, Path.RCCL):
+                    c.allreduce(Op.SUM, s, out, path=path)
+                    fmi_amd.sync()
+                    assert_bit_equal(out.numpy(), x)
+    finally:
+        fmi_amd.tune_set(fmi_amd.Tune.COMM_A2A, 0)
+        fmi_amd.tune_set(fmi_amd.Tune.COMM_GATHER, 0)
     c.scan(Op.SUM, s, out)
     c.reduce(Op.SUM, s, out, 0)
     c.bcast(out, 0)
