@@ -441,28 +441,32 @@ def after_value(args, ar, world, dist, line, proc):
 def exchange_variants(args, ar) -> dict:
     """The headline step (path TREE, 256 MiB per peer) with each RCCL realisation of its two exchanges:
     ncclAllToAll or grouped send/recv for the all-to-all (FMI_TUNE_COMM_A2A), ncclAllGather or grouped
-    send/recv of the shard to every peer for the all-gather (FMI_TUNE_COMM_GATHER). Same bytes, same
-    result bits (self-checked); the step time decides the default. Max over ranks."""
+    send/recv of the shard to every peer for the all-gather (FMI_TUNE_COMM_GATHER), and the allreduce
+    pipelined in 4 or 8 chunks (FMI_TUNE_COMM_PIPELINE: chunk k's all-gather on a second communicator while
+    chunk k+1's all-to-all runs). Same bytes, same result bits (self-checked); the step time decides the
+    default. Max over ranks."""
     import fmi_amd
     from fmi_amd import Tune
 
     n = args.bucket_mib * MIB // 4
     steps = max(10, args.steps // 10)
     out = {}
+    variants = [(a2a, gather, 0) for a2a in (0, 1) for gather in (0, 1)] + [(0, 0, 4), (0, 0, 8)]
     try:
-        for a2a in (0, 1):
-            for gather in (0, 1):
-                fmi_amd.tune_set(Tune.COMM_A2A, a2a)
-                fmi_amd.tune_set(Tune.COMM_GATHER, gather)
-                ms, _, ex = ar.bench(n, steps=steps, warmup=2, sets=2, peers_per_gpu=1, seed=77)
-                res, seed = ex.pop("result")
-                ok = ar.self_check(res, n, seed, width=1024)["ok"]
-                res.free()
-                out[f"a2a_{'grouped' if a2a else 'nccl'}+gather_{'grouped' if gather else 'nccl'}"] = {
-                    "ms_per_step": round(ms, 4), "self_check_ok": ok}
+        for a2a, gather, chunks in variants:
+            fmi_amd.tune_set(Tune.COMM_A2A, a2a)
+            fmi_amd.tune_set(Tune.COMM_GATHER, gather)
+            fmi_amd.tune_set(Tune.COMM_PIPELINE, chunks)
+            ms, _, ex = ar.bench(n, steps=steps, warmup=2, sets=2, peers_per_gpu=1, seed=77)
+            res, seed = ex.pop("result")
+            ok = ar.self_check(res, n, seed, width=1024)["ok"]
+            res.free()
+            name = f"a2a_{'grouped' if a2a else 'nccl'}+gather_{'grouped' if gather else 'nccl'}"
+            out[name + (f"+pipeline{chunks}" if chunks else "")] = {"ms_per_step": round(ms, 4), "self_check_ok": ok}
     finally:
         fmi_amd.tune_set(Tune.COMM_A2A, 0)
         fmi_amd.tune_set(Tune.COMM_GATHER, 0)
+        fmi_amd.tune_set(Tune.COMM_PIPELINE, 0)
     return out
 
 

@@ -80,6 +80,8 @@ struct RcclApi {
     ncclResult_t (*AllReduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t);
     // RCCL's native all-to-all (optional symbol; grouped send/recv otherwise)
     ncclResult_t (*AllToAll)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t);
+    // optional: a second communicator for the pipelined allreduce (FMI_TUNE_COMM_PIPELINE)
+    ncclResult_t (*CommSplit)(ncclComm_t, int, int, ncclComm_t*, ncclConfig_t*);
 };
 
 const RcclApi* rccl_api() {
@@ -114,6 +116,7 @@ const RcclApi* rccl_api() {
         FMI_RCCL_SYM(AllReduce)
 #undef FMI_RCCL_SYM
         api.AllToAll = reinterpret_cast<decltype(api.AllToAll)>(dlsym(h, "ncclAllToAll"));
+        api.CommSplit = reinterpret_cast<decltype(api.CommSplit)>(dlsym(h, "ncclCommSplit"));
         ok = true;
     });
     if (!ok) {
@@ -163,6 +166,12 @@ public:
     virtual int agree_max(int64_t* vals, int k, hipStream_t s) = 0;
     virtual int reduce_scatter(int, int, const void*, void*, size_t, hipStream_t) {
         return fail(FMI_ERR_UNSUPPORTED, "path RCCL needs the RCCL transport");
+    }
+    // A second communicator over the same ranks (collective), so two exchanges can be in flight at once on
+    // two streams. nullptr: this transport's exchanges are host-synchronous, use it as is.
+    virtual int split(std::unique_ptr<Transport>* out) {
+        out->reset();
+        return FMI_OK;
     }
     int n() const { return n_; }
     int rank() const { return rank_; }
@@ -333,6 +342,13 @@ public:
     void unmap_window(const std::vector<char*>& peers) override {
         for (int j = 0; j < static_cast<int>(peers.size()); ++j)
             if (j != rank_ && peers[j]) (void)hipIpcCloseMemHandle(peers[j]);
+    }
+    int split(std::unique_ptr<Transport>* out) override {
+        if (!api_->CommSplit) return fail(FMI_ERR_UNSUPPORTED, "librccl lacks ncclCommSplit");
+        ncclComm_t nc = nullptr;
+        FMI_NCCL(api_, CommSplit(comm_, 0, rank_, &nc, nullptr));
+        *out = std::make_unique<RcclTransport>(api_, nc, n_, rank_);
+        return FMI_OK;
     }
     int agree_max(int64_t* vals, int k, hipStream_t s) override {
         int64_t* d = nullptr;
@@ -840,17 +856,53 @@ struct Window {
     char** shards = nullptr;   // device table: peers[j] + bytes (rank j's reduced-shard area), any N
 };
 
+// Streams, events and the second transport of the pipelined allreduce (FMI_TUNE_COMM_PIPELINE).
+struct ChunkPipe {
+    std::unique_ptr<Transport> t2;  // nullptr with LOCAL / PROC: their exchanges are host-synchronous
+    bool split_done = false;
+    hipStream_t gs = nullptr;  // all-gathers
+    hipEvent_t reduced[2] = {}, gathered[2] = {}, start = nullptr;
+    bool ready = false;
+
+    int init(Transport* t) {
+        if (!split_done) {
+            FMI_COMM_RC(t->split(&t2));
+            split_done = true;
+        }
+        if (ready) return FMI_OK;
+        FMI_COMM_HIP(hipStreamCreateWithFlags(&gs, hipStreamNonBlocking));
+        for (int k = 0; k < 2; ++k)
+            for (hipEvent_t* ev : {&reduced[k], &gathered[k]}) FMI_COMM_HIP(hipEventCreateWithFlags(ev, hipEventDisableTiming));
+        FMI_COMM_HIP(hipEventCreateWithFlags(&start, hipEventDisableTiming));
+        ready = true;
+        return FMI_OK;
+    }
+    ~ChunkPipe() {
+        if (gs) {
+            (void)hipStreamSynchronize(gs);
+            (void)hipStreamDestroy(gs);
+        }
+        for (int k = 0; k < 2; ++k)
+            for (hipEvent_t ev : {reduced[k], gathered[k]})
+                if (ev) (void)hipEventDestroy(ev);
+        if (start) (void)hipEventDestroy(start);
+    }
+};
+
 struct Comm {
-    static constexpr int kSlots = 8;  // 0-3: collective scratch; 4-7: host-pipeline chunk slots
+    // 0-3: collective scratch; 4-7: host-pipeline chunk slots; 8-15: pipelined-allreduce slots (2 x 4)
+    static constexpr int kSlots = 16;
     std::unique_ptr<Transport> t;
     std::mutex mu;
     void* buf[kSlots] = {};
     size_t cap[kSlots] = {};
     HostPipe pipe;
+    ChunkPipe chunks;
     std::map<char*, Window> windows;  // keyed by this rank's base
 
     ~Comm() {
         if (pipe.cs) (void)hipStreamSynchronize(pipe.cs);
+        if (chunks.gs) (void)hipStreamSynchronize(chunks.gs);
         // Windows are read by the peers: wait until every rank is done with them (communicators are torn
         // down collectively, as the reference's Communicator destructor finalizes every channel). A path
         // DIRECT collective may have run on any stream of this process and still be reading a peer's window
@@ -1006,6 +1058,63 @@ int allreduce_direct(Comm* c, const Window& w, size_t off, int op, int dtype, in
     return FMI_OK;
 }
 
+// Path TREE pipelined over K chunks (FMI_TUNE_COMM_PIPELINE = K): every chunk is its own sharded allreduce
+// of a sub-range (element-wise, so the bits are those of the whole-bucket call), with chunk c's all-gather
+// on a second stream and communicator while chunk c + 1's all-to-all and kernel run on `s`. Two buffer slots;
+// events order their reuse: the kernel of chunk c + 2 waits until chunk c's gather has read its shard.
+int allreduce_tree_pipelined(Comm* c, int op, int dtype, int alg, const void* send, void* recv, size_t n,
+                             hipStream_t s, size_t K) {
+    const int N = c->t->n();
+    const size_t esz = dtype_size(dtype);
+    ChunkPipe& p = c->chunks;
+    FMI_COMM_RC(p.init(c->t.get()));
+    Transport* tg = p.t2 ? p.t2.get() : c->t.get();
+    const size_t step = kShardAlign * static_cast<size_t>(N);
+    const size_t ce = ((n + K - 1) / K + step - 1) / step * step;  // chunk elements, whole shards
+    const size_t nchunks = (n + ce - 1) / ce;
+    FMI_COMM_HIP(hipEventRecord(p.start, s));
+    FMI_COMM_HIP(hipStreamWaitEvent(p.gs, p.start, 0));  // the gathers follow the caller's earlier work
+    for (size_t k = 0; k < nchunks; ++k) {
+        const int j = static_cast<int>(k & 1);
+        const size_t lo = k * ce;
+        const size_t cn = std::min(ce, n - lo);
+        const size_t shard = shard_elems(cn, N);
+        const size_t padded = shard * N;
+        const char* src = static_cast<const char*>(send) + lo * esz;
+        char* dst = static_cast<char*>(recv) + lo * esz;
+        if (padded != cn) {  // only the last chunk can need padding
+            char* pad = nullptr;
+            FMI_COMM_RC(c->scratch(8 + 4 * j, padded * esz, s, &pad));
+            FMI_COMM_HIP(hipMemcpyAsync(pad, src, cn * esz, hipMemcpyDeviceToDevice, s));
+            FMI_COMM_HIP(hipMemsetAsync(pad + cn * esz, 0, (padded - cn) * esz, s));
+            src = pad;
+        }
+        char* staging = nullptr;
+        char* red = nullptr;
+        FMI_COMM_RC(c->scratch(9 + 4 * j, padded * esz, s, &staging));
+        if (k >= 2) FMI_COMM_HIP(hipStreamWaitEvent(s, p.gathered[j], 0));  // chunk k - 2 has read red[j]
+        FMI_COMM_RC(c->scratch(10 + 4 * j, shard * esz, s, &red));
+        FMI_COMM_RC(c->t->all_to_all(src, staging, shard * esz, s));
+        std::vector<const void*> parts(N);
+        for (int r = 0; r < N; ++r) parts[r] = staging + r * shard * esz;
+        FMI_COMM_RC(fmi_dev_reduce_tree(op, dtype, alg, red, parts.data(), N, 0, shard, s));
+        FMI_COMM_HIP(hipEventRecord(p.reduced[j], s));
+        FMI_COMM_HIP(hipStreamWaitEvent(p.gs, p.reduced[j], 0));
+        if (padded == cn) {
+            FMI_COMM_RC(tg->all_gather(red, dst, shard * esz, p.gs));
+        } else {
+            char* out = nullptr;
+            FMI_COMM_RC(c->scratch(11 + 4 * j, padded * esz, p.gs, &out));
+            FMI_COMM_RC(tg->all_gather(red, out, shard * esz, p.gs));
+            FMI_COMM_HIP(hipMemcpyAsync(dst, out, cn * esz, hipMemcpyDeviceToDevice, p.gs));
+        }
+        FMI_COMM_HIP(hipEventRecord(p.gathered[j], p.gs));
+    }
+    // the caller's stream sees the whole result
+    FMI_COMM_HIP(hipStreamWaitEvent(s, p.gathered[(nchunks - 1) & 1], 0));
+    return FMI_OK;
+}
+
 // The sharded allreduce of one device bucket on stream s (caller holds c->mu; arguments validated).
 int allreduce_device(Comm* c, int op, int dtype, int alg, int path, const void* send, void* recv, size_t n,
                      hipStream_t s) {
@@ -1025,6 +1134,12 @@ int allreduce_device(Comm* c, int op, int dtype, int alg, int path, const void* 
         const Window* w = c->window_of(send, n * esz, &off);
         if (!w) return fail(FMI_ERR_INVALID, "path DIRECT: send must lie inside a window from fmi_comm_window_alloc");
         if (!per_rank) return allreduce_direct(c, *w, off, op, dtype, alg, recv, n, s);
+    }
+    if (path == FMI_PATH_TREE && !per_rank) {
+        const long long K = tune(FMI_TUNE_COMM_PIPELINE);
+        // worth it only for chunks of at least 1 MiB per rank
+        if (K >= 2 && n * esz / static_cast<size_t>(K) >= (size_t(1) << 20) * static_cast<size_t>(N))
+            return allreduce_tree_pipelined(c, op, dtype, alg, send, recv, n, s, static_cast<size_t>(K));
     }
     const size_t shard = shard_elems(n, N);
     const size_t padded = shard * N;

@@ -37,10 +37,11 @@ DeviceState g_state;  // one process drives one device (one process per GPU, as 
 
 // Defaults from tools/tune_pair.py on MI355X (C2, 256 MiB f32): nontemporal one-shot tiles, 4 × 16 B per
 // operand per thread, 256-thread workgroups — 125 µs = 6.4 TB/s vs 142 µs for plain loads/stores.
-std::atomic<long long> g_tune[10] = {2 /*variant: nontemporal tiles*/, 4 /*unroll*/, 256 /*block*/,
+std::atomic<long long> g_tune[11] = {2 /*variant: nontemporal tiles*/, 4 /*unroll*/, 256 /*block*/,
                                      8 /*grid per CU*/, 64ll << 20 /*host chunk*/, 1 /*host zero-copy*/,
                                      64 /*fused in-flight KiB per CU (tools/ab_fused_cap.py)*/,
-                                     1 /*one-pass blocked scan*/, 0 /*ncclAllToAll*/, 0 /*ncclAllGather*/};
+                                     1 /*one-pass blocked scan*/, 0 /*ncclAllToAll*/, 0 /*ncclAllGather*/,
+                                     0 /*no allreduce pipelining*/};
 
 int hip_fail(const char* what, hipError_t e) {
     return fail(FMI_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
@@ -994,6 +995,9 @@ int fmi_tune_set(int key, long long value) {
         case FMI_TUNE_COMM_GATHER:
             if (value != 0 && value != 1) return fail(FMI_ERR_INVALID, "exchange variant must be 0 or 1");
             break;
+        case FMI_TUNE_COMM_PIPELINE:
+            if (value < 0 || value > 64) return fail(FMI_ERR_INVALID, "pipeline chunks must be in [0, 64]");
+            break;
         default: return fail(FMI_ERR_INVALID, "unknown tuning key");
     }
     g_tune[key].store(value);
@@ -1001,7 +1005,7 @@ int fmi_tune_set(int key, long long value) {
 }
 
 int fmi_tune_get(int key, long long* value) {
-    if (!value || key < 0 || key > FMI_TUNE_COMM_GATHER) return fail(FMI_ERR_INVALID, "bad tuning query");
+    if (!value || key < 0 || key > FMI_TUNE_COMM_PIPELINE) return fail(FMI_ERR_INVALID, "bad tuning query");
     *value = g_tune[key].load();
     return FMI_OK;
 }

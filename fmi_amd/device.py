@@ -59,6 +59,7 @@ class Tune(enum.IntEnum):
     BLOCKS_ONE_PASS = 7
     COMM_A2A = 8
     COMM_GATHER = 9
+    COMM_PIPELINE = 10
 
 
 NP_DTYPE = {DType.F32: np.float32, DType.F64: np.float64, DType.I32: np.int32, DType.I64: np.int64,

@@ -290,9 +290,13 @@ typedef enum {
                                     the inputs of blocks >= 1 twice). Same bits either way */
     FMI_TUNE_COMM_A2A = 8,        /* RCCL transport all-to-all: 0 = ncclAllToAll where librccl has it (default),
                                     1 = grouped ncclSend / ncclRecv to every peer. Same bytes either way */
-    FMI_TUNE_COMM_GATHER = 9      /* RCCL transport all-gather: 0 = ncclAllGather (default), 1 = grouped
+    FMI_TUNE_COMM_GATHER = 9,     /* RCCL transport all-gather: 0 = ncclAllGather (default), 1 = grouped
                                     ncclSend / ncclRecv of this rank's shard to every peer (each peer link
                                     carries one shard, no ring). Same bytes either way */
+    FMI_TUNE_COMM_PIPELINE = 10   /* path TREE allreduce in K chunks (0 or 1 = off, default; 2..64): chunk k's
+                                    all-gather runs on a second stream and communicator (ncclCommSplit)
+                                    while chunk k + 1's all-to-all and kernel run; chunks of >= 1 MiB per
+                                    rank only. Same bits (element-wise); every rank must set the same K */
 } fmi_tune_key_t;
 int fmi_tune_set(int key, long long value);
 int fmi_tune_get(int key, long long* value);

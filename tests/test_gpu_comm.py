@@ -180,6 +180,40 @@ def test_comm_reduce_sendbuf_partials(device, N):
             assert_bit_equal(res[root][1], want, f"N={N} {op.name} root {root} result")
 
 
+@pytest.mark.parametrize("N", [2, 5, 8])
+def test_comm_allreduce_pipelined_chunks(device, N):
+    """FMI_TUNE_COMM_PIPELINE = K: path TREE in K chunks (each its own sharded allreduce; the all-gathers on a
+    second stream). Element-wise, so the result must equal, bit for bit, the single-GPU fused kernel over the
+    whole buckets; ragged n (the last chunk pads its shards); buffer slots reused across calls."""
+    from fmi_amd import Alg
+
+    n = N * (1 << 20) + 12345
+    ins = [Bucket(n, np.float32).fill_synthetic(53, r) for r in range(N)]
+    ref = Bucket(n, np.float32)
+    fmi_amd.reduce_tree(Op.SUM, Alg.ALLREDUCE, ref, ins)
+    fmi_amd.sync()
+    want = ref.numpy()
+    ref.free()
+    try:
+        for K in (3, 4):
+            fmi_amd.tune_set(fmi_amd.Tune.COMM_PIPELINE, K)
+
+            def body(c, r):
+                out = Bucket(n, np.float32)
+                for _ in range(2):  # buffer slots reused across calls
+                    c.allreduce(Op.SUM, ins[r], out)
+                fmi_amd.sync()
+                got = out.numpy()
+                out.free()
+                return bool(np.array_equal(got.view(np.uint32), want.view(np.uint32)))
+
+            assert all(run_ranks(N, body)), f"K={K}"
+    finally:
+        fmi_amd.tune_set(fmi_amd.Tune.COMM_PIPELINE, 0)
+    for b in ins:
+        b.free()
+
+
 def test_comm_300_ranks(device):
     """No rank cap (the reference's collectives take any num_peers, src/comm/PeerToPeer.cpp:59-184): a
     300-rank communicator (LOCAL transport, 300 threads on the one GPU). Every shard reduction is a 300-peer
@@ -378,6 +412,7 @@ def test_comm_rccl_transport_single_rank(device):
             for gather in (0, 1):
                 fmi_amd.tune_set(fmi_amd.Tune.COMM_A2A, a2a)
                 fmi_amd.tune_set(fmi_amd.Tune.COMM_GATHER, gather)
+                fmi_amd.tune_set(fmi_amd.Tune.COMM_PIPELINE, 4 * a2a)
                 for path in (Path.TREE, Path.RCCL):
                     c.allreduce(Op.SUM, s, out, path=path)
                     fmi_amd.sync()
@@ -385,6 +420,7 @@ def test_comm_rccl_transport_single_rank(device):
     finally:
         fmi_amd.tune_set(fmi_amd.Tune.COMM_A2A, 0)
         fmi_amd.tune_set(fmi_amd.Tune.COMM_GATHER, 0)
+        fmi_amd.tune_set(fmi_amd.Tune.COMM_PIPELINE, 0)
     c.scan(Op.SUM, s, out)
     c.reduce(Op.SUM, s, out, 0)
     c.bcast(out, 0)
