@@ -209,9 +209,9 @@ def _headline(args, value, step_ms, workload, parallelism, n, roofline):
     }
 
 
-def _roofline(kernel, algo_bytes, kernel_avg_ms, source, extra=None):
+def _roofline(kernel, algo_bytes, kernel_avg_ms, source, extra=None, pmc_key=None):
     achieved = algo_bytes / (kernel_avg_ms * 1e-3) / 1e9
-    traffic, traffic_src = pmc_traffic(kernel)
+    traffic, traffic_src = pmc_traffic(pmc_key or kernel)
     r = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kernel,
          "kernel_avg_us": round(kernel_avg_ms * 1e3, 2), "algorithmic_bytes_per_launch": algo_bytes,
@@ -353,7 +353,8 @@ def run_dist(args, world, rank, local_rank):
                      "HIP events around back-to-back launches of the same fused shard kernel on the library "
                      "stream, right after the timed region (rotating shard sets), max over ranks",
                      {"launch_shape": kern["kernel"],
-                      "note": "the allreduce step is xGMI-bound (xgmi_roofline); this is its HBM-bound kernel"})
+                      "note": "the allreduce step is xGMI-bound (xgmi_roofline); this is its HBM-bound kernel"},
+                     pmc_key=f"tree_kernel<fmi::dev::OpSum, float, 0, {world}, false>")
     path_desc = {"tree": "all-to-all + fused tree kernel + all-gather (bit-exact)",
                  "rccl": "RCCL reduce-scatter + all-gather", "direct": "fused tree over IPC-mapped peer windows"}
     line = _headline(args, value, step_ms,

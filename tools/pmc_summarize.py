@@ -35,6 +35,9 @@ def main():
     ap.add_argument("--command", required=True)
     ap.add_argument("--no-default", action="store_true",
                     help="do not overwrite profiles/pmc_summary.json (the file bench.py reads for C2)")
+    ap.add_argument("--merge", action="store_true",
+                    help="add these kernels to profiles/pmc_summary.json (replacing same-name entries) instead of "
+                         "overwriting it: e.g. the N > 1 shard kernels beside C2's pair kernel")
     ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                                   "profiles"))
     args = ap.parse_args()
@@ -75,8 +78,16 @@ def main():
         "command": args.command,
         "kernels": kernels,
     }
-    if not args.no_default:
-        with open(os.path.join(args.out, "pmc_summary.json"), "w") as f:
+    default = os.path.join(args.out, "pmc_summary.json")
+    if args.merge and os.path.exists(default):
+        merged = json.load(open(default))
+        names = {k["kernel"] for k in kernels}
+        merged["kernels"] = [k for k in merged["kernels"] if k["kernel"] not in names] + kernels
+        merged.setdefault("merged", []).append({"source": summary["source"], "command": args.command})
+        with open(default, "w") as f:
+            json.dump(merged, f, indent=1)
+    elif not args.no_default:
+        with open(default, "w") as f:
             json.dump(summary, f, indent=1)
     with open(os.path.join(args.out, f"{args.tag}_pmc_summary.json"), "w") as f:
         json.dump(summary, f, indent=1)
