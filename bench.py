@@ -26,6 +26,7 @@ Also reported (one JSON line on rank 0):
   c5            — config C5: the 1 GiB page-locked host bucket through fmi_comm_allreduce_host (H2D +
                   allreduce + D2H pipelined), N = 1 one rank, N > 1 every rank.
   cpu_baseline  — (N = 1) oracle/cpu_baseline (a C++ port of the reference's CPU path) on this host.
+  c3            — (N = 1) config C3's kernels: i64 max pair 64 MiB, f32 peer scan 8 x 64 MiB, fraction of peak.
   diagnostics   — (N > 1) the replicated-pair rate (C2 on every GPU, no exchange), the per-phase breakdown
                   of the exchange and, opt-in, path DIRECT.
 Everything after `value` runs under a per-rank deadline (--diag-deadline); if it expires, rank 0 prints the
@@ -68,6 +69,7 @@ def parse():
                          "exact N>1 code with several ranks on one GPU (tests)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-c5", action="store_true", help="skip the host-bucket (C5) measurement")
+    ap.add_argument("--no-c3", action="store_true", help="N=1: skip the config C3 kernels (i64 max, peer scan)")
     ap.add_argument("--c5-mib", type=int, default=1024, help="host bucket per rank of the c5 block (config C5)")
     ap.add_argument("--no-diagnostics", action="store_true", help="N>1: skip the untimed diagnostics")
     ap.add_argument("--diag-deadline", type=float, default=240.0,
@@ -275,12 +277,64 @@ def run_single(args):
     line["config"]["peers"] = 2
     if not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args)
+    if not args.no_c3:
+        try:
+            line["c3"] = c3_single()
+        except Exception as e:  # reported, never fails the measured line
+            line["c3"] = f"failed: {type(e).__name__}: {e}"
     if not args.no_c5:
         try:
             line["c5"] = c5_single(args.c5_mib)
         except Exception as e:  # reported, never fails the measured line
             line["c5"] = f"failed: {type(e).__name__}: {e}"
     print(json.dumps(line), flush=True)
+
+
+def c3_single(reps: int = 60) -> dict:
+    """Config C3 on this GPU, in the driver's run: the int64 max pairwise combine of 64 MiB buckets (8
+    rotating sets, 1.5 GiB: beyond the 256 MiB MALL) and the f32 peer-axis scan (scan_no_order) of 8 peers x
+    64 MiB (2 rotating sets); mean launch time from two HIP events around back-to-back launches on the library
+    stream, against the algorithmic bytes (3 x 64 MiB and 2 x 8 x 64 MiB)."""
+    import numpy as np
+
+    import fmi_amd
+    from fmi_amd import Alg, Bucket, Event, Op
+
+    def timed(launch, k):
+        for i in range(3):
+            launch(i)
+        e0, e1 = Event(), Event()
+        e0.record()
+        for i in range(k):
+            launch(i)
+        e1.record()
+        e1.sync()
+        ms = e0.elapsed_ms(e1) / k
+        e0.destroy()
+        e1.destroy()
+        return ms
+
+    n64 = 64 * MIB // 8
+    pairs = [(Bucket(n64, np.int64).fill_synthetic(42 + s, 0), Bucket(n64, np.int64).fill_synthetic(42 + s, 1))
+             for s in range(8)]
+    ms_max = timed(lambda i: fmi_amd.reduce_pair(Op.MAX, *pairs[i % 8]), reps)
+    for a, b in pairs:
+        a.free()
+        b.free()
+    P, n32 = 8, 64 * MIB // 4
+    ins = [[Bucket(n32, np.float32).fill_synthetic(7 + s, p) for p in range(P)] for s in range(2)]
+    outs = [[Bucket(n32, np.float32) for _ in range(P)] for _ in range(2)]
+    ms_scan = timed(lambda i: fmi_amd.scan_peers(Op.SUM, Alg.SCAN, outs[i % 2], ins[i % 2]), max(10, reps // 3))
+    for b in [x for s in ins + outs for x in s]:
+        b.free()
+
+    def row(ms, algo):
+        return {"kernel_avg_us": round(ms * 1e3, 2), "algorithmic_bytes": algo,
+                "GB_s": round(algo / (ms * 1e-3) / 1e9, 1), "frac": round(algo / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+
+    return {"i64_max_pair_64MiB": dict(row(ms_max, 3 * 64 * MIB), rotating_sets=8),
+            "f32_scan_P8_64MiB": dict(row(ms_scan, 2 * P * 64 * MIB), rotating_sets=2),
+            "timing": "two HIP events around back-to-back launches on the library stream (gaps included)"}
 
 
 def c5_single(mib: int, iters: int = 3) -> dict:
