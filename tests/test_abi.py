@@ -240,3 +240,29 @@ def test_header_contract_matches_the_tests():
     assert "fmi_comm_reduce_sendbuf" in hdr and "fmi_comm_reduce_sendbuf" in rccl
     gpu_tests = open(os.path.join(ROOT, "tests", "test_gpu_comm.py")).read()
     assert "send bucket untouched" in gpu_tests and "plain reduce leaves send untouched" in gpu_tests
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_programs_combine_every_input_exactly_once(seed):
+    """Structure of the run-time-sized programs at random P up to 2,000 (no peer cap): every reduce /
+    allreduce result combines each of the P inputs exactly once, and scan output k exactly the inputs 0..k
+    (the reference's semantics, whatever the bracketing), for random ranks / roots."""
+    import collections
+    import random
+
+    rng = random.Random(seed)
+    for _ in range(6):
+        P = rng.randint(1, 2000)
+        r = rng.randrange(P)
+        for alg in (Alg.ALLREDUCE, Alg.REDUCE_LTR):
+            leaves = collections.Counter(int(x) for x in re.findall(r"x(\d+)", fmi_amd.schedule_expr(alg, P, r)))
+            assert leaves == collections.Counter(range(P)), (alg, P, r)
+        # reduce works on transformed ids: id 0 (the root) ends with every input; id t > 0 with its binomial
+        # subtree t .. t + 2^(trailing zeros of t) - 1 (the partial it forwarded, PeerToPeer.cpp:72)
+        t = r
+        span = P if t == 0 else (t & -t)
+        leaves = collections.Counter(int(x) for x in re.findall(r"x(\d+)", fmi_amd.schedule_expr(Alg.REDUCE, P, t)))
+        assert leaves == collections.Counter(range(t, min(P, t + span))), (P, t)
+        for alg in (Alg.SCAN, Alg.SCAN_LTR):
+            leaves = collections.Counter(int(x) for x in re.findall(r"x(\d+)", fmi_amd.schedule_expr(alg, P, r)))
+            assert leaves == collections.Counter(range(r + 1)), (alg, P, r)
