@@ -1,5 +1,7 @@
 """One rank of the gloo-bootstrapped CommAllreduce test (tests/test_gpu_bench_dist.py), started by
-torch.multiprocessing: the product N>1 driver code of bench.py (fmi_amd.collectives.CommAllreduce: id
+`torch.distributed.run -m tests._gloo_comm_worker OUTDIR` (a fresh interpreter per rank: the pytest process,
+which already holds the system HIP runtime through libfmi_dev.so, never imports torch and its bundled runtime):
+the product N>1 driver code of bench.py (fmi_amd.collectives.CommAllreduce: id
 broadcast over torch.distributed, bench loop, self-check, path DIRECT check, host-bucket allreduce) over the
 PROC transport, every rank a process on the one GPU. Saves what it computed; the parent compares with the
 oracle (this process makes no oracle call)."""
@@ -8,14 +10,12 @@ import os
 import numpy as np
 
 
-def run(rank, world, port, outdir):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    os.environ.setdefault("FMI_PROC_TIMEOUT_S", "90")
+def run(outdir):
     import torch
     import torch.distributed as dist
 
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rank = int(os.environ["RANK"])
+    dist.init_process_group("gloo")
     try:
         import fmi_amd
         from fmi_amd.collectives import CommAllreduce
@@ -43,3 +43,9 @@ def run(rank, world, port, outdir):
         np.savez(os.path.join(outdir, f"rank{rank}.npz"), **out)
     finally:
         dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    import sys
+
+    run(sys.argv[1])

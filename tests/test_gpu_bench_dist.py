@@ -35,13 +35,13 @@ def _free_port():
 
 
 def test_comm_allreduce_gloo_world2():
-    import torch.multiprocessing as mp
-
-    from tests import _gloo_comm_worker
-
     world, n = 2, 1_000_003
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_gloo_comm_worker.run, args=(world, _free_port(), d), nprocs=world, join=True)
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "-m", "tests._gloo_comm_worker", d]
+        r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=240,
+                           env=dict(os.environ, FMI_PROC_TIMEOUT_S="90", OMP_NUM_THREADS="1"))
+        assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
         res = [dict(np.load(os.path.join(d, f"rank{r}.npz"))) for r in range(world)]
     seed = int(res[0]["tree_seed"][0])
     want, _ = orc.allreduce([orc.synthetic(np.float32, n, seed, p) for p in range(world)], orc.op_sum)
