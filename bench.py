@@ -91,7 +91,7 @@ def pmc_traffic(kernel_substr: str):
         data = json.load(open(path))
         for k in data.get("kernels", []):
             if kernel_substr in k.get("kernel", ""):
-                return k.get("hbm_bytes_per_launch"), data.get("source")
+                return k.get("hbm_bytes_per_launch"), k.get("source", data.get("source"))
     except Exception:
         return None, None
     return None, None

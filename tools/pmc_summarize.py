@@ -78,6 +78,8 @@ def main():
         "command": args.command,
         "kernels": kernels,
     }
+    for k in kernels:  # each entry names its own source once summaries are merged
+        k["source"] = summary["source"]
     default = os.path.join(args.out, "pmc_summary.json")
     if args.merge and os.path.exists(default):
         merged = json.load(open(default))
