@@ -205,8 +205,10 @@ class ShardedAllreduce:
                 ev[k][0].record()
             else:
                 tl = time.perf_counter()
-            for b in pair[1:]:
-                self.engine.reduce_pair(Op.SUM, pair[0], b)
+            if len(pair) == 2:
+                self.engine.reduce_pair(Op.SUM, pair[0], pair[1])
+            elif len(pair) > 2:
+                self.engine.reduce_tree(Op.SUM, Alg.ALLREDUCE, pair[0], pair, rank=0)
             if on_gpu:
                 ev[k][1].record()
             else:
@@ -288,6 +290,8 @@ class CommAllreduce:
 
         from .comm import Path
 
+        if peers_per_gpu & (peers_per_gpu - 1):
+            raise ValueError(f"{peers_per_gpu} peers per GPU: recursive doubling needs a power of two")
         path_name = self.path if path is None else path
         path_id = {"tree": Path.TREE, "rccl": Path.RCCL, "direct": Path.DIRECT}[path_name]
         direct = path_id == Path.DIRECT  # the reduced bucket must live in a symmetric window
@@ -310,8 +314,10 @@ class CommAllreduce:
                 freed[s].wait_on(side)
             if ev:
                 ev[0].record(side)
-            for b in pair[1:]:
-                fdev.reduce_pair(Op.SUM, pair[0], b, stream=side)
+            if len(pair) == 2:  # round 0 of recursive doubling: pairs (2g, 2g+1)
+                fdev.reduce_pair(Op.SUM, pair[0], pair[1], stream=side)
+            elif len(pair) > 2:  # rounds 0..k-1: the 2^k-peer allreduce program over this GPU's peers
+                fdev.reduce_tree(Op.SUM, Alg.ALLREDUCE, pair[0], pair, stream=side)
             if ev:
                 ev[1].record(side)
             if overlap:
