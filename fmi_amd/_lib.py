@@ -12,7 +12,8 @@ import sys
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libfmi_dev.so")
+# FMI_DEV_LIB: another build of the same library (e.g. the host-sanitized one, tools/sanitize_lib.sh)
+LIB_PATH = os.environ.get("FMI_DEV_LIB") or os.path.join(_HERE, "lib", "libfmi_dev.so")
 
 FMI_OK = 0
 FMI_ERR_INVALID = -1
