@@ -412,7 +412,14 @@ class CommAllreduce:
                 mismatches += int(np.count_nonzero(err > bound))
                 worst = max(worst, float(np.max(err / np.maximum(bound, 1e-300))) if w else 0.0)
             else:
-                mismatches += int(np.count_nonzero(got.view(np.uint32) != want.view(np.uint32)))
+                bad = np.nonzero(got.view(np.uint32) != want.view(np.uint32))[0]
+                if bad.size and mismatches == 0:  # where it went wrong, for the log (the line carries counts)
+                    i = int(bad[0])
+                    import sys
+
+                    print(f"self_check rank {r}: first mismatch at element {st + i}: got {got[i]!r} want {want[i]!r} "
+                          f"(shard {(st + i) // shard} of {N})", file=sys.stderr, flush=True)
+                mismatches += int(bad.size)
             checked += w
         for b in peers + [ref]:
             b.free()
