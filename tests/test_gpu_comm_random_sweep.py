@@ -33,7 +33,7 @@ def _cases(seed):
     rng = np.random.default_rng(seed)
     for k in range(CASES):
         N = int(rng.choice([1, 2, 3, 4, 5, 7, 8, 11, 16, 19]))
-        kind = str(rng.choice(["allreduce", "allreduce_direct", "reduce", "scan"]))
+        kind = str(rng.choice(["allreduce", "allreduce_direct", "reduce", "reduce_sendbuf", "scan"]))
         ordered = bool(rng.integers(0, 2))
         op = OPS[int(rng.integers(0, 4))]
         dtype = ALL_DTYPES[int(rng.integers(0, len(ALL_DTYPES)))]
@@ -62,6 +62,10 @@ def test_random_comm_cases(device, seed):
                 return got
             elif kind == "reduce":
                 c.reduce(op, s, out if r == root else None, root, ordered=ordered)
+            elif kind == "reduce_sendbuf":  # every sendbuf as the reference leaves it (PeerToPeer.cpp:72)
+                c.reduce(op, s, out if r == root else None, root, ordered=ordered, sendbuf_partials=True)
+                fmi_amd.sync()
+                return out.numpy(), s.numpy()
             else:
                 c.scan(op, s, out, ordered=ordered)
             fmi_amd.sync()
@@ -78,6 +82,11 @@ def test_random_comm_cases(device, seed):
             elif kind == "reduce":
                 want, _ = orc.reduce(xs, fn, root=root, commutative=not ordered, associative=not ordered)
                 assert_bit_equal(res[root], want, f"{what} root {root}")
+            elif kind == "reduce_sendbuf":
+                want, sends = orc.reduce(xs, fn, root=root, commutative=not ordered, associative=not ordered)
+                assert_bit_equal(res[root][0], want, f"{what} root {root}")
+                for r in range(N):
+                    assert_bit_equal(res[r][1], sends[r], f"{what} sendbuf of rank {r}")
             else:
                 want, _ = orc.scan(xs, fn, commutative=not ordered, associative=not ordered)
                 for r in range(N):
