@@ -1,5 +1,6 @@
-"""Seeded random sweep over the P-way entry points: random P (1..70, so single fused kernels, fused 16-peer
-blocks with ragged last blocks, and the 8/16-bit pairwise-pass programs), algorithm, op, dtype, bucket
+"""Seeded random sweep over the P-way entry points: random P (1..70 mostly, and 130 / 257 / 333 — no peer
+cap — so single fused kernels, one-pass blocked kernels, fused 16-peer block launches over two and three
+levels, ragged last blocks, and the 8/16-bit pairwise-pass programs over run-time-sized schedules), algorithm, op, dtype, bucket
 length and element offset (aligned and unaligned views), every result bit-exact against the oracle's
 simulation of the reference collective. Deterministic: the case list is a function of the seed."""
 import os
@@ -29,7 +30,7 @@ CASES = 160
 def _cases(seed):
     rng = np.random.default_rng(seed)
     for k in range(CASES):
-        P = int(rng.choice([1, 2, 3, 5, 8, 13, 16, 17, 23, 31, 32, 33, 40, 47, 64, 70]))
+        P = int(rng.choice([1, 2, 3, 5, 8, 13, 16, 17, 23, 31, 32, 33, 40, 47, 64, 70, 130, 257, 333]))
         alg = Alg(int(rng.integers(0, 5)))
         op = OPS[int(rng.integers(0, 4))]
         dtype = ALL_DTYPES[int(rng.integers(0, len(ALL_DTYPES)))]
