@@ -142,7 +142,8 @@ int fmi_dev_combine(int op, int dtype, void* out, const void* a, const void* b, 
  * whose operand order is reproduced, which differs only for float MAX/MIN on signed zeros).
  * Replaces the whole chain of f.f calls of reference PeerToPeer::allreduce_no_order / reduce_no_order /
  * reduce_ltr (src/comm/PeerToPeer.cpp:96-130, :59-84, :44-57) for buckets that sit on one device.
- * ins[p] = bucket of peer p (p < P); out may alias any ins[p]. P in [1, 256]. One fused kernel (a single
+ * ins[p] = bucket of peer p (p < P); out may alias any ins[p]. Any P >= 1 (no peer cap, as in the
+ * reference). One fused kernel (a single
  * pass over the P buckets) for P <= 16, and for ALLREDUCE up to 31; larger P as fused sub-programs of the
  * identical order over blocks of 16 peers (every input read once, plus one write and one read per block
  * value). Unaligned buckets and the 8/16-bit dtypes run the same order as pairwise passes. */
@@ -152,7 +153,7 @@ int fmi_dev_reduce_tree(int op, int dtype, int alg, void* out, const void* const
 /* Peer-axis inclusive scan of P device buckets: outs[k] = x0 (+) ... (+) xk with the evaluation order
  * of `alg` (FMI_ALG_SCAN or FMI_ALG_SCAN_LTR). Replaces reference PeerToPeer::scan_no_order / scan_ltr
  * (src/comm/PeerToPeer.cpp:154-184, :141-152) and Communicator::scan (include/Communicator.h:135-150)
- * when the P buckets sit on one device. outs[k] may alias ins[k]. P in [1, 256]: one fused pass up to 31
+ * when the P buckets sit on one device. outs[k] may alias ins[k]. Any P >= 1: one fused pass up to 31
  * peers; beyond, every input is read at most twice (block totals, then the blocks continued from their
  * carry). */
 int fmi_dev_scan_peers(int op, int dtype, int alg, void* const* outs, const void* const* ins, int P,
