@@ -403,10 +403,15 @@ def run_dist(args, world, rank, local_rank):
     check = ar.self_check(out, n, seed, tolerance=args.path == "rccl")
     out.free()
     kern = ar.shard_kernel(n, launches=max(10, min(args.steps, 50)))
-    roof = _roofline("tree_kernel", kern["algorithmic_bytes_per_launch"], kern["kernel_avg_us"] * 1e-3,
-                     "HIP events around back-to-back launches of the same fused shard kernel on the library "
-                     "stream, right after the timed region (rotating shard sets), max over ranks",
-                     {"launch_shape": kern["kernel"],
+    live = extra.pop("shard_kernel_launches") > 0
+    shard_ms = extra.pop("shard_kernel_avg_ms")
+    roof = _roofline("tree_kernel", kern["algorithmic_bytes_per_launch"],
+                     shard_ms if live else kern["kernel_avg_us"] * 1e-3,
+                     ("HIP events recorded by fmi_comm around every shard-kernel launch of the K timed allreduces, "
+                      "on the stream it runs on, mean per launch, max over ranks") if live else
+                     ("HIP events around back-to-back launches of the shard kernel on the library stream after the "
+                      "timed region (N = 1: the allreduce launches no kernel)"),
+                     {"launch_shape": kern["kernel"], "kernel_avg_us_isolated": kern["kernel_avg_us"],
                       "note": "the allreduce step is xGMI-bound (xgmi_roofline); this is its HBM-bound kernel"},
                      pmc_key=f"tree_kernel<fmi::dev::OpSum, float, 0, {world}, false>")
     path_desc = {"tree": "all-to-all + fused tree kernel + all-gather (bit-exact)",

@@ -85,6 +85,8 @@ SIGNATURES = {
     "fmi_comm_size": (_i, [_vp, _c.POINTER(_i), _c.POINTER(_i)]),
     "fmi_comm_window_alloc": (_i, [_vp, _sz, _c.POINTER(_vp)]),
     "fmi_comm_window_free": (_i, [_vp, _vp]),
+    "fmi_comm_timing": (_i, [_vp, _i]),
+    "fmi_comm_timing_read": (_i, [_vp, _c.POINTER(_c.c_float), _c.POINTER(_i)]),
     "fmi_comm_allreduce": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _sz, _vp]),
     "fmi_comm_allreduce_host": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _sz, _sz]),
     "fmi_comm_reduce": (_i, [_vp, _i, _i, _i, _vp, _vp, _sz, _i, _vp]),

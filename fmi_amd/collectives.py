@@ -333,13 +333,16 @@ class CommAllreduce:
         evs = [(fdev.Event(), fdev.Event()) for _ in range(steps)]
         dist.barrier(group=self.group)
         fdev.sync()
+        self.comm.timing(True)  # event pairs around every shard-kernel launch of the timed steps
         t0 = time.perf_counter()
         for k in range(steps):
             step(k, evs[k])
         fdev.sync()
         dist.barrier(group=self.group)
         t1 = time.perf_counter()
-        step_ms = self.max_over_ranks((t1 - t0) * 1e3 / steps)[0]
+        shard_ms, launches = self.comm.timing_read()
+        self.comm.timing(False)
+        step_ms, shard_avg_ms = self.max_over_ranks((t1 - t0) * 1e3 / steps, shard_ms / max(1, launches))
         kernel_ms = [a.elapsed_ms(b) for a, b in evs]
         for a, b in evs:
             a.destroy()
@@ -348,6 +351,8 @@ class CommAllreduce:
         extra = {
             "exchange": f"fmi_comm/{path_name}",
             "transport": self.transport,
+            "shard_kernel_avg_ms": shard_avg_ms,
+            "shard_kernel_launches": launches,
             "shard_elems": self.shard_elems(n),
             "algbw_GiB_s": round(gib / (step_ms * 1e-3), 2),
             "busbw_GiB_s": round(gib / (step_ms * 1e-3) * 2 * (self.world - 1) / self.world, 2),

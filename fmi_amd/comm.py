@@ -67,6 +67,16 @@ class Comm:
         except Exception:
             pass
 
+    def timing(self, enable: bool) -> None:
+        """Record an event pair around every shard-kernel launch of the collectives (fmi_comm_timing)."""
+        _lib.call("fmi_comm_timing", self.handle, 1 if enable else 0)
+
+    def timing_read(self):
+        """(total shard-kernel ms, launches) since timing was enabled or last read."""
+        ms, k = ctypes.c_float(), ctypes.c_int()
+        _lib.call("fmi_comm_timing_read", self.handle, ctypes.byref(ms), ctypes.byref(k))
+        return float(ms.value), int(k.value)
+
     def allreduce(self, op: Op, send: Bucket, recv: Bucket, ordered: bool = False, path: Path = Path.TREE,
                   stream=None) -> None:
         alg = Alg.REDUCE_LTR if ordered else Alg.ALLREDUCE

@@ -889,11 +889,45 @@ struct ChunkPipe {
     }
 };
 
+// Live timing of the shard kernels (fmi_comm_timing): an event pair around every shard-kernel launch of the
+// collectives, on the stream the kernel runs on, read back as a total by fmi_comm_timing_read.
+struct KernelTiming {
+    static constexpr size_t kMaxPairs = 8192;
+    bool on = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> pool;
+    size_t used = 0;
+
+    int begin(hipStream_t s) {
+        if (!on || used >= kMaxPairs) return FMI_OK;
+        if (used == pool.size()) {
+            std::pair<hipEvent_t, hipEvent_t> e{};
+            FMI_COMM_HIP(hipEventCreate(&e.first));
+            FMI_COMM_HIP(hipEventCreate(&e.second));
+            pool.push_back(e);
+        }
+        FMI_COMM_HIP(hipEventRecord(pool[used].first, s));
+        return FMI_OK;
+    }
+    int end(hipStream_t s) {
+        if (!on || used >= kMaxPairs) return FMI_OK;
+        FMI_COMM_HIP(hipEventRecord(pool[used].second, s));
+        ++used;
+        return FMI_OK;
+    }
+    ~KernelTiming() {
+        for (auto& [a, b] : pool) {
+            (void)hipEventDestroy(a);
+            (void)hipEventDestroy(b);
+        }
+    }
+};
+
 struct Comm {
     // 0-3: collective scratch; 4-7: host-pipeline chunk slots; 8-15: pipelined-allreduce slots (2 x 4)
     static constexpr int kSlots = 16;
     std::unique_ptr<Transport> t;
     std::mutex mu;
+    KernelTiming timing;
     void* buf[kSlots] = {};
     size_t cap[kSlots] = {};
     HostPipe pipe;
@@ -1038,7 +1072,9 @@ int allreduce_direct(Comm* c, const Window& w, size_t off, int op, int dtype, in
         std::vector<const void*> ins(N);
         for (int j = 0; j < N; ++j) ins[j] = w.peers[j] + off + lo * esz;
         char* out = w.peers[k] + w.bytes + off + lo * esz;
+        FMI_COMM_RC(c->timing.begin(s));
         FMI_COMM_RC(fmi_dev_reduce_tree(op, dtype, alg, out, ins.data(), N, 0, len, s));
+        FMI_COMM_RC(c->timing.end(s));
     }
     FMI_COMM_RC(c->t->barrier_async(s));
     // Window bases are allocation starts (256-B aligned) and w.bytes is a multiple of 256, so every owner's
@@ -1097,7 +1133,9 @@ int allreduce_tree_pipelined(Comm* c, int op, int dtype, int alg, const void* se
         FMI_COMM_RC(c->t->all_to_all(src, staging, shard * esz, s));
         std::vector<const void*> parts(N);
         for (int r = 0; r < N; ++r) parts[r] = staging + r * shard * esz;
+        FMI_COMM_RC(c->timing.begin(s));
         FMI_COMM_RC(fmi_dev_reduce_tree(op, dtype, alg, red, parts.data(), N, 0, shard, s));
+        FMI_COMM_RC(c->timing.end(s));
         FMI_COMM_HIP(hipEventRecord(p.reduced[j], s));
         FMI_COMM_HIP(hipStreamWaitEvent(p.gs, p.reduced[j], 0));
         if (padded == cn) {
@@ -1154,6 +1192,7 @@ int allreduce_device(Comm* c, int op, int dtype, int alg, int path, const void* 
         std::vector<const void*> parts(N);
         for (int j = 0; j < N; ++j) parts[j] = staging + j * shard * esz;
         if (per_rank) {
+            FMI_COMM_RC(c->timing.begin(s));
             if (N <= sched::kMaxFusedPeers) {
                 PeerPtrs ptrs{};
                 for (int j = 0; j < N; ++j) {
@@ -1165,6 +1204,7 @@ int allreduce_device(Comm* c, int op, int dtype, int alg, int path, const void* 
                 for (int r = 0; r < N; ++r)
                     FMI_COMM_RC(fmi_dev_reduce_tree(op, dtype, alg, red + r * shard * esz, parts.data(), N, r, shard, s));
             }
+            FMI_COMM_RC(c->timing.end(s));
             if (padded == n) return c->t->all_to_all(red, static_cast<char*>(recv), shard * esz, s);
             char* out = nullptr;
             FMI_COMM_RC(c->scratch(3, padded * esz, s, &out));
@@ -1172,7 +1212,9 @@ int allreduce_device(Comm* c, int op, int dtype, int alg, int path, const void* 
             FMI_COMM_HIP(hipMemcpyAsync(recv, out, n * esz, hipMemcpyDeviceToDevice, s));
             return FMI_OK;
         }
+        FMI_COMM_RC(c->timing.begin(s));
         FMI_COMM_RC(fmi_dev_reduce_tree(op, dtype, alg, red, parts.data(), N, 0, shard, s));
+        FMI_COMM_RC(c->timing.end(s));
     } else {
         FMI_COMM_RC(c->t->reduce_scatter(op, dtype, src, red, shard, s));
     }
@@ -1324,6 +1366,33 @@ int fmi_comm_window_free(fmi_comm_t comm, void* ptr) {
     if (it->second.shards) FMI_COMM_HIP(hipFree(it->second.shards));
     FMI_COMM_HIP(hipFree(it->first));
     c->windows.erase(it);
+    return FMI_OK;
+}
+
+int fmi_comm_timing(fmi_comm_t comm, int enable) {
+    if (!comm) return fail(FMI_ERR_INVALID, "null communicator");
+    Comm* c = static_cast<Comm*>(comm);
+    std::lock_guard<std::mutex> lk(c->mu);
+    c->timing.on = enable != 0;
+    c->timing.used = 0;
+    return FMI_OK;
+}
+
+int fmi_comm_timing_read(fmi_comm_t comm, float* total_ms, int* launches) {
+    if (!comm || !total_ms || !launches) return fail(FMI_ERR_INVALID, "null argument");
+    Comm* c = static_cast<Comm*>(comm);
+    std::lock_guard<std::mutex> lk(c->mu);
+    float total = 0.f;
+    for (size_t k = 0; k < c->timing.used; ++k) {
+        auto& [a, b] = c->timing.pool[k];
+        FMI_COMM_HIP(hipEventSynchronize(b));
+        float ms = 0.f;
+        FMI_COMM_HIP(hipEventElapsedTime(&ms, a, b));
+        total += ms;
+    }
+    *total_ms = total;
+    *launches = static_cast<int>(c->timing.used);
+    c->timing.used = 0;
     return FMI_OK;
 }
 

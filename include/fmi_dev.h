@@ -219,6 +219,12 @@ int fmi_comm_size(fmi_comm_t comm, int* nranks, int* rank);
  * a peer's window through its mapping), then barrier with the peers, then unmap and free. */
 int fmi_comm_window_alloc(fmi_comm_t comm, size_t bytes, void** ptr);
 int fmi_comm_window_free(fmi_comm_t comm, void* ptr);
+/* Live timing of the collectives' shard kernels (the fused P-way kernel each rank runs on its shard, path
+ * TREE / DIRECT allreduce): while enabled, an event pair is recorded around every such launch on the stream
+ * it runs on (up to 8192 launches). fmi_comm_timing_read waits for them and returns the summed kernel time
+ * and the launch count, then starts a new tally. Enabling also starts a new tally. */
+int fmi_comm_timing(fmi_comm_t comm, int enable);
+int fmi_comm_timing_read(fmi_comm_t comm, float* total_ms, int* launches);
 /* alg: FMI_ALG_ALLREDUCE (commutative+associative) or FMI_ALG_REDUCE_LTR (ordered) */
 int fmi_comm_allreduce(fmi_comm_t comm, int op, int dtype, int alg, int path, const void* send, void* recv, size_t n,
                        fmi_stream_t stream);

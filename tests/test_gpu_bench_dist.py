@@ -72,5 +72,6 @@ def test_bench_py_proc_transport(world):
     assert line["c4"]["tree"]["self_check"]["ok"]
     assert line["c5"]["result_ok"]
     assert line["roofline"]["algorithmic_bytes_per_launch"] > 0
+    assert "every shard-kernel launch of the K timed allreduces" in line["roofline"]["kernel_avg_source"]
     assert line["config"]["peers"] == world and line["config"]["transport"] == "proc"
     assert "replicated_pairs" in line["diagnostics"]

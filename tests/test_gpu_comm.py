@@ -214,6 +214,33 @@ def test_comm_allreduce_pipelined_chunks(device, N):
         b.free()
 
 
+def test_comm_timing_counts_shard_kernels(device):
+    """fmi_comm_timing: one event pair per shard-kernel launch of the collectives on the stream it runs on
+    (TREE allreduce, DIRECT allreduce, per-rank float max); read returns the tally and starts a new one."""
+    N, n = 3, 65536 + 17
+
+    def body(c, r):
+        s, out = Bucket.from_numpy(inputs(np.float32, n, r)), Bucket(n, np.float32)
+        w = c.window(n, np.float32)
+        w.upload(inputs(np.float32, n, r))
+        c.timing(True)
+        for _ in range(3):
+            c.allreduce(Op.SUM, s, out)
+        c.allreduce(Op.MAX, s, out)  # float max: the per-rank kernel, one launch
+        c.allreduce(Op.SUM, w, out, path=Path.DIRECT)
+        ms, k = c.timing_read()
+        again = c.timing_read()
+        c.timing(False)
+        c.allreduce(Op.SUM, s, out)
+        after = c.timing_read()
+        c.window_free(w)
+        return ms, k, again, after
+
+    for r, (ms, k, again, after) in enumerate(run_ranks(N, body)):
+        assert k == 5 and ms > 0, (r, ms, k)
+        assert again == (0.0, 0) and after == (0.0, 0)
+
+
 def test_comm_300_ranks(device):
     """No rank cap (the reference's collectives take any num_peers, src/comm/PeerToPeer.cpp:59-184): a
     300-rank communicator (LOCAL transport, 300 threads on the one GPU). Every shard reduction is a 300-peer
