@@ -167,6 +167,20 @@ public:
     virtual int reduce_scatter(int, int, const void*, void*, size_t, hipStream_t) {
         return fail(FMI_ERR_UNSUPPORTED, "path RCCL needs the RCCL transport");
     }
+    // Ragged exchanges: shard j covers bytes [j * shard, min(total, (j + 1) * shard)) of a bucket (the last
+    // shards short or empty), so a bucket needs no zero padding. all_to_all_ragged: recv[j * shard ...] = rank
+    // j's shard `rank` (span(rank) bytes); all_gather_ragged: recv[j * shard ...] = rank j's send (span(j)).
+    virtual bool ragged() const { return false; }
+    virtual int all_to_all_ragged(const char*, char*, size_t, size_t, hipStream_t) {
+        return fail(FMI_ERR_UNSUPPORTED, "transport has no ragged exchanges");
+    }
+    virtual int all_gather_ragged(const char*, char*, size_t, size_t, hipStream_t) {
+        return fail(FMI_ERR_UNSUPPORTED, "transport has no ragged exchanges");
+    }
+    static size_t span(int j, size_t shard, size_t total) {
+        const size_t lo = static_cast<size_t>(j) * shard;
+        return lo >= total ? 0 : std::min(shard, total - lo);
+    }
     // A second communicator over the same ranks (collective), so two exchanges can be in flight at once on
     // two streams. nullptr: this transport's exchanges are host-synchronous, use it as is.
     virtual int split(std::unique_ptr<Transport>* out) {
@@ -241,6 +255,34 @@ public:
         FMI_NCCL(api_, GroupEnd());
         if (bytes && recv + rank_ * bytes != send)
             FMI_COMM_HIP(hipMemcpyAsync(recv + rank_ * bytes, send, bytes, hipMemcpyDeviceToDevice, s));
+        return FMI_OK;
+    }
+    // Exact lengths through grouped send / recv: both sides of a pair compute the same length and skip an
+    // empty one alike.
+    bool ragged() const override { return true; }
+    int all_to_all_ragged(const char* send, char* recv, size_t shard, size_t total, hipStream_t s) override {
+        const size_t mine = span(rank_, shard, total);
+        FMI_NCCL(api_, GroupStart());
+        for (int j = 0; j < n_; ++j) {
+            const size_t out = span(j, shard, total);
+            if (out) FMI_NCCL(api_, Send(send + j * shard, out, ncclUint8, j, comm_, s));
+            if (mine) FMI_NCCL(api_, Recv(recv + j * shard, mine, ncclUint8, j, comm_, s));
+        }
+        FMI_NCCL(api_, GroupEnd());
+        return FMI_OK;
+    }
+    int all_gather_ragged(const char* send, char* recv, size_t shard, size_t total, hipStream_t s) override {
+        const size_t mine = span(rank_, shard, total);
+        FMI_NCCL(api_, GroupStart());
+        for (int j = 0; j < n_; ++j) {
+            if (j == rank_) continue;
+            const size_t in = span(j, shard, total);
+            if (mine) FMI_NCCL(api_, Send(send, mine, ncclUint8, j, comm_, s));
+            if (in) FMI_NCCL(api_, Recv(recv + j * shard, in, ncclUint8, j, comm_, s));
+        }
+        FMI_NCCL(api_, GroupEnd());
+        if (mine && recv + rank_ * shard != send)
+            FMI_COMM_HIP(hipMemcpyAsync(recv + rank_ * shard, send, mine, hipMemcpyDeviceToDevice, s));
         return FMI_OK;
     }
     int gather(const char* send, char* recv, size_t bytes, int root, hipStream_t s) override {
@@ -419,6 +461,25 @@ public:
         return exchange(send, s, [&](const std::vector<const char*>& all) -> int {
             for (int j = 0; j < n_; ++j)
                 if (bytes) FMI_COMM_HIP(hipMemcpyAsync(recv + j * bytes, all[j], bytes, hipMemcpyDeviceToDevice, s));
+            return FMI_OK;
+        });
+    }
+    bool ragged() const override { return true; }
+    int all_to_all_ragged(const char* send, char* recv, size_t shard, size_t total, hipStream_t s) override {
+        const size_t mine = span(rank_, shard, total);
+        return exchange(send, s, [&](const std::vector<const char*>& all) -> int {
+            for (int j = 0; j < n_; ++j)
+                if (mine) FMI_COMM_HIP(hipMemcpyAsync(recv + j * shard, all[j] + rank_ * shard, mine, hipMemcpyDeviceToDevice, s));
+            return FMI_OK;
+        });
+    }
+    int all_gather_ragged(const char* send, char* recv, size_t shard, size_t total, hipStream_t s) override {
+        return exchange(send, s, [&](const std::vector<const char*>& all) -> int {
+            for (int j = 0; j < n_; ++j) {
+                const size_t in = span(j, shard, total);
+                if (in && recv + j * shard != all[j])
+                    FMI_COMM_HIP(hipMemcpyAsync(recv + j * shard, all[j], in, hipMemcpyDeviceToDevice, s));
+            }
             return FMI_OK;
         });
     }
@@ -1181,6 +1242,23 @@ int allreduce_device(Comm* c, int op, int dtype, int alg, int path, const void* 
     }
     const size_t shard = shard_elems(n, N);
     const size_t padded = shard * N;
+    if (padded != n && path == FMI_PATH_TREE && !per_rank && c->t->ragged()) {
+        // no zero-padded copies in or out: the last shards are short (or empty) and move at their length
+        char* staging = nullptr;
+        char* red = nullptr;
+        FMI_COMM_RC(c->scratch(1, padded * esz, s, &staging));
+        FMI_COMM_RC(c->scratch(2, shard * esz, s, &red));
+        FMI_COMM_RC(c->t->all_to_all_ragged(static_cast<const char*>(send), staging, shard * esz, n * esz, s));
+        const size_t len = Transport::span(c->t->rank(), shard, n);  // elements of my shard
+        if (len) {
+            std::vector<const void*> parts(N);
+            for (int j = 0; j < N; ++j) parts[j] = staging + j * shard * esz;
+            FMI_COMM_RC(c->timing.begin(s));
+            FMI_COMM_RC(fmi_dev_reduce_tree(op, dtype, alg, red, parts.data(), N, 0, len, s));
+            FMI_COMM_RC(c->timing.end(s));
+        }
+        return c->t->all_gather_ragged(red, static_cast<char*>(recv), shard * esz, n * esz, s);
+    }
     const char* src = nullptr;
     FMI_COMM_RC(padded_source(c, n, padded, esz, send, s, &src));
     char* red = nullptr;
