@@ -177,6 +177,15 @@ public:
     virtual int all_gather_ragged(const char*, char*, size_t, size_t, hipStream_t) {
         return fail(FMI_ERR_UNSUPPORTED, "transport has no ragged exchanges");
     }
+    // gather_ragged: root's recv[j * shard ...] = rank j's send (span(j) bytes).
+    virtual int gather_ragged(const char*, char*, size_t, size_t, int, hipStream_t) {
+        return fail(FMI_ERR_UNSUPPORTED, "transport has no ragged exchanges");
+    }
+    // all_to_all_back_ragged: recv[j * shard ...] = rank j's send[rank * shard ...] (span(j) bytes): the
+    // inverse of all_to_all_ragged, every owner handing each rank its version of the owner's shard.
+    virtual int all_to_all_back_ragged(const char*, char*, size_t, size_t, hipStream_t) {
+        return fail(FMI_ERR_UNSUPPORTED, "transport has no ragged exchanges");
+    }
     static size_t span(int j, size_t shard, size_t total) {
         const size_t lo = static_cast<size_t>(j) * shard;
         return lo >= total ? 0 : std::min(shard, total - lo);
@@ -283,6 +292,32 @@ public:
         FMI_NCCL(api_, GroupEnd());
         if (mine && recv + rank_ * shard != send)
             FMI_COMM_HIP(hipMemcpyAsync(recv + rank_ * shard, send, mine, hipMemcpyDeviceToDevice, s));
+        return FMI_OK;
+    }
+    int gather_ragged(const char* send, char* recv, size_t shard, size_t total, int root, hipStream_t s) override {
+        const size_t mine = span(rank_, shard, total);
+        FMI_NCCL(api_, GroupStart());
+        if (rank_ == root) {
+            for (int j = 0; j < n_; ++j) {
+                const size_t in = span(j, shard, total);
+                if (j != root && in) FMI_NCCL(api_, Recv(recv + j * shard, in, ncclUint8, j, comm_, s));
+            }
+        } else if (mine) {
+            FMI_NCCL(api_, Send(send, mine, ncclUint8, root, comm_, s));
+        }
+        FMI_NCCL(api_, GroupEnd());
+        if (rank_ == root && mine) FMI_COMM_HIP(hipMemcpyAsync(recv + root * shard, send, mine, hipMemcpyDeviceToDevice, s));
+        return FMI_OK;
+    }
+    int all_to_all_back_ragged(const char* send, char* recv, size_t shard, size_t total, hipStream_t s) override {
+        const size_t mine = span(rank_, shard, total);
+        FMI_NCCL(api_, GroupStart());
+        for (int j = 0; j < n_; ++j) {
+            const size_t in = span(j, shard, total);
+            if (mine) FMI_NCCL(api_, Send(send + j * shard, mine, ncclUint8, j, comm_, s));
+            if (in) FMI_NCCL(api_, Recv(recv + j * shard, in, ncclUint8, j, comm_, s));
+        }
+        FMI_NCCL(api_, GroupEnd());
         return FMI_OK;
     }
     int gather(const char* send, char* recv, size_t bytes, int root, hipStream_t s) override {
@@ -479,6 +514,25 @@ public:
                 const size_t in = span(j, shard, total);
                 if (in && recv + j * shard != all[j])
                     FMI_COMM_HIP(hipMemcpyAsync(recv + j * shard, all[j], in, hipMemcpyDeviceToDevice, s));
+            }
+            return FMI_OK;
+        });
+    }
+    int gather_ragged(const char* send, char* recv, size_t shard, size_t total, int root, hipStream_t s) override {
+        return exchange(send, s, [&](const std::vector<const char*>& all) -> int {
+            if (rank_ != root) return FMI_OK;
+            for (int j = 0; j < n_; ++j) {
+                const size_t in = span(j, shard, total);
+                if (in) FMI_COMM_HIP(hipMemcpyAsync(recv + j * shard, all[j], in, hipMemcpyDeviceToDevice, s));
+            }
+            return FMI_OK;
+        });
+    }
+    int all_to_all_back_ragged(const char* send, char* recv, size_t shard, size_t total, hipStream_t s) override {
+        return exchange(send, s, [&](const std::vector<const char*>& all) -> int {
+            for (int j = 0; j < n_; ++j) {
+                const size_t in = span(j, shard, total);
+                if (in) FMI_COMM_HIP(hipMemcpyAsync(recv + j * shard, all[j] + rank_ * shard, in, hipMemcpyDeviceToDevice, s));
             }
             return FMI_OK;
         });
@@ -1559,17 +1613,23 @@ int fmi_comm_reduce(fmi_comm_t comm, int op, int dtype, int alg, const void* sen
     }
     const size_t shard = shard_elems(n, N);
     const size_t padded = shard * N;
-    const char* src = nullptr;
-    FMI_COMM_RC(padded_source(c, n, padded, esz, send, s, &src));
+    const bool is_root = c->t->rank() == root;
     char* staging = nullptr;
     char* red = nullptr;
     FMI_COMM_RC(c->scratch(1, padded * esz, s, &staging));
     FMI_COMM_RC(c->scratch(2, shard * esz, s, &red));
-    FMI_COMM_RC(c->t->all_to_all(src, staging, shard * esz, s));
     std::vector<const void*> parts(N);
     for (int j = 0; j < N; ++j) parts[j] = staging + j * shard * esz;
+    if (padded != n && c->t->ragged()) {  // short last shards at their own length: no padded copies
+        FMI_COMM_RC(c->t->all_to_all_ragged(static_cast<const char*>(send), staging, shard * esz, n * esz, s));
+        const size_t len = Transport::span(c->t->rank(), shard, n);
+        FMI_COMM_RC(fmi_dev_reduce_tree(op, dtype, alg, red, parts.data(), N, root, len, s));
+        return c->t->gather_ragged(red, is_root ? static_cast<char*>(recv) : nullptr, shard * esz, n * esz, root, s);
+    }
+    const char* src = nullptr;
+    FMI_COMM_RC(padded_source(c, n, padded, esz, send, s, &src));
+    FMI_COMM_RC(c->t->all_to_all(src, staging, shard * esz, s));
     FMI_COMM_RC(fmi_dev_reduce_tree(op, dtype, alg, red, parts.data(), N, root, shard, s));
-    const bool is_root = c->t->rank() == root;
     if (padded == n) return c->t->gather(red, is_root ? static_cast<char*>(recv) : nullptr, shard * esz, root, s);
     char* out = nullptr;
     FMI_COMM_RC(c->scratch(3, padded * esz, s, &out));
@@ -1600,13 +1660,18 @@ int fmi_comm_reduce_sendbuf(fmi_comm_t comm, int op, int dtype, int alg, void* s
     if (N > 1) {
         const size_t shard = shard_elems(n, N);
         const size_t padded = shard * N;
-        const char* src = nullptr;
-        FMI_COMM_RC(padded_source(c, n, padded, esz, send, s, &src));
+        const bool ragged = padded != n && c->t->ragged();  // short last shards at their own length
         char* staging = nullptr;
         char* partial = nullptr;
         FMI_COMM_RC(c->scratch(1, padded * esz, s, &staging));
         FMI_COMM_RC(c->scratch(2, padded * esz, s, &partial));
-        FMI_COMM_RC(c->t->all_to_all(src, staging, shard * esz, s));
+        if (ragged) {
+            FMI_COMM_RC(c->t->all_to_all_ragged(static_cast<const char*>(send), staging, shard * esz, n * esz, s));
+        } else {
+            const char* src = nullptr;
+            FMI_COMM_RC(padded_source(c, n, padded, esz, send, s, &src));
+            FMI_COMM_RC(c->t->all_to_all(src, staging, shard * esz, s));
+        }
         // transformed id t = (rank - root) mod N (PeerToPeer.cpp:287-293): input t is real rank (t + root) % N,
         // and output t goes to the block of that real rank (the all-to-all back delivers block j to rank j)
         std::vector<const void*> ins(N);
@@ -1616,8 +1681,11 @@ int fmi_comm_reduce_sendbuf(fmi_comm_t comm, int op, int dtype, int alg, void* s
             ins[t] = staging + real * shard * esz;
             outs[t] = partial + real * shard * esz;
         }
-        FMI_COMM_RC(reduce_partials(op, dtype, outs.data(), ins.data(), N, shard, s));
-        if (padded == n) {
+        const size_t len = ragged ? Transport::span(c->t->rank(), shard, n) : shard;
+        FMI_COMM_RC(reduce_partials(op, dtype, outs.data(), ins.data(), N, len, s));
+        if (ragged) {
+            FMI_COMM_RC(c->t->all_to_all_back_ragged(partial, static_cast<char*>(send), shard * esz, n * esz, s));
+        } else if (padded == n) {
             FMI_COMM_RC(c->t->all_to_all(partial, static_cast<char*>(send), shard * esz, s));
         } else {
             char* out = nullptr;
@@ -1647,19 +1715,25 @@ int fmi_comm_scan(fmi_comm_t comm, int op, int dtype, int alg, const void* send,
     }
     const size_t shard = shard_elems(n, N);
     const size_t padded = shard * N;
-    const char* src = nullptr;
-    FMI_COMM_RC(padded_source(c, n, padded, esz, send, s, &src));
     char* staging = nullptr;
     char* prefix = nullptr;
     FMI_COMM_RC(c->scratch(1, padded * esz, s, &staging));
     FMI_COMM_RC(c->scratch(2, padded * esz, s, &prefix));
-    FMI_COMM_RC(c->t->all_to_all(src, staging, shard * esz, s));
     std::vector<const void*> ins(N);
     std::vector<void*> outs(N);
     for (int j = 0; j < N; ++j) {
         ins[j] = staging + j * shard * esz;
         outs[j] = prefix + j * shard * esz;  // prefix of rank j over my shard
     }
+    if (padded != n && c->t->ragged()) {  // short last shards at their own length: no padded copies
+        FMI_COMM_RC(c->t->all_to_all_ragged(static_cast<const char*>(send), staging, shard * esz, n * esz, s));
+        const size_t len = Transport::span(c->t->rank(), shard, n);
+        FMI_COMM_RC(fmi_dev_scan_peers(op, dtype, alg, outs.data(), ins.data(), N, len, s));
+        return c->t->all_to_all_back_ragged(prefix, static_cast<char*>(recv), shard * esz, n * esz, s);
+    }
+    const char* src = nullptr;
+    FMI_COMM_RC(padded_source(c, n, padded, esz, send, s, &src));
+    FMI_COMM_RC(c->t->all_to_all(src, staging, shard * esz, s));
     FMI_COMM_RC(fmi_dev_scan_peers(op, dtype, alg, outs.data(), ins.data(), N, shard, s));
     // rank k gathers its prefix shard j from rank j: an all-to-all back
     if (padded == n) return c->t->all_to_all(prefix, static_cast<char*>(recv), shard * esz, s);
