@@ -16,6 +16,8 @@
 #include <dlfcn.h>
 #include <fcntl.h>
 #include <rccl/rccl.h>
+
+#include "fmi_exchange_plan.h"
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -186,10 +188,7 @@ public:
     virtual int all_to_all_back_ragged(const char*, char*, size_t, size_t, hipStream_t) {
         return fail(FMI_ERR_UNSUPPORTED, "transport has no ragged exchanges");
     }
-    static size_t span(int j, size_t shard, size_t total) {
-        const size_t lo = static_cast<size_t>(j) * shard;
-        return lo >= total ? 0 : std::min(shard, total - lo);
-    }
+    static size_t span(int j, size_t shard, size_t total) { return plan::span(j, shard, total); }
     // A second communicator over the same ranks (collective), so two exchanges can be in flight at once on
     // two streams. nullptr: this transport's exchanges are host-synchronous, use it as is.
     virtual int split(std::unique_ptr<Transport>* out) {
@@ -241,112 +240,33 @@ public:
             FMI_NCCL(api_, AllToAll(send, recv, bytes, ncclUint8, comm_, s));
             return FMI_OK;
         }
-        FMI_NCCL(api_, GroupStart());
-        for (int j = 0; j < n_; ++j) {
-            FMI_NCCL(api_, Send(send + j * bytes, bytes, ncclUint8, j, comm_, s));
-            FMI_NCCL(api_, Recv(recv + j * bytes, bytes, ncclUint8, j, comm_, s));
-        }
-        FMI_NCCL(api_, GroupEnd());
-        return FMI_OK;
+        return run_plan(plan::all_to_all(n_, rank_, bytes), send, recv, s);
     }
     int all_gather(const char* send, char* recv, size_t bytes, hipStream_t s) override {
         if (tune(FMI_TUNE_COMM_GATHER) == 0) {
             FMI_NCCL(api_, AllGather(send, recv, bytes, ncclUint8, comm_, s));
             return FMI_OK;
         }
-        // this rank's shard straight to every peer, one link each (no ring); the local copy on the stream
-        FMI_NCCL(api_, GroupStart());
-        for (int j = 0; j < n_; ++j) {
-            if (j == rank_) continue;
-            FMI_NCCL(api_, Send(send, bytes, ncclUint8, j, comm_, s));
-            FMI_NCCL(api_, Recv(recv + j * bytes, bytes, ncclUint8, j, comm_, s));
-        }
-        FMI_NCCL(api_, GroupEnd());
-        if (bytes && recv + rank_ * bytes != send)
-            FMI_COMM_HIP(hipMemcpyAsync(recv + rank_ * bytes, send, bytes, hipMemcpyDeviceToDevice, s));
-        return FMI_OK;
+        return run_plan(plan::all_gather(n_, rank_, bytes), send, recv, s);  // one link per peer, no ring
     }
-    // Exact lengths through grouped send / recv: both sides of a pair compute the same length and skip an
-    // empty one alike.
     bool ragged() const override { return true; }
     int all_to_all_ragged(const char* send, char* recv, size_t shard, size_t total, hipStream_t s) override {
-        const size_t mine = span(rank_, shard, total);
-        FMI_NCCL(api_, GroupStart());
-        for (int j = 0; j < n_; ++j) {
-            const size_t out = span(j, shard, total);
-            if (out) FMI_NCCL(api_, Send(send + j * shard, out, ncclUint8, j, comm_, s));
-            if (mine) FMI_NCCL(api_, Recv(recv + j * shard, mine, ncclUint8, j, comm_, s));
-        }
-        FMI_NCCL(api_, GroupEnd());
-        return FMI_OK;
+        return run_plan(plan::all_to_all_ragged(n_, rank_, shard, total), send, recv, s);
     }
     int all_gather_ragged(const char* send, char* recv, size_t shard, size_t total, hipStream_t s) override {
-        const size_t mine = span(rank_, shard, total);
-        FMI_NCCL(api_, GroupStart());
-        for (int j = 0; j < n_; ++j) {
-            if (j == rank_) continue;
-            const size_t in = span(j, shard, total);
-            if (mine) FMI_NCCL(api_, Send(send, mine, ncclUint8, j, comm_, s));
-            if (in) FMI_NCCL(api_, Recv(recv + j * shard, in, ncclUint8, j, comm_, s));
-        }
-        FMI_NCCL(api_, GroupEnd());
-        if (mine && recv + rank_ * shard != send)
-            FMI_COMM_HIP(hipMemcpyAsync(recv + rank_ * shard, send, mine, hipMemcpyDeviceToDevice, s));
-        return FMI_OK;
+        return run_plan(plan::all_gather_ragged(n_, rank_, shard, total), send, recv, s);
     }
     int gather_ragged(const char* send, char* recv, size_t shard, size_t total, int root, hipStream_t s) override {
-        const size_t mine = span(rank_, shard, total);
-        FMI_NCCL(api_, GroupStart());
-        if (rank_ == root) {
-            for (int j = 0; j < n_; ++j) {
-                const size_t in = span(j, shard, total);
-                if (j != root && in) FMI_NCCL(api_, Recv(recv + j * shard, in, ncclUint8, j, comm_, s));
-            }
-        } else if (mine) {
-            FMI_NCCL(api_, Send(send, mine, ncclUint8, root, comm_, s));
-        }
-        FMI_NCCL(api_, GroupEnd());
-        if (rank_ == root && mine) FMI_COMM_HIP(hipMemcpyAsync(recv + root * shard, send, mine, hipMemcpyDeviceToDevice, s));
-        return FMI_OK;
+        return run_plan(plan::gather_ragged(n_, rank_, shard, total, root), send, recv, s);
     }
     int all_to_all_back_ragged(const char* send, char* recv, size_t shard, size_t total, hipStream_t s) override {
-        const size_t mine = span(rank_, shard, total);
-        FMI_NCCL(api_, GroupStart());
-        for (int j = 0; j < n_; ++j) {
-            const size_t in = span(j, shard, total);
-            if (mine) FMI_NCCL(api_, Send(send + j * shard, mine, ncclUint8, j, comm_, s));
-            if (in) FMI_NCCL(api_, Recv(recv + j * shard, in, ncclUint8, j, comm_, s));
-        }
-        FMI_NCCL(api_, GroupEnd());
-        return FMI_OK;
+        return run_plan(plan::all_to_all_back_ragged(n_, rank_, shard, total), send, recv, s);
     }
     int gather(const char* send, char* recv, size_t bytes, int root, hipStream_t s) override {
-        FMI_NCCL(api_, GroupStart());
-        if (rank_ == root) {
-            for (int j = 0; j < n_; ++j) {
-                if (j == root) continue;
-                FMI_NCCL(api_, Recv(recv + j * bytes, bytes, ncclUint8, j, comm_, s));
-            }
-        } else {
-            FMI_NCCL(api_, Send(send, bytes, ncclUint8, root, comm_, s));
-        }
-        FMI_NCCL(api_, GroupEnd());
-        if (rank_ == root && bytes) FMI_COMM_HIP(hipMemcpyAsync(recv + root * bytes, send, bytes, hipMemcpyDeviceToDevice, s));
-        return FMI_OK;
+        return run_plan(plan::gather(n_, rank_, bytes, root), send, recv, s);
     }
     int scatter(const char* send, char* recv, size_t bytes, int root, hipStream_t s) override {
-        FMI_NCCL(api_, GroupStart());
-        if (rank_ == root) {
-            for (int j = 0; j < n_; ++j) {
-                if (j == root) continue;
-                FMI_NCCL(api_, Send(send + j * bytes, bytes, ncclUint8, j, comm_, s));
-            }
-        } else {
-            FMI_NCCL(api_, Recv(recv, bytes, ncclUint8, root, comm_, s));
-        }
-        FMI_NCCL(api_, GroupEnd());
-        if (rank_ == root && bytes) FMI_COMM_HIP(hipMemcpyAsync(recv, send + root * bytes, bytes, hipMemcpyDeviceToDevice, s));
-        return FMI_OK;
+        return run_plan(plan::scatter(n_, rank_, bytes, root), send, recv, s);
     }
     int bcast(char* buf, size_t bytes, int root, hipStream_t s) override {
         FMI_NCCL(api_, Broadcast(buf, buf, bytes, ncclUint8, root, comm_, s));
@@ -442,6 +362,19 @@ public:
     }
 
 private:
+    // One group of the plan's sends and receives (RCCL pairs them per peer in posting order), then the
+    // local part on the stream.
+    int run_plan(const plan::Plan& p, const char* send, char* recv, hipStream_t s) {
+        if (!p.sends.empty() || !p.recvs.empty()) {
+            FMI_NCCL(api_, GroupStart());
+            for (const plan::Xfer& x : p.sends) FMI_NCCL(api_, Send(send + x.off, x.len, ncclUint8, x.peer, comm_, s));
+            for (const plan::Xfer& x : p.recvs) FMI_NCCL(api_, Recv(recv + x.off, x.len, ncclUint8, x.peer, comm_, s));
+            FMI_NCCL(api_, GroupEnd());
+        }
+        if (p.copy_len && recv + p.copy_dst != send + p.copy_src)
+            FMI_COMM_HIP(hipMemcpyAsync(recv + p.copy_dst, send + p.copy_src, p.copy_len, hipMemcpyDeviceToDevice, s));
+        return FMI_OK;
+    }
     const RcclApi* api_;
     ncclComm_t comm_;
     void* token_ = nullptr;
@@ -485,71 +418,33 @@ class LocalTransport final : public Transport {
 public:
     LocalTransport(std::shared_ptr<Hub> hub, int n, int rank) : Transport(n, rank), hub_(std::move(hub)) {}
 
+    // Every exchange below runs the RCCL transport's own plan (fmi_exchange_plan.h): each receive copies
+    // from the matching send of the peer's plan (same peer order, same length, or the call fails), so the
+    // LOCAL ranks of the GPU tests exercise the pairings RCCL is given between GPUs.
     int all_to_all(const char* send, char* recv, size_t bytes, hipStream_t s) override {
-        return exchange(send, s, [&](const std::vector<const char*>& all) -> int {
-            for (int j = 0; j < n_; ++j)
-                if (bytes) FMI_COMM_HIP(hipMemcpyAsync(recv + j * bytes, all[j] + rank_ * bytes, bytes, hipMemcpyDeviceToDevice, s));
-            return FMI_OK;
-        });
+        return run_plan([&](int r) { return plan::all_to_all(n_, r, bytes); }, send, recv, s);
     }
     int all_gather(const char* send, char* recv, size_t bytes, hipStream_t s) override {
-        return exchange(send, s, [&](const std::vector<const char*>& all) -> int {
-            for (int j = 0; j < n_; ++j)
-                if (bytes) FMI_COMM_HIP(hipMemcpyAsync(recv + j * bytes, all[j], bytes, hipMemcpyDeviceToDevice, s));
-            return FMI_OK;
-        });
+        return run_plan([&](int r) { return plan::all_gather(n_, r, bytes); }, send, recv, s);
     }
     bool ragged() const override { return true; }
     int all_to_all_ragged(const char* send, char* recv, size_t shard, size_t total, hipStream_t s) override {
-        const size_t mine = span(rank_, shard, total);
-        return exchange(send, s, [&](const std::vector<const char*>& all) -> int {
-            for (int j = 0; j < n_; ++j)
-                if (mine) FMI_COMM_HIP(hipMemcpyAsync(recv + j * shard, all[j] + rank_ * shard, mine, hipMemcpyDeviceToDevice, s));
-            return FMI_OK;
-        });
+        return run_plan([&](int r) { return plan::all_to_all_ragged(n_, r, shard, total); }, send, recv, s);
     }
     int all_gather_ragged(const char* send, char* recv, size_t shard, size_t total, hipStream_t s) override {
-        return exchange(send, s, [&](const std::vector<const char*>& all) -> int {
-            for (int j = 0; j < n_; ++j) {
-                const size_t in = span(j, shard, total);
-                if (in && recv + j * shard != all[j])
-                    FMI_COMM_HIP(hipMemcpyAsync(recv + j * shard, all[j], in, hipMemcpyDeviceToDevice, s));
-            }
-            return FMI_OK;
-        });
+        return run_plan([&](int r) { return plan::all_gather_ragged(n_, r, shard, total); }, send, recv, s);
     }
     int gather_ragged(const char* send, char* recv, size_t shard, size_t total, int root, hipStream_t s) override {
-        return exchange(send, s, [&](const std::vector<const char*>& all) -> int {
-            if (rank_ != root) return FMI_OK;
-            for (int j = 0; j < n_; ++j) {
-                const size_t in = span(j, shard, total);
-                if (in) FMI_COMM_HIP(hipMemcpyAsync(recv + j * shard, all[j], in, hipMemcpyDeviceToDevice, s));
-            }
-            return FMI_OK;
-        });
+        return run_plan([&](int r) { return plan::gather_ragged(n_, r, shard, total, root); }, send, recv, s);
     }
     int all_to_all_back_ragged(const char* send, char* recv, size_t shard, size_t total, hipStream_t s) override {
-        return exchange(send, s, [&](const std::vector<const char*>& all) -> int {
-            for (int j = 0; j < n_; ++j) {
-                const size_t in = span(j, shard, total);
-                if (in) FMI_COMM_HIP(hipMemcpyAsync(recv + j * shard, all[j] + rank_ * shard, in, hipMemcpyDeviceToDevice, s));
-            }
-            return FMI_OK;
-        });
+        return run_plan([&](int r) { return plan::all_to_all_back_ragged(n_, r, shard, total); }, send, recv, s);
     }
     int gather(const char* send, char* recv, size_t bytes, int root, hipStream_t s) override {
-        return exchange(send, s, [&](const std::vector<const char*>& all) -> int {
-            if (rank_ != root) return FMI_OK;
-            for (int j = 0; j < n_; ++j)
-                if (bytes) FMI_COMM_HIP(hipMemcpyAsync(recv + j * bytes, all[j], bytes, hipMemcpyDeviceToDevice, s));
-            return FMI_OK;
-        });
+        return run_plan([&](int r) { return plan::gather(n_, r, bytes, root); }, send, recv, s);
     }
     int scatter(const char* send, char* recv, size_t bytes, int root, hipStream_t s) override {
-        return exchange(send, s, [&](const std::vector<const char*>& all) -> int {
-            if (bytes) FMI_COMM_HIP(hipMemcpyAsync(recv, all[root] + rank_ * bytes, bytes, hipMemcpyDeviceToDevice, s));
-            return FMI_OK;
-        });
+        return run_plan([&](int r) { return plan::scatter(n_, r, bytes, root); }, send, recv, s);
     }
     int bcast(char* buf, size_t bytes, int root, hipStream_t s) override {
         return exchange(buf, s, [&](const std::vector<const char*>& all) -> int {
@@ -628,6 +523,37 @@ public:
     }
 
 private:
+    // Execute plan_of(rank_) against the published buffers: my k-th receive from peer j copies from the k-th
+    // send to me in plan_of(j); a receive without a send of its length fails (RCCL would hang on it).
+    template <class PlanOf>
+    int run_plan(PlanOf&& plan_of, const char* send, char* recv, hipStream_t s) {
+        const plan::Plan mine = plan_of(rank_);
+        return exchange(send, s, [&](const std::vector<const char*>& all) -> int {
+            std::vector<plan::Plan> peer(n_);
+            std::vector<char> built(n_, 0);
+            std::vector<size_t> next(n_, 0);  // per peer: where to look for its next send to me
+            for (const plan::Xfer& r : mine.recvs) {
+                const int j = r.peer;
+                if (!built[j]) {
+                    peer[j] = plan_of(j);
+                    built[j] = 1;
+                }
+                const std::vector<plan::Xfer>& sends = peer[j].sends;
+                size_t& k = next[j];
+                while (k < sends.size() && sends[k].peer != rank_) ++k;
+                if (k == sends.size() || sends[k].len != r.len)
+                    return fail(FMI_ERR_COMM, "exchange plan: rank " + std::to_string(j) + " posts no send of " +
+                                                  std::to_string(r.len) + " B to rank " + std::to_string(rank_));
+                FMI_COMM_HIP(hipMemcpyAsync(recv + r.off, all[j] + sends[k].off, r.len, hipMemcpyDeviceToDevice, s));
+                ++k;
+            }
+            if (mine.copy_len && recv + mine.copy_dst != send + mine.copy_src)
+                FMI_COMM_HIP(hipMemcpyAsync(recv + mine.copy_dst, send + mine.copy_src, mine.copy_len,
+                                            hipMemcpyDeviceToDevice, s));
+            return FMI_OK;
+        });
+    }
+
     // Publish my buffer, wait for everyone, run `work` over all ranks' buffers, wait until everyone's
     // copies have completed (so no rank reuses a published buffer while another still reads it).
     int exchange(const char* mine, hipStream_t s, const std::function<int(const std::vector<const char*>&)>& work) {
