@@ -37,11 +37,11 @@ DeviceState g_state;  // one process drives one device (one process per GPU, as 
 
 // Defaults from tools/tune_pair.py on MI355X (C2, 256 MiB f32): nontemporal one-shot tiles, 4 × 16 B per
 // operand per thread, 256-thread workgroups — 125 µs = 6.4 TB/s vs 142 µs for plain loads/stores.
-std::atomic<long long> g_tune[11] = {2 /*variant: nontemporal tiles*/, 4 /*unroll*/, 256 /*block*/,
+std::atomic<long long> g_tune[12] = {2 /*variant: nontemporal tiles*/, 4 /*unroll*/, 256 /*block*/,
                                      8 /*grid per CU*/, 64ll << 20 /*host chunk*/, 1 /*host zero-copy*/,
                                      64 /*fused in-flight KiB per CU (tools/ab_fused_cap.py)*/,
                                      1 /*one-pass blocked scan*/, 0 /*ncclAllToAll*/, 0 /*ncclAllGather*/,
-                                     0 /*no allreduce pipelining*/};
+                                     0 /*no allreduce pipelining*/, 1 /*fused kernels: buffer ops where measured faster*/};
 
 int hip_fail(const char* what, hipError_t e) {
     return fail(FMI_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
@@ -557,6 +557,15 @@ int fail(int code, const std::string& msg) {
 
 hipStream_t library_stream() { return g_state.stream; }
 
+// The fused kernels' `pol` argument. Auto (1): buffer accesses where tools/ab_fused_policy.py measured them
+// ahead with >= 1.5 GiB of rotating buckets (tree P >= 4: +1.6..3.2 %; scan P >= 8: +0.8..0.9 %), global
+// accesses where they were not (tree P = 2: -0.7 %, scan P = 2 / 4: +0.3 / -2.4 %).
+int fused_policy(bool scan, int P) {
+    const long long v = g_tune[FMI_TUNE_FUSED_POLICY].load();
+    if (v == 1) return (scan ? P >= 8 : P >= 4) ? 1 : 0;
+    return v == 2 ? 1 : 0;
+}
+
 size_t fused_lds_bytes(int P, size_t wg_load_bytes_per_peer) {
     const long long budget = g_tune[FMI_TUNE_FUSED_INFLIGHT_KIB].load() << 10;
     if (budget <= 0 || P <= 0) return 0;
@@ -998,6 +1007,9 @@ int fmi_tune_set(int key, long long value) {
         case FMI_TUNE_COMM_PIPELINE:
             if (value < 0 || value > 64) return fail(FMI_ERR_INVALID, "pipeline chunks must be in [0, 64]");
             break;
+        case FMI_TUNE_FUSED_POLICY:
+            if (value < 0 || value > 2) return fail(FMI_ERR_INVALID, "fused access policy must be 0, 1 or 2");
+            break;
         default: return fail(FMI_ERR_INVALID, "unknown tuning key");
     }
     g_tune[key].store(value);
@@ -1005,7 +1017,7 @@ int fmi_tune_set(int key, long long value) {
 }
 
 int fmi_tune_get(int key, long long* value) {
-    if (!value || key < 0 || key > FMI_TUNE_COMM_PIPELINE) return fail(FMI_ERR_INVALID, "bad tuning query");
+    if (!value || key < 0 || key > FMI_TUNE_FUSED_POLICY) return fail(FMI_ERR_INVALID, "bad tuning query");
     *value = g_tune[key].load();
     return FMI_OK;
 }

@@ -24,7 +24,7 @@ template <class Op, class T, int P>
 void all_ranks_one(const PeerPtrs& ptrs, size_t n, int, hipStream_t s) {
     const size_t nvec = n / kVecLanes<T>;
     const unsigned grid = static_cast<unsigned>(std::min<size_t>(grid_for(nvec, kFusedBlock), kFusedGridCap));
-    scan_kernel<Op, T, sched::kAllreduce, P><<<grid, kFusedBlock, fused_lds_bytes(P, kFusedBlock * 16), s>>>(ptrs, n);
+    scan_kernel<Op, T, sched::kAllreduce, P><<<grid, kFusedBlock, fused_lds_bytes(P, kFusedBlock * 16), s>>>(ptrs, n, fused_policy(true, P));
 }
 
 template <class Op, class T, int... I>

@@ -25,9 +25,9 @@ void fused_one(const PeerPtrs& ptrs, size_t n, int rank, hipStream_t s) {
     const unsigned grid = static_cast<unsigned>(std::min<size_t>(grid_for(nvec, kFusedBlock), kFusedGridCap));
     const size_t lds = fused_lds_bytes(P, kFusedBlock * 16);
     if constexpr (sched::stores_all_outputs(ALG))
-        scan_kernel<Op, T, ALG, P><<<grid, kFusedBlock, lds, s>>>(ptrs, n);
+        scan_kernel<Op, T, ALG, P><<<grid, kFusedBlock, lds, s>>>(ptrs, n, fused_policy(true, P));
     else
-        tree_kernel<Op, T, ALG, P, ALL_RANKS><<<grid, kFusedBlock, lds, s>>>(ptrs, n, rank);
+        tree_kernel<Op, T, ALG, P, ALL_RANKS><<<grid, kFusedBlock, lds, s>>>(ptrs, n, rank, fused_policy(false, P));
 }
 
 template <class Op, class T, int ALG, bool ALL_RANKS, int LO, int... I>

@@ -22,6 +22,7 @@ hipStream_t library_stream();
 // workgroups keep in flight per CU stay within FMI_TUNE_FUSED_INFLIGHT_KIB: fewer concurrent HBM streams
 // at large P, better DRAM row locality. `wg_load_bytes_per_peer` = bytes one workgroup loads per peer.
 size_t fused_lds_bytes(int P, size_t wg_load_bytes_per_peer);
+int fused_policy(bool scan, int P);  // FMI_TUNE_FUSED_POLICY: the fused kernels' `pol` argument
 
 // The dtypes every kernel is instantiated for (the fused P-way kernels included).
 inline bool is_core_dtype(int dtype) { return dtype >= FMI_F32 && dtype <= FMI_I64; }

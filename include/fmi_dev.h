@@ -300,10 +300,14 @@ typedef enum {
     FMI_TUNE_COMM_GATHER = 9,     /* RCCL transport all-gather: 0 = ncclAllGather (default), 1 = grouped
                                     ncclSend / ncclRecv of this rank's shard to every peer (each peer link
                                     carries one shard, no ring). Same bytes either way */
-    FMI_TUNE_COMM_PIPELINE = 10   /* path TREE allreduce in K chunks (0 or 1 = off, default; 2..64): chunk k's
+    FMI_TUNE_COMM_PIPELINE = 10,  /* path TREE allreduce in K chunks (0 or 1 = off, default; 2..64): chunk k's
                                     all-gather runs on a second stream and communicator (ncclCommSplit)
                                     while chunk k + 1's all-to-all and kernel run; chunks of >= 1 MiB per
                                     rank only. Same bits (element-wise); every rank must set the same K */
+    FMI_TUNE_FUSED_POLICY = 11    /* fused P-way kernels (tree, scan; <= 16 peers), 16-B accesses: 2 = buffer
+                                    loads nt with sc1 (tree) / nt sc1 (scan) stores; 0 = global_load /
+                                    global_store nt; 1 = auto (default): 2 for trees of >= 4 and scans of
+                                    >= 8 peers, 0 otherwise (tools/ab_fused_policy.py). Same bits always */
 } fmi_tune_key_t;
 int fmi_tune_set(int key, long long value);
 int fmi_tune_get(int key, long long* value);

@@ -139,6 +139,12 @@ def test_tuning_knobs_validate():
     fmi_amd.tune_set(fmi_amd.Tune.BLOCKS_ONE_PASS, 1)
     with pytest.raises(fmi_amd.FmiError):
         fmi_amd.tune_set(fmi_amd.Tune.BLOCKS_ONE_PASS, 2)
+    assert fmi_amd.tune_get(fmi_amd.Tune.FUSED_POLICY) == 1  # default: per kernel (tools/ab_fused_policy.py)
+    for v in (0, 2, 1):
+        fmi_amd.tune_set(fmi_amd.Tune.FUSED_POLICY, v)
+        assert fmi_amd.tune_get(fmi_amd.Tune.FUSED_POLICY) == v
+    with pytest.raises(fmi_amd.FmiError):
+        fmi_amd.tune_set(fmi_amd.Tune.FUSED_POLICY, 3)
     for key in (fmi_amd.Tune.COMM_A2A, fmi_amd.Tune.COMM_GATHER):  # RCCL exchange realisations
         assert fmi_amd.tune_get(key) == 0
         fmi_amd.tune_set(key, 1)

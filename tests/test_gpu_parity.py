@@ -350,6 +350,37 @@ def test_fused_occupancy_cap_keeps_bits(device, cap):
         fmi_amd.tune_set(Tune.FUSED_INFLIGHT_KIB, old)
 
 
+@pytest.mark.parametrize("pol", [0, 2], ids=["global_nt", "buffer_sc1"])
+def test_fused_access_policy_keeps_bits(device, pol):
+    """FMI_TUNE_FUSED_POLICY forced to each access form for every peer count (the default picks per kernel):
+    the fused tree and scan kernels, every algorithm, four dtypes and all four ops, ragged n (tail lanes) and
+    a grid-stride size, against the oracle."""
+    old = fmi_amd.tune_get(Tune.FUSED_POLICY)
+    try:
+        fmi_amd.tune_set(Tune.FUSED_POLICY, pol)
+        for dtype, n in ((np.float32, 4099 * 4 + 3), (np.int64, 65536 * 3 + 1), (np.uint8, 1 << 16), (np.float64, 1027)):
+            for P in (2, 3, 4, 8, 16):
+                xs = _peer_inputs(dtype, n, P)
+                ins = [dev(x) for x in xs]
+                for op in OPS:
+                    f = orc.OPS[OPNAME[op]]
+                    with np.errstate(all="ignore"):
+                        want_ar, _ = orc.allreduce(xs, f)
+                        want_rd, _ = orc.reduce(xs, f, root=0)
+                        want_sc, _ = orc.scan(xs, f)
+                    out = Bucket(n, dtype)
+                    fmi_amd.reduce_tree(op, Alg.ALLREDUCE, out, ins, rank=P - 1)
+                    assert_bit_equal(out.numpy(), want_ar[P - 1], f"pol {pol} allreduce {op.name} P={P}")
+                    fmi_amd.reduce_tree(op, Alg.REDUCE, out, ins)
+                    assert_bit_equal(out.numpy(), want_rd, f"pol {pol} reduce {op.name} P={P}")
+                    outs = [Bucket(n, dtype) for _ in range(P)]
+                    fmi_amd.scan_peers(op, Alg.SCAN, outs, ins)
+                    for k in range(P):
+                        assert_bit_equal(outs[k].numpy(), want_sc[k], f"pol {pol} scan {op.name} P={P} peer {k}")
+    finally:
+        fmi_amd.tune_set(Tune.FUSED_POLICY, old)
+
+
 @pytest.mark.parametrize("dtype", EXTRA_DTYPES, ids=lambda d: np.dtype(d).name)
 def test_extra_dtypes_p_way_programs(device, dtype):
     """The other integer widths through every P-way entry point (pairwise passes in the reference's order),

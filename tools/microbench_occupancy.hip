@@ -142,18 +142,18 @@ int main() {
                        pair_tile<OpMax, int64_t, 4, 3><<<grid64, 256, lds>>>(qa[k % 8], qa[k % 8], qb[k % 8], n64);
                    }, 15));
             report("tree8 allreduce B256 nt", cap, tree_bytes, median_us([&](int k) {
-                       tree_kernel<OpSum, float, A, P, false><<<grid3, 256, lds>>>(ptrs[k % 2], n3, 0);
+                       tree_kernel<OpSum, float, A, P, false><<<grid3, 256, lds>>>(ptrs[k % 2], n3, 0, 0);
                    }, 15));
             report("scan8 B256 nt", cap, scan_bytes, median_us([&](int k) {
-                       scan_kernel<OpSum, float, S, P><<<grid3, 256, lds>>>(ptrs[k % 2], n3);
+                       scan_kernel<OpSum, float, S, P><<<grid3, 256, lds>>>(ptrs[k % 2], n3, 0);
                    }, 15));
             // persistent grid-stride form: cap workgroups per CU × 256 CUs, each thread walks the bucket
             if (cap) {
                 report("scan8 B256 nt grid-stride", cap, scan_bytes, median_us([&](int k) {
-                           scan_kernel<OpSum, float, S, P><<<256 * cap, 256, lds>>>(ptrs[k % 2], n3);
+                           scan_kernel<OpSum, float, S, P><<<256 * cap, 256, lds>>>(ptrs[k % 2], n3, 0);
                        }, 15));
                 report("tree8 B256 nt grid-stride", cap, tree_bytes, median_us([&](int k) {
-                           tree_kernel<OpSum, float, A, P, false><<<256 * cap, 256, lds>>>(ptrs[k % 2], n3, 0);
+                           tree_kernel<OpSum, float, A, P, false><<<256 * cap, 256, lds>>>(ptrs[k % 2], n3, 0, 0);
                        }, 15));
             }
         }

@@ -113,7 +113,7 @@ int main(int argc, char** argv) {
     // bit-exactness of the split form against scan_kernel on one draw (inputs: small integers in f32 would
     // hide bracketing; use a counter-based fill instead)
     for (int j = 0; j < 8; ++j)
-        synth_kernel<float><<<4096, 256>>>(static_cast<float*>(buf[j]), n, 42, static_cast<uint32_t>(j));
+        synth_kernel<float><<<4096, 256>>>(static_cast<float*>(buf[j]), n, 42, static_cast<uint32_t>(j), 0);
     PeerPtrs ref{}, spl{};
     for (int j = 0; j < P; ++j) {
         ref.in[j] = spl.in[j] = buf[j];
@@ -121,7 +121,7 @@ int main(int argc, char** argv) {
         spl.out[j] = buf[16 + j];
     }
     const unsigned grid = static_cast<unsigned>(nvec / 256);
-    scan_kernel<OpSum, float, fmi::sched::kScan, P><<<grid, 256>>>(ref, n);
+    scan_kernel<OpSum, float, fmi::sched::kScan, P><<<grid, 256>>>(ref, n, 0);
     split1<<<grid, 256>>>(spl, nvec);
     split2<<<grid, 256>>>(spl, nvec);
     CHECK(hipDeviceSynchronize());
@@ -149,12 +149,12 @@ int main(int argc, char** argv) {
             p.in[j] = buf[pick[j]];
             p.out[j] = buf[pick[8 + j]];
         }
-        const double us_scan = median_us([&] { scan_kernel<OpSum, float, fmi::sched::kScan, P><<<grid, 256>>>(p, n); }, 9);
+        const double us_scan = median_us([&] { scan_kernel<OpSum, float, fmi::sched::kScan, P><<<grid, 256>>>(p, n, 0); }, 9);
         const double us_split = median_us([&] {
             split1<<<grid, 256>>>(p, nvec);
             split2<<<grid, 256>>>(p, nvec);
         }, 9);
-        const double us_tree = median_us([&] { tree_kernel<OpSum, float, fmi::sched::kAllreduce, P, false><<<grid, 256>>>(p, n, 0); }, 9);
+        const double us_tree = median_us([&] { tree_kernel<OpSum, float, fmi::sched::kAllreduce, P, false><<<grid, 256>>>(p, n, 0, 0); }, 9);
         std::printf("{\"trial\": %d, \"scan8_us\": %.2f, \"scan8_frac\": %.4f, \"split_us\": %.2f, \"split_frac_of_16_units\": %.4f, "
                     "\"tree8_us\": %.2f, \"tree8_frac\": %.4f}\n",
                     t, us_scan, scan_bytes / (us_scan * 1e-6) / 8e12, us_split, scan_bytes / (us_split * 1e-6) / 8e12,

@@ -107,9 +107,9 @@ int main() {
                 p.in[j] = arena + s.off[j];
                 p.out[j] = arena + s.off[8 + j];
             }
-            const double us_scan = median_us([&] { scan_kernel<OpSum, float, fmi::sched::kScan, P><<<grid, 256>>>(p, n); }, 9);
+            const double us_scan = median_us([&] { scan_kernel<OpSum, float, fmi::sched::kScan, P><<<grid, 256>>>(p, n, 0); }, 9);
             const double us_tree =
-                median_us([&] { tree_kernel<OpSum, float, fmi::sched::kAllreduce, P, false><<<grid, 256>>>(p, n, 0); }, 9);
+                median_us([&] { tree_kernel<OpSum, float, fmi::sched::kAllreduce, P, false><<<grid, 256>>>(p, n, 0, 0); }, 9);
             std::printf("{\"round\": %d, \"scheme\": \"%s\", \"scan8_us\": %.2f, \"scan8_frac\": %.4f, \"tree8_us\": %.2f, "
                         "\"tree8_frac\": %.4f}\n",
                         round, s.name.c_str(), us_scan, scan_bytes / (us_scan * 1e-6) / 8e12, us_tree,
