@@ -13,7 +13,7 @@
 // interleaved over R rounds; median over rounds.
 //
 // Build: hipcc -std=c++20 -O3 --offload-arch=gfx950 -ffp-contract=off tools/microbench_cachepol.hip -o build/mbc
-// Run:   build/mbc [rounds, default 5]
+// Run:   build/mbc [rounds, default 5] [name filter]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -115,6 +115,77 @@ __global__ void __launch_bounds__(B) pair_saddr(T* out, const T* a, const T* b, 
             if (tile0 + u * B + t < nvec) store_lanes<true, T, W>(to + (u * B + t) * W, combine<Op, T, W>(va[u], vb[u]));
     }
     pair_tail<Op, T>(out, a, b, n);
+}
+
+// saddr form done right: uniform tile base pointers, each access a 32-bit unsigned byte offset from them
+// (global_load v, v_off, s[base] — no per-lane 64-bit address arithmetic); same full / ragged split and tail.
+template <class Op, class T, int U, unsigned B>
+__global__ void __launch_bounds__(B) pair_saddr2(T* out, const T* a, const T* b, size_t n) {
+    constexpr int W = kVecLanes<T>;
+    using L = Lanes<T, W>;
+    const size_t nvec = n / W;
+    const size_t tile0 = static_cast<size_t>(blockIdx.x) * U * B;  // first lane group of the tile
+    const char* ta = reinterpret_cast<const char*>(a + tile0 * W);
+    const char* tb = reinterpret_cast<const char*>(b + tile0 * W);
+    char* to = reinterpret_cast<char*>(out + tile0 * W);
+    const unsigned lane = threadIdx.x * 16u;
+    L va[U], vb[U];
+    if (tile0 + U * B <= nvec) {
+        // each group's 32-bit offset as an opaque register, so every access is (tile base SGPRs) + offset
+        unsigned off[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            off[u] = lane + u * B * 16u;
+            asm("" : "+v"(off[u]));
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            va[u] = load_lanes<true, T, W>(reinterpret_cast<const T*>(ta + off[u]));
+            vb[u] = load_lanes<true, T, W>(reinterpret_cast<const T*>(tb + off[u]));
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            store_lanes<true, T, W>(reinterpret_cast<T*>(to + off[u]), combine<Op, T, W>(va[u], vb[u]));
+    } else {
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (tile0 + u * B + threadIdx.x < nvec) {
+                const unsigned off = lane + u * B * 16u;
+                va[u] = load_lanes<true, T, W>(reinterpret_cast<const T*>(ta + off));
+                vb[u] = load_lanes<true, T, W>(reinterpret_cast<const T*>(tb + off));
+            }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (tile0 + u * B + threadIdx.x < nvec)
+                store_lanes<true, T, W>(reinterpret_cast<T*>(to + lane + u * B * 16u), combine<Op, T, W>(va[u], vb[u]));
+    }
+    pair_tail<Op, T>(out, a, b, n);
+}
+
+// the production pair_tile with __launch_bounds__(256) instead of 1024 (same body and tail)
+template <class Op, class T, int U, int NT>
+__global__ void __launch_bounds__(256) pair_tile_lb256(T* out, const T* a, const T* b, size_t n) {
+    const size_t nvec = n / kVecLanes<T>;
+    pair_tile_body<Op, T, U, NT>(out, a, b, nvec, blockIdx.x);
+    pair_tail<Op, T>(out, a, b, n);
+}
+
+// global nt loads, buffer store with policy SA through a per-tile descriptor
+template <int SA>
+__global__ void __launch_bounds__(256) pair_mix_k(float* out, const float* a, const float* b) {
+    const size_t tile = static_cast<size_t>(blockIdx.x) * 4 * 256 * 16;  // bytes
+    const unsigned lane = threadIdx.x * 16u;
+    const char* ta = reinterpret_cast<const char*>(a) + tile;
+    const char* tb = reinterpret_cast<const char*>(b) + tile;
+    u32x4v x[4], y[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        x[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4v*>(ta + lane + u * 4096u));
+        y[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4v*>(tb + lane + u * 4096u));
+    }
+    const auto ro = rsrc(reinterpret_cast<char*>(out) + tile, 1 << 30);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) __builtin_amdgcn_raw_buffer_store_b128(addf(x[u], y[u]), ro, lane + u * 4096u, 0, SA);
 }
 
 struct P8 {
@@ -301,6 +372,17 @@ int main(int argc, char** argv) {
     PVAR("t4", AR, 4, false, 2, 5.0 * p8_bytes) PVAR("t4", AR, 4, false, 18, 5.0 * p8_bytes)
     PPROD("t8", AR, 8, false, 0, 9.0 * p8_bytes) PPROD("t8", AR, 8, false, 1, 9.0 * p8_bytes)
     PVAR("t8", AR, 8, false, 2, 9.0 * p8_bytes) PVAR("t8", AR, 8, false, 18, 9.0 * p8_bytes)
+    vs.push_back({"pair saddr2 candidate U4 B256", [&](int k) {
+                      pair_saddr2<OpSum, float, 4, 256><<<pgrid, 256>>>(po[k % PSETS], pa[k % PSETS], pb[k % PSETS], pn);
+                  }, 3.0 * pair_bytes, {}});
+    vs.push_back({"pair production body, launch_bounds 256", [&](int k) {
+                      pair_tile_lb256<OpSum, float, 4, 3><<<pgrid, 256>>>(po[k % PSETS], pa[k % PSETS], pb[k % PSETS], pn);
+                  }, 3.0 * pair_bytes, {}});
+#define PMIX(SA)                                                                                              \
+    vs.push_back({"pair mix global-nt loads, buffer st" #SA, [&](int k) {                                    \
+                      pair_mix_k<SA><<<pgrid, 256>>>(po[k % PSETS], pa[k % PSETS], pb[k % PSETS]);           \
+                  }, 3.0 * pair_bytes, {}});
+    PMIX(2) PMIX(16) PMIX(18) PMIX(0)
     // aux bits: 1 sc0, 2 nt, 16 sc1
     PAIR(PROD, PROD) PAIR(2, 2) PAIR(2, 16) PAIR(2, 17) PAIR(2, 18) PAIR(2, 0) PAIR(16, 2) PAIR(18, 18) PAIR(0, 2)
     P8V(PROD, PROD, true, "scan8", 16.0 * p8_bytes) P8V(2, 2, true, "scan8", 16.0 * p8_bytes)
@@ -332,6 +414,23 @@ int main(int argc, char** argv) {
                 first = false;
             }
         }
+    }
+    if (argc > 2) {  // keep only the variants whose name contains one of argv[2]'s '|'-separated parts
+        std::vector<std::string> parts;
+        for (std::string f = argv[2];;) {
+            const size_t bar = f.find('|');
+            parts.push_back(f.substr(0, bar));
+            if (bar == std::string::npos) break;
+            f = f.substr(bar + 1);
+        }
+        std::vector<Variant> keep;
+        for (auto& v : vs)
+            for (const auto& part : parts)
+                if (v.name.find(part) != std::string::npos) {
+                    keep.push_back(v);
+                    break;
+                }
+        vs.swap(keep);
     }
     hipEvent_t e0, e1;
     CHECK(hipEventCreate(&e0));
