@@ -89,12 +89,12 @@ def pmc_traffic(kernel_substr: str):
         return None, None
     try:
         data = json.load(open(path))
-        for k in data.get("kernels", []):
-            if kernel_substr in k.get("kernel", ""):
-                return k.get("hbm_bytes_per_launch"), k.get("source", data.get("source"))
+        hits = [k for k in data.get("kernels", []) if kernel_substr in k.get("kernel", "")]
     except Exception:
         return None, None
-    return None, None
+    if len(hits) != 1:  # absent, or ambiguous (several instantiations match): report nothing rather than a wrong kernel's bytes
+        return None, None
+    return hits[0].get("hbm_bytes_per_launch"), hits[0].get("source", data.get("source"))
 
 
 def cpu_baseline(args):
@@ -211,6 +211,18 @@ def _headline(args, value, step_ms, workload, parallelism, n, roofline):
     }
 
 
+def c2_kernel_signature():
+    """The pair_tile instantiation C2 launches under the current tuning (fmi_dev.hip: launch_combine →
+    launch_pair_vec): the PMC summary is looked up by exactly this, never by a bare kernel name that other
+    instantiations (C3's i64 max) share."""
+    import fmi_amd
+    from fmi_amd import Tune
+
+    nt = {0: 0, 1: 0, 2: 3, 3: 1, 4: 2}[fmi_amd.tune_get(Tune.PAIR_VARIANT)]
+    form = "pair_stride" if fmi_amd.tune_get(Tune.PAIR_VARIANT) == 1 else "pair_tile"
+    return f"{form}<fmi::dev::OpSum, float, {fmi_amd.tune_get(Tune.PAIR_UNROLL)}, {nt}>"
+
+
 def _roofline(kernel, algo_bytes, kernel_avg_ms, source, extra=None, pmc_key=None):
     achieved = algo_bytes / (kernel_avg_ms * 1e-3) / 1e9
     traffic, traffic_src = pmc_traffic(pmc_key or kernel)
@@ -270,7 +282,7 @@ def run_single(args):
         b.free()
     roof = _roofline("pair_tile", 3 * nbytes, kernel_avg_ms,
                      "HIP events bracketing the K timed launches on the library stream",
-                     {"kernel_avg_us_isolated": round(isolated_us, 2)})
+                     {"kernel_avg_us_isolated": round(isolated_us, 2)}, pmc_key=c2_kernel_signature())
     line = _headline(args, (nbytes / GIB) / (step_ms * 1e-3), step_ms,
                      "C2: 1-GPU pairwise float32 sum-reduce of two 256 MiB device-resident peer buckets",
                      "single GPU (2 peers resident)", n, roof)

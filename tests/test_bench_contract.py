@@ -53,3 +53,22 @@ def test_defaults_are_the_contract(monkeypatch):
     a = bench.parse()
     assert a.gpus == 1 and a.bucket_mib == 256 and a.steps > 0 and a.warmup > 0 and a.path == "tree"
     assert a.c4_mib == 1024 and a.transport == "rccl"  # C4: 1 GiB per peer, one process per GPU over RCCL
+
+
+def test_roofline_traffic_is_the_launched_kernels():
+    """roofline.traffic comes from the committed PMC summary of exactly the kernel the line measures: C2's
+    default pair_tile<OpSum, float, 4, 3> (not another pair_tile instantiation, e.g. C3's i64 max), and the
+    N>1 shard kernel per world size; PMC bytes within 1 % of the algorithmic bytes. A key matching several
+    instantiations reports nothing rather than a wrong kernel's bytes."""
+    import fmi_amd
+
+    fmi_amd.load()
+    key = bench.c2_kernel_signature()
+    assert key == "pair_tile<fmi::dev::OpSum, float, 4, 3>"
+    traffic, src = bench.pmc_traffic(key)
+    algo = 3 * 256 * (1 << 20)
+    assert traffic is not None and abs(traffic / algo - 1) < 0.01, (traffic, src)
+    assert bench.pmc_traffic("pair_tile") == (None, None)  # ambiguous
+    for world, shard_mib in ((2, 128), (4, 64), (8, 32)):
+        t, _ = bench.pmc_traffic(f"tree_kernel<fmi::dev::OpSum, float, 0, {world}, false>")
+        assert t is not None and abs(t / ((world + 1) * shard_mib * (1 << 20)) - 1) < 0.01, (world, t)

@@ -83,8 +83,10 @@ def main():
     default = os.path.join(args.out, "pmc_summary.json")
     if args.merge and os.path.exists(default):
         merged = json.load(open(default))
-        names = {k["kernel"] for k in kernels}
-        merged["kernels"] = [k for k in merged["kernels"] if k["kernel"] not in names] + kernels
+        # same instantiation = same name up to the parameter list (a kernel whose arguments changed replaces
+        # its old entry instead of standing beside it)
+        names = {k["kernel"].split("(")[0] for k in kernels}
+        merged["kernels"] = [k for k in merged["kernels"] if k["kernel"].split("(")[0] not in names] + kernels
         merged.setdefault("merged", []).append({"source": summary["source"], "command": args.command})
         with open(default, "w") as f:
             json.dump(merged, f, indent=1)
