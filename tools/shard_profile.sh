@@ -9,5 +9,5 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpu
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $R/gpurun_out/shf -o run -- python3 $R/tools/shard_kernels.py > $R/gpurun_out/shf.log 2>&1
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $R/gpurun_out/shw -o run -- python3 $R/tools/shard_kernels.py > $R/gpurun_out/shw.log 2>&1
 cd $R
-python3 tools/pmc_summarize.py --trace gpurun_out/sht --fetch gpurun_out/shf --write gpurun_out/shw --tag r02_shard \
+python3 tools/pmc_summarize.py --trace gpurun_out/sht --fetch gpurun_out/shf --write gpurun_out/shw --tag ${TAG:-r02_shard} \
   --command "rocprofv3 -- python3 tools/shard_kernels.py (tools/shard_profile.sh)" --merge > gpurun_out/r02_shard_pmc.json
