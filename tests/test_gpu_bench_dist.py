@@ -7,7 +7,7 @@ ranks on one GPU).
   shard kernel) in 2 processes; the allreduce result is compared bit for bit with the oracle's simulation of
   the reference's 2-peer allreduce (src/comm/PeerToPeer.cpp:96-130), and the self-check must reject a result
   checked against the wrong buckets.
-- test_bench_py_proc_transport[world 2, 3, 4]: bench.py itself under torch.distributed.run; its JSON line must
+- test_bench_py_proc_transport[world 2, 3, 4, 8]: bench.py itself under torch.distributed.run; its JSON line must
   carry a passing self_check (headline and C4 TREE) and a correct C5 result.
 """
 import json
@@ -54,7 +54,7 @@ def test_comm_allreduce_gloo_world2():
     assert res[0]["step_ms"][0] == res[1]["step_ms"][0] > 0  # max over ranks
 
 
-@pytest.mark.parametrize("world", [2, 3, 4])
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
 def test_bench_py_proc_transport(world):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", str(world),
