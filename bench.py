@@ -72,6 +72,8 @@ def parse():
     ap.add_argument("--no-c3", action="store_true", help="N=1: skip the config C3 kernels (i64 max, peer scan)")
     ap.add_argument("--c5-mib", type=int, default=1024, help="host bucket per rank of the c5 block (config C5)")
     ap.add_argument("--no-diagnostics", action="store_true", help="N>1: skip the untimed diagnostics")
+    ap.add_argument("--no-numa-bind", action="store_true",
+                    help="N>1: do not pin each rank to its GPU's NUMA node (default: pinned when the host has several)")
     ap.add_argument("--diag-deadline", type=float, default=240.0,
                     help="seconds everything after `value` (c4, c5, diagnostics) may take before the line is "
                          "printed without the rest of it")
@@ -388,6 +390,34 @@ def c5_single(mib: int, iters: int = 3) -> dict:
 # ------------------------------------------------------------------------------------------------------
 # N > 1: the sharded allreduce, one peer per GPU
 # ------------------------------------------------------------------------------------------------------
+def bind_near_gpu(dev: int) -> dict:
+    """Pin this rank to the CPUs of its GPU's NUMA node (from the PCI address torch reports) before any
+    host buffer is allocated: page-locked C5 buckets then sit on the GPU's socket, and RCCL's proxy threads
+    run there. A no-op on one-node hosts or when the node is unknown."""
+    import glob
+
+    import torch
+
+    try:
+        pr = torch.cuda.get_device_properties(dev)
+        bdf = "%04x:%02x:%02x.0" % (pr.pci_domain_id, pr.pci_bus_id, pr.pci_device_id)
+        node = int(open(f"/sys/bus/pci/devices/{bdf}/numa_node").read())
+        nodes = glob.glob("/sys/devices/system/node/node[0-9]*")
+        if node < 0 or len(nodes) < 2:
+            return {"numa_node": node, "bound": False}
+        cpus = set()
+        for part in open(f"/sys/devices/system/node/node{node}/cpulist").read().strip().split(","):
+            lo, _, hi = part.partition("-")
+            cpus.update(range(int(lo), int(hi or lo) + 1))
+        allowed = cpus & os.sched_getaffinity(0)
+        if len(allowed) < 2:
+            return {"numa_node": node, "bound": False}
+        os.sched_setaffinity(0, allowed)
+        return {"numa_node": node, "bound": True, "cpus": len(allowed)}
+    except (OSError, ValueError, AttributeError, RuntimeError) as e:
+        return {"bound": False, "error": f"{type(e).__name__}: {e}"}
+
+
 def run_dist(args, world, rank, local_rank):
     # torch first: libfmi_dev.so then binds to the HIP runtime torch already loaded (one runtime per process,
     # shared streams/pointers with RCCL) — see DESIGN.md §Runtime.
@@ -396,6 +426,7 @@ def run_dist(args, world, rank, local_rank):
 
     proc = args.transport == "proc"
     dev = local_rank % max(1, torch.cuda.device_count()) if proc else local_rank
+    numa = bind_near_gpu(dev) if not args.no_numa_bind else {"bound": False, "disabled": True}
     torch.cuda.set_device(dev)
     if proc:
         dist.init_process_group("gloo")
@@ -433,7 +464,7 @@ def run_dist(args, world, rank, local_rank):
                      f"(a {args.bucket_mib} MiB device-resident bucket) per GPU, through fmi_comm_allreduce",
                      f"{world} GPUs, one peer per GPU, buckets sharded {world} ways; path {args.path}: "
                      f"{path_desc[args.path]}; transport {args.transport}", n, roof)
-    line["config"].update({"peers": world, "path": args.path, "transport": args.transport,
+    line["config"].update({"numa_binding_rank0": numa, "peers": world, "path": args.path, "transport": args.transport,
                            "algbw_GiB_s": extra["algbw_GiB_s"], "busbw_GiB_s": extra["busbw_GiB_s"],
                            "shard_elems": extra["shard_elems"]})
     line["self_check"] = check
