@@ -272,3 +272,24 @@ def test_programs_combine_every_input_exactly_once(seed):
         for alg in (Alg.SCAN, Alg.SCAN_LTR):
             leaves = collections.Counter(int(x) for x in re.findall(r"x(\d+)", fmi_amd.schedule_expr(alg, P, r)))
             assert leaves == collections.Counter(range(r + 1)), (alg, P, r)
+
+
+def test_python_enums_match_the_header():
+    """Every enumerator the C-ABI header defines has the same value in the Python binding (a binding that
+    drifts from include/fmi_dev.h would pass wrong ops, dtypes or tuning keys through ctypes silently)."""
+    import re
+
+    from fmi_amd.comm import Path, Transport
+
+    text = open(os.path.join(ROOT, "include", "fmi_dev.h")).read()
+    consts = {m.group(1): int(m.group(2)) for m in re.finditer(r"\b(FMI_[A-Z0-9_]+)\s*=\s*(\d+)", text)}
+    groups = [(fmi_amd.Op, "FMI_OP_"), (fmi_amd.DType, "FMI_"), (fmi_amd.Alg, "FMI_ALG_"), (Transport, "FMI_TRANSPORT_"),
+              (Path, "FMI_PATH_"), (fmi_amd.Tune, "FMI_TUNE_")]
+    for enum_cls, prefix in groups:
+        for member in enum_cls:
+            name = prefix + member.name
+            assert name in consts, f"{name} missing from include/fmi_dev.h"
+            assert consts[name] == int(member), f"{name}: header {consts[name]}, Python {int(member)}"
+        declared = {k for k in consts if k.startswith(prefix)}
+        if prefix not in ("FMI_",):  # every header enumerator of the group is bound in Python
+            assert declared == {prefix + m.name for m in enum_cls}, (prefix, declared ^ {prefix + m.name for m in enum_cls})
