@@ -298,7 +298,9 @@ def run_single(args):
             line["c3"] = f"failed: {type(e).__name__}: {e}"
     if not args.no_c5:
         try:
+            quiet_device()
             line["c5"] = c5_single(args.c5_mib)
+            line["c5"]["after_pause_s"] = QUIET_S
         except Exception as e:  # reported, never fails the measured line
             line["c5"] = f"failed: {type(e).__name__}: {e}"
     print(json.dumps(line), flush=True)
@@ -349,6 +351,21 @@ def c3_single(reps: int = 60) -> dict:
     return {"i64_max_pair_64MiB": dict(row(ms_max, 3 * 64 * MIB), rotating_sets=8),
             "f32_scan_P8_64MiB": dict(row(ms_scan, 2 * P * 64 * MIB), rotating_sets=2),
             "timing": "two HIP events around back-to-back launches on the library stream (gaps included)"}
+
+
+QUIET_S = 1.0
+
+
+def quiet_device():
+    """Let the device go idle before a host-ingress measurement. The driver clears freed VRAM
+    asynchronously on the copy engines: right after the C3 / C4 loops free their buckets (GiBs), the H2D
+    and D2H copies of C5 share those engines for ~0.3 s and C5 reads 39 ms instead of 23.5 ms
+    (tools/c5_pinned_probe.py: the same buffers, 23.4 ms once 0.3 s have passed). A pause of QUIET_S
+    seconds, outside every timed region."""
+    import fmi_amd
+
+    fmi_amd.sync()
+    time.sleep(QUIET_S)
 
 
 def c5_single(mib: int, iters: int = 3) -> dict:
@@ -517,9 +534,10 @@ def after_value(args, ar, world, dist, line, proc):
         if not chk["ok"]:
             line["self_check"] = dict(line["self_check"], ok=False, failed_in=f"c4 path {path}")
     if not args.no_c5:
+        quiet_device()
         line["c5"] = dict(ar.host_bench(args.c5_mib * MIB // 4),
                           workload=f"C5: {args.c5_mib} MiB f32 page-locked host bucket per rank, H2D + sharded "
-                                   f"allreduce + D2H pipelined")
+                                   f"allreduce + D2H pipelined", after_pause_s=QUIET_S)
     if args.no_diagnostics:
         return
     diag = line["diagnostics"] = {}
