@@ -225,9 +225,12 @@ def c2_kernel_signature():
     return f"{form}<fmi::dev::OpSum, float, {fmi_amd.tune_get(Tune.PAIR_UNROLL)}, {nt}>"
 
 
-def _roofline(kernel, algo_bytes, kernel_avg_ms, source, extra=None, pmc_key=None):
+def _roofline(kernel, algo_bytes, kernel_avg_ms, source, extra=None, pmc_key=None, profiled_shape=True):
+    """profiled_shape: the run uses the bucket size the committed PMC profiles were taken at (the default
+    256 MiB); otherwise the PMC bytes belong to another launch size and traffic is null."""
     achieved = algo_bytes / (kernel_avg_ms * 1e-3) / 1e9
-    traffic, traffic_src = pmc_traffic(pmc_key or kernel)
+    traffic, traffic_src = pmc_traffic(pmc_key or kernel) if profiled_shape else (
+        None, "not reported: the committed PMC profiles are of the default 256 MiB bucket, this run uses another size")
     r = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kernel,
          "kernel_avg_us": round(kernel_avg_ms * 1e3, 2), "algorithmic_bytes_per_launch": algo_bytes,
@@ -284,7 +287,8 @@ def run_single(args):
         b.free()
     roof = _roofline("pair_tile", 3 * nbytes, kernel_avg_ms,
                      "HIP events bracketing the K timed launches on the library stream",
-                     {"kernel_avg_us_isolated": round(isolated_us, 2)}, pmc_key=c2_kernel_signature())
+                     {"kernel_avg_us_isolated": round(isolated_us, 2)}, pmc_key=c2_kernel_signature(),
+                     profiled_shape=args.bucket_mib == 256)
     line = _headline(args, (nbytes / GIB) / (step_ms * 1e-3), step_ms,
                      "C2: 1-GPU pairwise float32 sum-reduce of two 256 MiB device-resident peer buckets",
                      "single GPU (2 peers resident)", n, roof)
@@ -473,7 +477,8 @@ def run_dist(args, world, rank, local_rank):
                       "timed region (N = 1: the allreduce launches no kernel)"),
                      {"launch_shape": kern["kernel"], "kernel_avg_us_isolated": kern["kernel_avg_us"],
                       "note": "the allreduce step is xGMI-bound (xgmi_roofline); this is its HBM-bound kernel"},
-                     pmc_key=f"tree_kernel<fmi::dev::OpSum, float, 0, {world}, false>")
+                     pmc_key=f"tree_kernel<fmi::dev::OpSum, float, 0, {world}, false>",
+                     profiled_shape=args.bucket_mib == 256)
     path_desc = {"tree": "all-to-all + fused tree kernel + all-gather (bit-exact)",
                  "rccl": "RCCL reduce-scatter + all-gather", "direct": "fused tree over IPC-mapped peer windows"}
     line = _headline(args, value, step_ms,
