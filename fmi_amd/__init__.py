@@ -9,12 +9,12 @@ Layout:
 """
 from ._lib import FmiError, LIB_PATH, load  # noqa: F401
 from .device import (  # noqa: F401
-    Alg, Bucket, DType, Event, HostRegistration, Op, PinnedArray, Stream, Tune, combine, describe, device_count,
-    finalize, host_reduce_pair, init, reduce_pair, reduce_tree, scan_peers, schedule_expr, sync, tune_get, tune_set,
+    Alg, Bucket, DType, Event, Graph, HostRegistration, Op, PinnedArray, Stream, Tune, combine, describe,
+    device_count, finalize, host_reduce_pair, init, reduce_pair, reduce_tree, scan_peers, schedule_expr, sync, tune_get, tune_set,
 )
 
 __all__ = [
-    "Alg", "Bucket", "DType", "Event", "FmiError", "HostRegistration", "LIB_PATH", "Op", "PinnedArray", "Stream",
+    "Alg", "Bucket", "DType", "Event", "FmiError", "Graph", "HostRegistration", "LIB_PATH", "Op", "PinnedArray", "Stream",
     "Tune", "combine", "describe", "device_count", "finalize", "host_reduce_pair", "init", "load", "reduce_pair",
     "reduce_tree", "scan_peers", "schedule_expr", "sync", "tune_get", "tune_set",
 ]

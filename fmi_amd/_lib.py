@@ -74,6 +74,10 @@ SIGNATURES = {
     "fmi_stream_wait_event": (_i, [_vp, _vp]),
     "fmi_event_sync": (_i, [_vp]),
     "fmi_event_elapsed_ms": (_i, [_c.POINTER(_c.c_float), _vp, _vp]),
+    "fmi_graph_capture_begin": (_i, [_vp]),
+    "fmi_graph_capture_end": (_i, [_vp, _c.POINTER(_vp)]),
+    "fmi_graph_launch": (_i, [_vp, _vp]),
+    "fmi_graph_destroy": (_i, [_vp]),
     "fmi_dev_reduce_pair": (_i, [_i, _i, _vp, _vp, _sz, _vp]),
     "fmi_dev_combine": (_i, [_i, _i, _vp, _vp, _vp, _sz, _vp]),
     "fmi_dev_reduce_tree": (_i, [_i, _i, _i, _vp, _c.POINTER(_vp), _i, _i, _sz, _vp]),

@@ -786,6 +786,47 @@ int fmi_event_elapsed_ms(float* ms, fmi_event_t start, fmi_event_t stop) {
     return FMI_OK;
 }
 
+// ---- HIP graphs -----------------------------------------------------------------------------------------
+int fmi_graph_capture_begin(fmi_stream_t stream) {
+    if (int rc = require_device()) return rc;
+    if (!stream) return fail(FMI_ERR_INVALID, "graph capture needs a stream from fmi_stream_create");
+    FMI_HIP_TRY(hipStreamBeginCapture(static_cast<hipStream_t>(stream), hipStreamCaptureModeThreadLocal));
+    return FMI_OK;
+}
+
+int fmi_graph_capture_end(fmi_stream_t stream, fmi_graph_t* graph) {
+    if (!stream || !graph) return fail(FMI_ERR_INVALID, "null argument");
+    *graph = nullptr;
+    hipGraph_t g = nullptr;
+    const hipError_t e = hipStreamEndCapture(static_cast<hipStream_t>(stream), &g);
+    if (e != hipSuccess || !g) {
+        if (g) (void)hipGraphDestroy(g);
+        // the failed call inside the capture left HIP's sticky last error set: clear it, so the next launch
+        // on this (now ordinary) stream does not report it as its own
+        (void)hipGetLastError();
+        return fail(FMI_ERR_HIP, std::string("graph capture failed (a call in the sequence is not capture-safe?): ") +
+                                     hipGetErrorString(e));
+    }
+    hipGraphExec_t x = nullptr;
+    const hipError_t ei = hipGraphInstantiate(&x, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    if (ei != hipSuccess) return fail(FMI_ERR_HIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(ei));
+    *graph = x;
+    return FMI_OK;
+}
+
+int fmi_graph_launch(fmi_graph_t graph, fmi_stream_t stream) {
+    if (!graph) return fail(FMI_ERR_INVALID, "null graph");
+    if (int rc = require_device()) return rc;
+    FMI_HIP_TRY(hipGraphLaunch(static_cast<hipGraphExec_t>(graph), resolve(stream)));
+    return FMI_OK;
+}
+
+int fmi_graph_destroy(fmi_graph_t graph) {
+    if (graph) FMI_HIP_TRY(hipGraphExecDestroy(static_cast<hipGraphExec_t>(graph)));
+    return FMI_OK;
+}
+
 // ---- hot path ----------------------------------------------------------------------------------------
 int fmi_dev_reduce_pair(int op, int dtype, void* inout, const void* in, size_t n, fmi_stream_t stream) {
     if (int rc = require_device()) return rc;

@@ -209,6 +209,38 @@ class Stream:
             self.handle = None
 
 
+class Graph:
+    """A launch sequence recorded once and replayed as one submission (fmi_graph_*): many small bucket
+    combines, where launch cost rather than HBM is the limit.
+
+        g = Graph.capture(stream, lambda: [reduce_pair(Op.SUM, a, b, stream=stream) for a, b in pairs])
+        g.launch(stream)   # every combine again, same buckets
+    """
+
+    def __init__(self, handle: int):
+        self.handle = handle
+
+    @classmethod
+    def capture(cls, stream: "Stream", record) -> "Graph":
+        _lib.call("fmi_graph_capture_begin", stream.handle)
+        h = ctypes.c_void_p()
+        try:
+            record()
+        finally:  # always end the capture, so a failure inside `record` leaves the stream usable
+            end_rc = _lib.load().fmi_graph_capture_end(stream.handle, ctypes.byref(h))
+        if end_rc != 0:
+            raise _lib.FmiError(end_rc, _lib.last_error())
+        return cls(h.value)
+
+    def launch(self, stream=None) -> None:
+        _lib.call("fmi_graph_launch", self.handle, _sptr(stream))
+
+    def destroy(self) -> None:
+        if self.handle:
+            _lib.call("fmi_graph_destroy", self.handle)
+            self.handle = None
+
+
 class Event:
     def __init__(self):
         h = ctypes.c_void_p()

@@ -125,6 +125,20 @@ int fmi_event_sync(fmi_event_t event);
 int fmi_stream_wait_event(fmi_stream_t stream, fmi_event_t event);
 int fmi_event_elapsed_ms(float* ms, fmi_event_t start, fmi_event_t stop);
 
+/* ---- HIP graphs: a launch-bound sequence (many small bucket combines, e.g. FMI's 1 MiB messages) is
+ * recorded once and replayed as one submission. Between capture_begin and capture_end on a stream made by
+ * fmi_stream_create, calls on that stream are recorded, not run. Capture-safe: fmi_dev_reduce_pair,
+ * fmi_dev_combine, the d2d / memset copies, and fmi_dev_reduce_tree / fmi_dev_scan_peers up to 16 peers
+ * (one fused kernel each). Everything else (host-ingress paths, communicators, P > 16 programs, which
+ * may allocate or synchronise) is not: that call or capture_end fails, the graph is discarded, and the
+ * stream must be destroyed and replaced (HIP leaves a stream whose capture was invalidated unusable).
+ * Pointers and sizes are frozen in the graph; replays recompute the same buckets. */
+typedef void* fmi_graph_t;
+int fmi_graph_capture_begin(fmi_stream_t stream);
+int fmi_graph_capture_end(fmi_stream_t stream, fmi_graph_t* graph);
+int fmi_graph_launch(fmi_graph_t graph, fmi_stream_t stream);
+int fmi_graph_destroy(fmi_graph_t graph);
+
 /* ---- the hot path ------------------------------------------------------------------------------ */
 /* Pairwise bucket combine: inout[i] = op(inout[i], in[i]) for i < n.
  * Replaces one application of the raw_func built by Communicator::convert_to_raw_function

@@ -1,0 +1,80 @@
+"""HIP graphs through the C-ABI (fmi_graph_*): a recorded sequence of bucket combines replays with the same
+results as the direct launches, against the oracle; a call that cannot be captured fails loudly (the stream
+is then replaced, as HIP leaves an invalidated capture's stream unusable)."""
+import numpy as np
+import pytest
+
+import fmi_amd
+from fmi_amd import Alg, Bucket, Graph, Op, Stream
+from oracle import fmi_oracle as orc
+from tests.test_gpu_parity import assert_bit_equal, inputs
+
+pytestmark = pytest.mark.gpu
+
+
+def test_graph_replays_combines_and_p_way_kernels(device):
+    s = Stream()
+    n = (1 << 18) + 5  # 1 MiB of f32 and a ragged tail
+    K = 24
+    a = [inputs(np.float32, n, 2 * k, seed=61) for k in range(K)]
+    b = [inputs(np.float32, n, 2 * k + 1, seed=61) for k in range(K)]
+    da, db = [Bucket.from_numpy(x) for x in a], [Bucket.from_numpy(x) for x in b]
+    peers = [inputs(np.int64, n, p, seed=62) for p in range(8)]
+    dp = [Bucket.from_numpy(x) for x in peers]
+    tree_out = Bucket(n, np.int64)
+    scan_out = [Bucket(n, np.int64) for _ in range(4)]
+
+    def record():
+        for k in range(K):
+            fmi_amd.reduce_pair(Op.SUM, da[k], db[k], stream=s)
+        fmi_amd.reduce_tree(Op.MAX, Alg.ALLREDUCE, tree_out, dp, stream=s)
+        fmi_amd.scan_peers(Op.SUM, Alg.SCAN, scan_out, dp[:4], stream=s)
+
+    g = Graph.capture(s, record)
+    s.sync()
+    for k in range(K):  # recorded, not run
+        assert_bit_equal(da[k].numpy(), a[k], f"bucket {k} untouched by the capture")
+    with np.errstate(all="ignore"):
+        once = [orc.pairwise("sum", a[k], b[k]) for k in range(K)]
+        twice = [orc.pairwise("sum", once[k], b[k]) for k in range(K)]
+        want_tree, _ = orc.allreduce(peers, orc.op_max)
+        want_scan, _ = orc.scan(peers[:4], orc.op_sum)
+    g.launch(s)
+    s.sync()
+    for k in range(K):
+        assert_bit_equal(da[k].numpy(), once[k], f"replay 1, bucket {k}")
+    assert_bit_equal(tree_out.numpy(), want_tree[0], "replayed fused tree")
+    for r in range(4):
+        assert_bit_equal(scan_out[r].numpy(), want_scan[r], f"replayed fused scan, peer {r}")
+    g.launch(s)  # in-place combines accumulate: the graph recomputes from the buckets as they are now
+    s.sync()
+    for k in range(K):
+        assert_bit_equal(da[k].numpy(), twice[k], f"replay 2, bucket {k}")
+    g.destroy()
+    s.destroy()
+
+
+def test_graph_capture_of_a_synchronising_call_fails_loudly(device):
+    s = Stream()
+    x, y = Bucket.from_numpy(np.ones(4096, np.float32)), Bucket.from_numpy(np.ones(4096, np.float32))
+
+    def record():
+        fmi_amd.reduce_pair(Op.SUM, x, y, stream=s)
+        s.sync()  # a host synchronisation cannot be recorded
+
+    with pytest.raises(fmi_amd.FmiError):
+        Graph.capture(s, record)
+    s.destroy()  # HIP leaves a stream whose capture was invalidated unusable: replace it (include/fmi_dev.h)
+    s = Stream()
+    assert np.all(x.numpy() == 1.0)  # nothing recorded ran
+    fmi_amd.reduce_pair(Op.SUM, x, y, stream=s)
+    s.sync()
+    assert np.all(x.numpy() == 2.0)
+    g = Graph.capture(s, lambda: fmi_amd.reduce_pair(Op.SUM, x, y, stream=s))  # capture works again
+    g.launch(s)
+    s.sync()
+    assert np.all(x.numpy() == 3.0)
+    g.destroy()
+    with pytest.raises(fmi_amd.FmiError):  # the library's own (null) stream is not capturable by callers
+        fmi_amd._lib.call("fmi_graph_capture_begin", None)
+    s.destroy()
