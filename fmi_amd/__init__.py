@@ -10,11 +10,11 @@ Layout:
 from ._lib import FmiError, LIB_PATH, load  # noqa: F401
 from .device import (  # noqa: F401
     Alg, Bucket, DType, Event, Graph, HostRegistration, Op, PinnedArray, Stream, Tune, combine, describe,
-    device_count, finalize, host_reduce_pair, init, reduce_pair, reduce_tree, scan_peers, schedule_expr, sync, tune_get, tune_set,
+    device_count, finalize, host_reduce_pair, init, reduce_pair, reduce_pair_batch, reduce_tree, scan_peers, schedule_expr, sync, tune_get, tune_set,
 )
 
 __all__ = [
     "Alg", "Bucket", "DType", "Event", "FmiError", "Graph", "HostRegistration", "LIB_PATH", "Op", "PinnedArray", "Stream",
-    "Tune", "combine", "describe", "device_count", "finalize", "host_reduce_pair", "init", "load", "reduce_pair",
+    "Tune", "combine", "describe", "device_count", "finalize", "host_reduce_pair", "init", "load", "reduce_pair", "reduce_pair_batch",
     "reduce_tree", "scan_peers", "schedule_expr", "sync", "tune_get", "tune_set",
 ]

@@ -79,6 +79,7 @@ SIGNATURES = {
     "fmi_graph_launch": (_i, [_vp, _vp]),
     "fmi_graph_destroy": (_i, [_vp]),
     "fmi_dev_reduce_pair": (_i, [_i, _i, _vp, _vp, _sz, _vp]),
+    "fmi_dev_reduce_pair_batch": (_i, [_i, _i, _vp, _i, _vp]),
     "fmi_dev_combine": (_i, [_i, _i, _vp, _vp, _vp, _sz, _vp]),
     "fmi_dev_reduce_tree": (_i, [_i, _i, _i, _vp, _c.POINTER(_vp), _i, _i, _sz, _vp]),
     "fmi_dev_scan_peers": (_i, [_i, _i, _i, _c.POINTER(_vp), _c.POINTER(_vp), _i, _sz, _vp]),

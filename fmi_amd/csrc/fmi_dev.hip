@@ -833,6 +833,69 @@ int fmi_dev_reduce_pair(int op, int dtype, void* inout, const void* in, size_t n
     return launch_combine(op, dtype, inout, inout, in, n, resolve(stream));
 }
 
+int fmi_dev_reduce_pair_batch(int op, int dtype, const fmi_pair_desc_t* descs, int count, fmi_stream_t stream) {
+    if (int rc = require_device()) return rc;
+    if (op < FMI_OP_SUM || op > FMI_OP_MIN) return fail(FMI_ERR_INVALID, "unknown op " + std::to_string(op));
+    const size_t esz = dtype_size(dtype);
+    if (esz == 0) return fail(FMI_ERR_INVALID, "unknown dtype " + std::to_string(dtype));
+    if (count < 0 || (count > 0 && !descs)) return fail(FMI_ERR_INVALID, "bad descriptor array");
+    // no descriptor may write bytes another one reads or writes (one launch runs them concurrently)
+    std::vector<std::pair<uintptr_t, uintptr_t>> writes;
+    for (int k = 0; k < count; ++k) {
+        if (descs[k].n == 0) continue;
+        if (!descs[k].inout || !descs[k].in) return fail(FMI_ERR_INVALID, "null bucket in descriptor " + std::to_string(k));
+        const uintptr_t w = reinterpret_cast<uintptr_t>(descs[k].inout);
+        writes.emplace_back(w, w + descs[k].n * esz);
+    }
+    std::sort(writes.begin(), writes.end());
+    for (size_t k = 1; k < writes.size(); ++k)
+        if (writes[k].first < writes[k - 1].second) return fail(FMI_ERR_INVALID, "batch descriptors' inout buckets overlap");
+    for (int k = 0; k < count; ++k) {
+        if (descs[k].n == 0) continue;
+        const uintptr_t r = reinterpret_cast<uintptr_t>(descs[k].in), re = r + descs[k].n * esz;
+        const uintptr_t own = reinterpret_cast<uintptr_t>(descs[k].inout);
+        auto it = std::upper_bound(writes.begin(), writes.end(), std::make_pair(re, uintptr_t(0)));
+        while (it != writes.begin()) {  // write ranges starting before `re`, latest first
+            --it;
+            if (it->second <= r) break;  // sorted and disjoint: nothing earlier reaches r
+            if (it->first != own) return fail(FMI_ERR_INVALID, "a batch descriptor reads another one's inout bucket");
+        }
+    }
+    hipStream_t s = resolve(stream);
+    const size_t W = 16 / esz;
+    PairBatch pb{};
+    int k = 0;
+    unsigned tiles = 0;
+    auto flush = [&]() -> int {
+        if (k == 0) return FMI_OK;
+        pb.count = k;
+        pb.first_tile[k] = tiles;
+        const int rc = launch_pair_batch(op, dtype, pb, s);
+        pb = PairBatch{};
+        k = 0;
+        tiles = 0;
+        return rc;
+    };
+    for (int d = 0; d < count; ++d) {
+        const fmi_pair_desc_t& x = descs[d];
+        if (x.n == 0) continue;
+        const size_t t = std::max<size_t>(1, (x.n / W + kPairBatchTile - 1) / kPairBatchTile);
+        if (!aligned16(x.inout) || !aligned16(x.in) || t > (size_t(1) << 20)) {  // unaligned, or large enough alone
+            if (int rc = launch_combine(op, dtype, x.inout, x.inout, x.in, x.n, s)) return rc;
+            continue;
+        }
+        if (k == kPairBatchMax || tiles + t > (size_t(1) << 22))
+            if (int rc = flush()) return rc;
+        pb.inout[k] = x.inout;
+        pb.in[k] = x.in;
+        pb.n[k] = x.n;
+        pb.first_tile[k] = tiles;
+        tiles += static_cast<unsigned>(t);
+        ++k;
+    }
+    return flush();
+}
+
 int fmi_dev_combine(int op, int dtype, void* out, const void* a, const void* b, size_t n, fmi_stream_t stream) {
     if (int rc = require_device()) return rc;
     return launch_combine(op, dtype, out, a, b, n, resolve(stream));

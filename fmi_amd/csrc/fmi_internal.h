@@ -133,6 +133,22 @@ int launch_chain_one_pass(int op, int dtype, bool scan, int P, const BlockedScan
 int launch_tree_blocks_one_pass(int op, int dtype, int alg, int P, const BlockedScanPtrs& ptrs, size_t n, int rank,
                                 hipStream_t s);
 
+// Many independent pairwise combines in one launch (fmi_dev_reduce_pair_batch, fmi_pair_batch.hip): up to
+// kPairBatchMax descriptors, every pointer 16-B aligned; workgroup t works on tile t - first_tile[k] of the
+// descriptor k with first_tile[k] <= t < first_tile[k + 1] (kPairBatchTile lane groups per tile).
+inline constexpr int kPairBatchMax = 64;
+inline constexpr unsigned kPairBatchBlock = 256;
+inline constexpr int kPairBatchUnroll = 4;
+inline constexpr size_t kPairBatchTile = size_t(kPairBatchBlock) * kPairBatchUnroll;
+struct PairBatch {
+    void* inout[kPairBatchMax];
+    const void* in[kPairBatchMax];
+    unsigned long long n[kPairBatchMax];         // elements
+    unsigned first_tile[kPairBatchMax + 1];      // prefix sums of the descriptors' tile counts
+    int count;
+};
+int launch_pair_batch(int op, int dtype, const PairBatch& pb, hipStream_t s);
+
 // Workgroups to cover `items` with `block` threads each (at least 1). Callers cap it before narrowing.
 inline size_t grid_for(size_t items, unsigned block) {
     const size_t g = (items + block - 1) / block;

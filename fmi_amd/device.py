@@ -280,6 +280,24 @@ def reduce_pair(op: Op, inout: Bucket, src: Bucket, n: Optional[int] = None, str
     _lib.call("fmi_dev_reduce_pair", int(op), int(inout.dtype), inout.ptr, src.ptr, n, _sptr(stream))
 
 
+class _PairDesc(ctypes.Structure):
+    _fields_ = [("inout", ctypes.c_void_p), ("in_", ctypes.c_void_p), ("n", ctypes.c_size_t)]
+
+
+def reduce_pair_batch(op: Op, pairs: Sequence, stream=None) -> None:
+    """inout = op(inout, in) for every (inout, in) bucket pair, batched into as few launches as possible
+    (fmi_dev_reduce_pair_batch): for many small buckets. All buckets share one dtype."""
+    if not pairs:
+        return
+    dtype = pairs[0][0].dtype
+    for a, b in pairs:
+        if a.dtype != dtype or b.dtype != dtype or b.n < a.n:
+            raise ValueError("reduce_pair_batch: one dtype for every bucket, and each `in` at least as long as its inout")
+    descs = (_PairDesc * len(pairs))(*[_PairDesc(a.ptr, b.ptr, a.n) for a, b in pairs])
+    _lib.call("fmi_dev_reduce_pair_batch", int(op), int(dtype), ctypes.cast(descs, ctypes.c_void_p), len(pairs),
+              _sptr(stream))
+
+
 def combine(op: Op, out: Bucket, a: Bucket, b: Bucket, stream=None) -> None:
     if not (out.dtype == a.dtype == b.dtype) or not (out.n == a.n == b.n):
         raise ValueError("combine: buckets must share dtype and length")

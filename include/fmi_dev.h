@@ -146,6 +146,19 @@ int fmi_graph_destroy(fmi_graph_t graph);
  * (reference src/comm/PeerToPeer.cpp:51,72,103,119,147,160,179). inout == in is allowed. */
 int fmi_dev_reduce_pair(int op, int dtype, void* inout, const void* in, size_t n, fmi_stream_t stream);
 
+/* Batched pairwise combine: for every descriptor k, descs[k].inout[i] = op(inout[i], in[i]) for
+ * i < descs[k].n, all of them in as few launches as possible (up to 64 descriptors per launch): the same
+ * bits as `count` calls of fmi_dev_reduce_pair, without a launch and its ramp per bucket — for many small
+ * buckets (FMI's 1 MiB messages). `descs` is host memory, read during the call. A descriptor's inout must
+ * not overlap another descriptor's inout or in (FMI_ERR_INVALID); inout == in is allowed. n = 0 entries are
+ * skipped; unaligned or very large buckets are combined by their own launch. Graph-capturable. */
+typedef struct {
+    void* inout;
+    const void* in;
+    size_t n;
+} fmi_pair_desc_t;
+int fmi_dev_reduce_pair_batch(int op, int dtype, const fmi_pair_desc_t* descs, int count, fmi_stream_t stream);
+
 /* Out-of-place pairwise combine: out[i] = op(a[i], b[i]); out may alias a or b. */
 int fmi_dev_combine(int op, int dtype, void* out, const void* a, const void* b, size_t n,
                     fmi_stream_t stream);

@@ -7,7 +7,7 @@ import pytest
 import fmi_amd
 from fmi_amd import Alg, Bucket, Graph, Op, Stream
 from oracle import fmi_oracle as orc
-from tests.test_gpu_parity import assert_bit_equal, inputs
+from tests.test_gpu_parity import OPNAME, assert_bit_equal, inputs
 
 pytestmark = pytest.mark.gpu
 
@@ -77,4 +77,47 @@ def test_graph_capture_of_a_synchronising_call_fails_loudly(device):
     g.destroy()
     with pytest.raises(fmi_amd.FmiError):  # the library's own (null) stream is not capturable by callers
         fmi_amd._lib.call("fmi_graph_capture_begin", None)
+    s.destroy()
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.int64, np.uint8, np.float64], ids=lambda d: np.dtype(d).name)
+def test_pair_batch_matches_separate_combines(device, dtype):
+    """fmi_dev_reduce_pair_batch: many buckets of mixed sizes (empty, below one 16-B lane group, ragged,
+    several tiles) and more descriptors than one launch takes (64), every op, against the oracle; an
+    unaligned bucket in the batch takes its own launch."""
+    sizes = [0, 1, 3, 17, 4099, 65536 + 7, 1 << 18, 5] * 12  # 96 descriptors
+    for op in (Op.SUM, Op.PROD, Op.MAX, Op.MIN):
+        a = [inputs(dtype, n, 2 * k, seed=71) for k, n in enumerate(sizes)]
+        b = [inputs(dtype, n, 2 * k + 1, seed=71) for k, n in enumerate(sizes)]
+        da = [Bucket.from_numpy(x) for x in a]
+        db = [Bucket.from_numpy(x) for x in b]
+        pairs = list(zip(da, db))
+        big = Bucket.from_numpy(np.concatenate([a[6], a[6][:1]]))  # an unaligned view as one more inout
+        unaligned = big.view(1, sizes[6])
+        ua = big.numpy()[1:].copy()
+        pairs.append((unaligned, db[6]))
+        fmi_amd.reduce_pair_batch(op, pairs)
+        fmi_amd.sync()
+        with np.errstate(all="ignore"):
+            for k in range(len(sizes)):
+                assert_bit_equal(da[k].numpy(), orc.pairwise(OPNAME[op], a[k], b[k]), f"{op.name} descriptor {k}")
+            assert_bit_equal(unaligned.numpy(), orc.pairwise(OPNAME[op], ua, b[6]), f"{op.name} unaligned")
+
+
+def test_pair_batch_rejects_overlap_and_is_graph_capturable(device):
+    x = Bucket.from_numpy(np.ones(8192, np.float32))
+    y = Bucket.from_numpy(np.ones(8192, np.float32))
+    with pytest.raises(fmi_amd.FmiError):  # two descriptors writing the same bytes
+        fmi_amd.reduce_pair_batch(Op.SUM, [(x.view(0, 4096), y.view(0, 4096)), (x.view(1024, 4096), y.view(0, 4096))])
+    with pytest.raises(fmi_amd.FmiError):  # one reads what another writes
+        fmi_amd.reduce_pair_batch(Op.SUM, [(x.view(0, 4096), y.view(0, 4096)), (y.view(0, 4096), x.view(0, 4096))])
+    s = Stream()
+    g = Graph.capture(s, lambda: fmi_amd.reduce_pair_batch(Op.SUM, [(x.view(0, 4096), y.view(0, 4096)),
+                                                                      (x.view(4096, 4096), y.view(4096, 4096))],
+                                                           stream=s))
+    g.launch(s)
+    g.launch(s)
+    s.sync()
+    assert np.all(x.numpy() == 3.0)
+    g.destroy()
     s.destroy()

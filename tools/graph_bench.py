@@ -1,5 +1,6 @@
-"""Small-message combines (FMI's C1 shape: 1 MiB f32 buckets) launched one by one vs replayed from a HIP
-graph (fmi_graph_*): K = 256 pairwise combines over distinct bucket pairs per submission, median of rounds.
+"""Small-message combines (FMI's C1 shape: 1 MiB f32 buckets) launched one by one, replayed from a HIP graph
+(fmi_graph_*), batched into one launch per 64 (fmi_dev_reduce_pair_batch), and the batch replayed from a
+graph: K = 256 pairwise combines over distinct bucket pairs per submission, median of rounds.
 
     python tools/graph_bench.py [--kib 1024] [--k 256] [--rounds 7]
 """
@@ -35,8 +36,15 @@ def main():
             fmi_amd.reduce_pair(Op.SUM, a, b, stream=s)
 
     g = Graph.capture(s, launches)
+    from fmi_amd import reduce_pair_batch
+
+    def batch():
+        reduce_pair_batch(Op.SUM, pairs, stream=s)
+
+    gb = Graph.capture(s, batch)
     res = {}
-    for name, fn in (("launches", launches), ("graph", lambda: g.launch(s))):
+    for name, fn in (("launches", launches), ("graph", lambda: g.launch(s)), ("batch", batch),
+                     ("batch_graph", lambda: gb.launch(s))):
         dev_us, wall_us = [], []
         for _ in range(args.rounds):
             fn()
@@ -58,6 +66,7 @@ def main():
         v["frac_of_8TBs"] = round(algo / (v["us_per_combine_device"] * 1e-6) / 8e12, 4)
     print(json.dumps({"bucket_kib": args.kib, "combines_per_submission": args.k, **res}), flush=True)
     g.destroy()
+    gb.destroy()
     s.destroy()
 
 
