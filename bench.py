@@ -348,12 +348,16 @@ def c3_single(reps: int = 60) -> dict:
     for b in [x for s in ins + outs for x in s]:
         b.free()
 
-    def row(ms, algo):
+    def row(ms, algo, key):
+        traffic, src = pmc_traffic(key)  # the committed PMC profile of exactly this instantiation
         return {"kernel_avg_us": round(ms * 1e3, 2), "algorithmic_bytes": algo,
-                "GB_s": round(algo / (ms * 1e-3) / 1e9, 1), "frac": round(algo / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+                "GB_s": round(algo / (ms * 1e-3) / 1e9, 1), "frac": round(algo / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                "traffic": traffic, "traffic_source": src}
 
-    return {"i64_max_pair_64MiB": dict(row(ms_max, 3 * 64 * MIB), rotating_sets=8),
-            "f32_scan_P8_64MiB": dict(row(ms_scan, 2 * P * 64 * MIB), rotating_sets=2),
+    return {"i64_max_pair_64MiB": dict(row(ms_max, 3 * 64 * MIB, "pair_tile<fmi::dev::OpMax, long, 4, 3>"),
+                                       rotating_sets=8),
+            "f32_scan_P8_64MiB": dict(row(ms_scan, 2 * P * 64 * MIB, "scan_kernel<fmi::dev::OpSum, float, 3, 8>"),
+                                      rotating_sets=2),
             "timing": "two HIP events around back-to-back launches on the library stream (gaps included)"}
 
 

@@ -72,3 +72,10 @@ def test_roofline_traffic_is_the_launched_kernels():
     for world, shard_mib in ((2, 128), (4, 64), (8, 32)):
         t, _ = bench.pmc_traffic(f"tree_kernel<fmi::dev::OpSum, float, 0, {world}, false>")
         assert t is not None and abs(t / ((world + 1) * shard_mib * (1 << 20)) - 1) < 0.01, (world, t)
+
+
+def test_c3_rows_find_their_pmc_profiles():
+    for key, algo in (("pair_tile<fmi::dev::OpMax, long, 4, 3>", 3 * 64 * (1 << 20)),
+                      ("scan_kernel<fmi::dev::OpSum, float, 3, 8>", 16 * 64 * (1 << 20))):
+        t, _ = bench.pmc_traffic(key)
+        assert t is not None and abs(t / algo - 1) < 0.01, (key, t)
