@@ -183,14 +183,43 @@ __device__ __forceinline__ Lanes<T, W> combine(const Lanes<T, W>& a, const Lanes
     }
 }
 
+// Buffer-op form of the fused kernels' 16-B accesses (pol = 1, FMI_TUNE_FUSED_POLICY): every access of a
+// 256-thread tile goes through a descriptor based at the tile's first byte of that bucket (a uniform
+// 64-bit address, so any bucket size) with the lane's 32-bit byte offset, and carries an explicit cache
+// policy: loads nt; the tree's one output stream sc1 (written lines leave the XCD L2 at once), the scan's
+// P output streams nt sc1. tools/microbench_cachepol.hip measured, on the same buffers, tree P = 8 3.3 %
+// and scan P = 8 4.6 % faster than global_load / global_store nt (bit-identical results). The pairwise
+// kernel keeps global nt accesses and stores only its last tiles with sc1 (pair_tile below).
+inline constexpr int kAuxNT = 2, kAuxSC1 = 16;
+inline constexpr int kTreeStoreAux = kAuxSC1, kScanStoreAux = kAuxNT | kAuxSC1, kFusedLoadAux = kAuxNT;
+using b128 = unsigned int __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const void* tile_base) {
+    // raw (stride 0) descriptor, 32-bit data format; num_records covers any 256-thread tile
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(tile_base), 0, 1 << 30, 0x00020000);
+}
+template <int AUX, class T, int W>
+__device__ __forceinline__ Lanes<T, W> load_tile(const void* bucket, size_t tile_byte, unsigned lane_byte) {
+    static_assert(sizeof(T) * W == 16, "16-B lane groups");
+    const b128 r = __builtin_amdgcn_raw_buffer_load_b128(tile_rsrc(static_cast<const char*>(bucket) + tile_byte), lane_byte, 0, AUX);
+    return __builtin_bit_cast(Lanes<T, W>, r);
+}
+template <int AUX, class T, int W>
+__device__ __forceinline__ void store_tile(void* bucket, size_t tile_byte, unsigned lane_byte, const Lanes<T, W>& x) {
+    static_assert(sizeof(T) * W == 16, "16-B lane groups");
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(b128, x), tile_rsrc(static_cast<char*>(bucket) + tile_byte),
+                                           lane_byte, 0, AUX);
+}
+
 // ---------------------------------------------------------------------------------------------------
 // Pairwise combine. A "tile" is U vectors per thread: thread t of block b owns vectors
 // b*U*B + u*B + t (u < U), so each of the U wave-instructions is one contiguous 1-KiB access and each
 // thread keeps 2U independent 16-B loads in flight before its first add.
 // ---------------------------------------------------------------------------------------------------
-// NT: cache policy bitmask — bit 0 nontemporal loads, bit 1 nontemporal stores.
+// NT: cache policy bitmask — bit 0 nontemporal loads, bit 1 nontemporal stores. `sc1` (uniform per tile):
+// store this tile with sc1 instead (pair_tile's tail tiles, FMI_TUNE_PAIR_TAIL_KIB).
 template <class Op, class T, int U, int NT>
-__device__ __forceinline__ void pair_tile_body(T* out, const T* a, const T* b, size_t nvec, size_t tile) {
+__device__ __forceinline__ void pair_tile_body(T* out, const T* a, const T* b, size_t nvec, size_t tile, bool sc1 = false) {
     constexpr int W = kVecLanes<T>;
     constexpr bool NTL = (NT & 1) != 0;
     constexpr bool NTS = (NT & 2) != 0;
@@ -204,8 +233,18 @@ __device__ __forceinline__ void pair_tile_body(T* out, const T* a, const T* b, s
             va[u] = load_lanes<NTL, T, W>(a + (base + u * B) * W);
             vb[u] = load_lanes<NTL, T, W>(b + (base + u * B) * W);
         }
+        // one descriptor at the tile's first output byte, lane offsets < U * B * 16 (U = 8: not taken; the
+        // second store path spills the 8-bit max / min forms to scratch under the 1024-thread bound)
+        if (U <= 4 && sc1) {
+            const size_t tile_byte = tile * U * B * 16;
 #pragma unroll
-        for (int u = 0; u < U; ++u) store_lanes<NTS, T, W>(out + (base + u * B) * W, combine<Op, T, W>(va[u], vb[u]));
+            for (int u = 0; u < U; ++u)
+                store_tile<kAuxSC1, T, W>(out, tile_byte, static_cast<unsigned>((u * B + threadIdx.x) * 16),
+                                          combine<Op, T, W>(va[u], vb[u]));
+        } else {
+#pragma unroll
+            for (int u = 0; u < U; ++u) store_lanes<NTS, T, W>(out + (base + u * B) * W, combine<Op, T, W>(va[u], vb[u]));
+        }
     } else {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -233,15 +272,19 @@ __device__ __forceinline__ void pair_tail(T* out, const T* a, const T* b, size_t
     }
 }
 
-// One-shot grid: one tile per workgroup. Pointers must be 16-B aligned.
+// One-shot grid: one tile per workgroup. Pointers must be 16-B aligned. Whole tiles from `sc1_from` on
+// store with sc1 (default: none, the round-1 kernel the exploration tools compare against): the end of the launch then leaves little dirty data in the XCD L2s for the release to
+// write back (C3 i64 max 64 MiB: 31.9 -> 30.6 us, C2 -1 %; tools/microbench_tailsweep.hip).
 template <class Op, class T, int U, int NT>
-__global__ void __launch_bounds__(1024) pair_tile(T* out, const T* a, const T* b, size_t n) {
+__global__ void __launch_bounds__(1024) pair_tile(T* out, const T* a, const T* b, size_t n,
+                                                     size_t sc1_from = ~size_t(0)) {
     const size_t nvec = n / kVecLanes<T>;
-    pair_tile_body<Op, T, U, NT>(out, a, b, nvec, blockIdx.x);
+    pair_tile_body<Op, T, U, NT>(out, a, b, nvec, blockIdx.x, blockIdx.x >= sc1_from);
     pair_tail<Op, T>(out, a, b, n);
 }
 
-// Grid-stride: a fixed grid (k workgroups per CU) walks the tiles. Pointers must be 16-B aligned.
+// Grid-stride: a fixed grid (k workgroups per CU) walks the tiles. Pointers must be 16-B aligned. Every
+// tile stores nontemporal (a second store path inside the loop spills the U = 8 forms to scratch).
 template <class Op, class T, int U, int NT>
 __global__ void __launch_bounds__(1024) pair_stride(T* out, const T* a, const T* b, size_t n) {
     const size_t nvec = n / kVecLanes<T>;
@@ -328,33 +371,6 @@ __device__ __forceinline__ void store_all(const Lanes<T, W>* v, const PeerPtrs& 
     ((store_lanes<kFusedNT, T, W>(static_cast<T*>(ptrs.out[R]) + elem, v[kOut<ALG, P, R>])), ...);
 }
 
-// Buffer-op form of the fused kernels' 16-B accesses (pol = 1, FMI_TUNE_FUSED_POLICY): every access of a
-// 256-thread tile goes through a descriptor based at the tile's first byte of that bucket (a uniform
-// 64-bit address, so any bucket size) with the lane's 32-bit byte offset, and carries an explicit cache
-// policy: loads nt; the tree's one output stream sc1 (written lines leave the XCD L2 at once), the scan's
-// P output streams nt sc1. tools/microbench_cachepol.hip measured, on the same buffers, tree P = 8 3.3 %
-// and scan P = 8 4.6 % faster than global_load / global_store nt (bit-identical results); the pairwise
-// kernel gained nothing and keeps its global accesses.
-inline constexpr int kAuxNT = 2, kAuxSC1 = 16;
-inline constexpr int kTreeStoreAux = kAuxSC1, kScanStoreAux = kAuxNT | kAuxSC1, kFusedLoadAux = kAuxNT;
-using b128 = unsigned int __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const void* tile_base) {
-    // raw (stride 0) descriptor, 32-bit data format; num_records covers any 256-thread tile
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(tile_base), 0, 1 << 30, 0x00020000);
-}
-template <int AUX, class T, int W>
-__device__ __forceinline__ Lanes<T, W> load_tile(const void* bucket, size_t tile_byte, unsigned lane_byte) {
-    static_assert(sizeof(T) * W == 16, "16-B lane groups");
-    const b128 r = __builtin_amdgcn_raw_buffer_load_b128(tile_rsrc(static_cast<const char*>(bucket) + tile_byte), lane_byte, 0, AUX);
-    return __builtin_bit_cast(Lanes<T, W>, r);
-}
-template <int AUX, class T, int W>
-__device__ __forceinline__ void store_tile(void* bucket, size_t tile_byte, unsigned lane_byte, const Lanes<T, W>& x) {
-    static_assert(sizeof(T) * W == 16, "16-B lane groups");
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(b128, x), tile_rsrc(static_cast<char*>(bucket) + tile_byte),
-                                           lane_byte, 0, AUX);
-}
 template <class T, int W, int P, size_t... I>
 __device__ __forceinline__ void load_peers_tile(Lanes<T, W>* v, const PeerPtrs& ptrs, size_t tile_byte, unsigned lane_byte,
                                                 std::index_sequence<I...>) {

@@ -331,10 +331,15 @@ typedef enum {
                                     all-gather runs on a second stream and communicator (ncclCommSplit)
                                     while chunk k + 1's all-to-all and kernel run; chunks of >= 1 MiB per
                                     rank only. Same bits (element-wise); every rank must set the same K */
-    FMI_TUNE_FUSED_POLICY = 11    /* fused P-way kernels (tree, scan; <= 16 peers), 16-B accesses: 2 = buffer
+    FMI_TUNE_FUSED_POLICY = 11,   /* fused P-way kernels (tree, scan; <= 16 peers), 16-B accesses: 2 = buffer
                                     loads nt with sc1 (tree) / nt sc1 (scan) stores; 0 = global_load /
                                     global_store nt; 1 = auto (default): 2 for trees of >= 4 and scans of
                                     >= 8 peers, 0 otherwise (tools/ab_fused_policy.py). Same bits always */
+    FMI_TUNE_PAIR_TAIL_KIB = 12   /* pairwise kernel (16-B aligned buckets): the last KiB of output of each
+                                    launch are stored with sc1 (the written lines leave the XCD L2 at once)
+                                    instead of nontemporal, so less dirty L2 data is left for the release at
+                                    the end of the launch; 0 = every tile nontemporal. Default 32768 (32 MiB,
+                                    tools/microbench_tailsweep.hip). Same bits always */
 } fmi_tune_key_t;
 int fmi_tune_set(int key, long long value);
 int fmi_tune_get(int key, long long* value);

@@ -145,6 +145,12 @@ def test_tuning_knobs_validate():
         assert fmi_amd.tune_get(fmi_amd.Tune.FUSED_POLICY) == v
     with pytest.raises(fmi_amd.FmiError):
         fmi_amd.tune_set(fmi_amd.Tune.FUSED_POLICY, 3)
+    assert fmi_amd.tune_get(fmi_amd.Tune.PAIR_TAIL_KIB) == 32768  # default (tools/microbench_tailsweep.hip)
+    for v in (0, 1, 32768):
+        fmi_amd.tune_set(fmi_amd.Tune.PAIR_TAIL_KIB, v)
+        assert fmi_amd.tune_get(fmi_amd.Tune.PAIR_TAIL_KIB) == v
+    with pytest.raises(fmi_amd.FmiError):
+        fmi_amd.tune_set(fmi_amd.Tune.PAIR_TAIL_KIB, -1)
     for key in (fmi_amd.Tune.COMM_A2A, fmi_amd.Tune.COMM_GATHER):  # RCCL exchange realisations
         assert fmi_amd.tune_get(key) == 0
         fmi_amd.tune_set(key, 1)

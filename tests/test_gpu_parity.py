@@ -124,6 +124,32 @@ def test_reduce_pair_every_launch_variant(device, variant, unroll, block):
             fmi_amd.tune_set(k, v)
 
 
+@pytest.mark.parametrize("dtype", [np.float32, np.int64, np.int8], ids=lambda d: np.dtype(d).name)
+@pytest.mark.parametrize("tail_kib", [0, 1, 16, 48, 100, 32768])
+def test_reduce_pair_sc1_tail_keeps_bits(device, dtype, tail_kib):
+    """FMI_TUNE_PAIR_TAIL_KIB moves the boundary between the nontemporal tiles and the sc1-stored tail tiles
+    of one launch (none, one tile, a few, most, all); the ragged last tile and the < 16-B tail stay where they
+    are. Every position gives the oracle's bits, with the launch variants that honour the tail (one-shot
+    tiles at unroll 1 / 4 and 256 / 1024 threads)."""
+    n = 3 * 4096 * 16 // np.dtype(dtype).itemsize + 4099  # > 3 tiles of 64 KiB at unroll 4, ragged end
+    a, b = inputs(dtype, n, 0), inputs(dtype, n, 1)
+    with np.errstate(all="ignore"):
+        want = orc.pairwise("max" if dtype == np.int64 else "sum", a, b)
+    keys = (Tune.PAIR_TAIL_KIB, Tune.PAIR_UNROLL, Tune.BLOCK)
+    old = {k: fmi_amd.tune_get(k) for k in keys}
+    try:
+        fmi_amd.tune_set(Tune.PAIR_TAIL_KIB, tail_kib)
+        for unroll, block in [(4, 256), (1, 256), (4, 1024)]:
+            fmi_amd.tune_set(Tune.PAIR_UNROLL, unroll)
+            fmi_amd.tune_set(Tune.BLOCK, block)
+            da, db = dev(a), dev(b)
+            fmi_amd.reduce_pair(Op.MAX if dtype == np.int64 else Op.SUM, da, db)
+            assert_bit_equal(da.numpy(), want, f"tail {tail_kib} KiB, unroll {unroll}, block {block}")
+    finally:
+        for k, v in old.items():
+            fmi_amd.tune_set(k, v)
+
+
 def test_combine_out_of_place(device):
     a, b = inputs(np.int64, 5003, 0), inputs(np.int64, 5003, 1)
     out = Bucket(5003, np.int64)
