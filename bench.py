@@ -59,7 +59,11 @@ def parse():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--bucket-mib", type=int, default=256)
     ap.add_argument("--c4-mib", type=int, default=1024, help="N>1: bucket per peer of the c4 block (config C4)")
-    ap.add_argument("--sets", type=int, default=4, help="rotating bucket sets (defeats the 256 MiB MALL)")
+    ap.add_argument("--sets", type=int, default=16,
+                    help="N=1: rotating bucket sets. The pair kernel's sc1 tiles (1 of 8) leave their output lines in "
+                         "the 256 MB MALL, which nontemporal reads do not displace: 16 sets put 15 x 32 MiB of sc1 "
+                         "writes between two uses of a set, so no step re-reads a bucket from the MALL")
+    ap.add_argument("--dist-sets", type=int, default=4, help="N>1: rotating bucket sets of the sharded allreduce")
     ap.add_argument("--path", default="tree", choices=["tree", "rccl", "direct"],
                     help="N>1 headline exchange: tree = all-to-all + fused kernel (bit-exact), rccl = "
                          "reduce-scatter + all-gather, direct = fused kernel over IPC-mapped peer windows")
@@ -254,7 +258,7 @@ def run_single(args):
     sets = [tuple(Bucket(n, np.float32).fill_synthetic(42 + s, j) for j in range(2)) for s in range(args.sets)]
     fmi_amd.sync()
 
-    def step(k):
+    def step(k):  # k runs on from the warm-up, so every set is re-used exactly len(sets) steps later
         a, b = sets[k % len(sets)]
         fmi_amd.reduce_pair(Op.SUM, a, b)
 
@@ -266,7 +270,7 @@ def run_single(args):
     ev0, ev1 = Event(), Event()
     t0 = time.perf_counter()
     ev0.record()
-    for k in range(args.steps):
+    for k in range(args.warmup, args.warmup + args.steps):
         step(k)
     ev1.record()
     fmi_amd.sync()
@@ -278,7 +282,7 @@ def run_single(args):
     pairs = [(Event(), Event()) for _ in range(probe)]
     for k in range(probe):
         pairs[k][0].record()
-        step(k)
+        step(args.warmup + args.steps + k)
         pairs[k][1].record()
     fmi_amd.sync()
     isolated_us = 1e3 * sum(a.elapsed_ms(b) for a, b in pairs) / probe
@@ -310,22 +314,26 @@ def run_single(args):
     print(json.dumps(line), flush=True)
 
 
+C3_PAIR_SETS = 64  # 63 x 8 MiB of sc1 tile writes between two uses of a set (see --sets)
+
+
 def c3_single(reps: int = 60) -> dict:
-    """Config C3 on this GPU, in the driver's run: the int64 max pairwise combine of 64 MiB buckets (8
-    rotating sets, 1.5 GiB: beyond the 256 MiB MALL) and the f32 peer-axis scan (scan_no_order) of 8 peers x
-    64 MiB (2 rotating sets); mean launch time from two HIP events around back-to-back launches on the library
-    stream, against the algorithmic bytes (3 x 64 MiB and 2 x 8 x 64 MiB)."""
+    """Config C3 on this GPU, in the driver's run: the int64 max pairwise combine of 64 MiB buckets (64
+    rotating sets, 8 GiB: no set is re-read from the 256 MiB MALL) and the f32 peer-axis scan (scan_no_order)
+    of 8 peers x 64 MiB (2 rotating sets: each launch writes 512 MiB); mean launch time from two HIP events
+    around back-to-back launches on the library stream, against the algorithmic bytes (3 x 64 MiB and
+    2 x 8 x 64 MiB)."""
     import numpy as np
 
     import fmi_amd
     from fmi_amd import Alg, Bucket, Event, Op
 
-    def timed(launch, k):
+    def timed(launch, k):  # the set index runs on from the warm-up: every set is re-used `sets` launches later
         for i in range(3):
             launch(i)
         e0, e1 = Event(), Event()
         e0.record()
-        for i in range(k):
+        for i in range(3, 3 + k):
             launch(i)
         e1.record()
         e1.sync()
@@ -336,8 +344,8 @@ def c3_single(reps: int = 60) -> dict:
 
     n64 = 64 * MIB // 8
     pairs = [(Bucket(n64, np.int64).fill_synthetic(42 + s, 0), Bucket(n64, np.int64).fill_synthetic(42 + s, 1))
-             for s in range(8)]
-    ms_max = timed(lambda i: fmi_amd.reduce_pair(Op.MAX, *pairs[i % 8]), reps)
+             for s in range(C3_PAIR_SETS)]
+    ms_max = timed(lambda i: fmi_amd.reduce_pair(Op.MAX, *pairs[i % C3_PAIR_SETS]), reps)
     for a, b in pairs:
         a.free()
         b.free()
@@ -355,7 +363,7 @@ def c3_single(reps: int = 60) -> dict:
                 "traffic": traffic, "traffic_source": src}
 
     return {"i64_max_pair_64MiB": dict(row(ms_max, 3 * 64 * MIB, "pair_tile<fmi::dev::OpMax, long, 4, 3>"),
-                                       rotating_sets=8),
+                                       rotating_sets=C3_PAIR_SETS),
             "f32_scan_P8_64MiB": dict(row(ms_scan, 2 * P * 64 * MIB, "scan_kernel<fmi::dev::OpSum, float, 3, 8>"),
                                       rotating_sets=2),
             "timing": "two HIP events around back-to-back launches on the library stream (gaps included)"}
@@ -465,7 +473,7 @@ def run_dist(args, world, rank, local_rank):
     ar = CommAllreduce(dist.group.WORLD, path=args.path, transport=args.transport)
     n = args.bucket_mib * MIB // 4
     S = n * 4
-    step_ms, _, extra = ar.bench(n, steps=args.steps, warmup=args.warmup, sets=args.sets, peers_per_gpu=1)
+    step_ms, _, extra = ar.bench(n, steps=args.steps, warmup=args.warmup, sets=args.dist_sets, peers_per_gpu=1)
     out, seed = extra.pop("result")
     value = world * (S / GIB) / (step_ms * 1e-3)
     check = ar.self_check(out, n, seed, tolerance=args.path == "rccl")
@@ -490,7 +498,8 @@ def run_dist(args, world, rank, local_rank):
                      f"(a {args.bucket_mib} MiB device-resident bucket) per GPU, through fmi_comm_allreduce",
                      f"{world} GPUs, one peer per GPU, buckets sharded {world} ways; path {args.path}: "
                      f"{path_desc[args.path]}; transport {args.transport}", n, roof)
-    line["config"].update({"numa_binding_rank0": numa, "peers": world, "path": args.path, "transport": args.transport,
+    line["config"].update({"rotating_sets": args.dist_sets, "numa_binding_rank0": numa, "peers": world,
+                           "path": args.path, "transport": args.transport,
                            "algbw_GiB_s": extra["algbw_GiB_s"], "busbw_GiB_s": extra["busbw_GiB_s"],
                            "shard_elems": extra["shard_elems"]})
     line["self_check"] = check
@@ -610,7 +619,7 @@ def replicated_pairs(args, ar) -> dict:
 
     n = args.bucket_mib * MIB // 4
     sets = [tuple(Bucket(n, np.float32).fill_synthetic(42 + s, 2 * ar.rank + j) for j in range(2))
-            for s in range(args.sets)]
+            for s in range(args.dist_sets)]
     steps = max(20, args.steps // 4)
     for k in range(5):
         fmi_amd.reduce_pair(Op.SUM, *sets[k % len(sets)])

@@ -42,7 +42,7 @@ std::atomic<long long> g_tune[13] = {2 /*variant: nontemporal tiles*/, 4 /*unrol
                                      64 /*fused in-flight KiB per CU (tools/ab_fused_cap.py)*/,
                                      1 /*one-pass blocked scan*/, 0 /*ncclAllToAll*/, 0 /*ncclAllGather*/,
                                      0 /*no allreduce pipelining*/, 1 /*fused kernels: buffer ops where measured faster*/,
-                                     32768 /*pairwise: last 32 MiB of output stored sc1 (tools/microbench_tailsweep.hip)*/};
+                                     1 /*pairwise: tiles t % 8 < 1 (one XCD) store sc1 (tools/ab_pair_sc1.py)*/};
 
 int hip_fail(const char* what, hipError_t e) {
     return fail(FMI_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
@@ -107,11 +107,7 @@ int launch_pair_vec(T* out, const T* a, const T* b, size_t n, hipStream_t s) {
     const size_t nvec = n / kVecLanes<T>;
     const size_t per_block = static_cast<size_t>(block) * static_cast<size_t>(unroll);
     const size_t ntiles = std::max<size_t>(1, (nvec + per_block - 1) / per_block);
-    // one-shot tiles [sc1_from, ntiles) store with sc1: the last FMI_TUNE_PAIR_TAIL_KIB of output (16 B per
-    // lane group)
-    const size_t tail_tiles = (static_cast<size_t>(g_tune[FMI_TUNE_PAIR_TAIL_KIB].load()) * 1024 + per_block * 16 - 1) /
-                              (per_block * 16);
-    const size_t sc1_from = ntiles > tail_tiles ? ntiles - tail_tiles : 0;
+    const unsigned sc1_k = static_cast<unsigned>(g_tune[FMI_TUNE_PAIR_SC1_OF_8].load());  // one-shot tiles t % 8 < k: sc1
     // One-shot tiles unless the grid would pass HIP's 2^32-thread limit (buckets of > 2^31 tiles' worth):
     // then the grid-stride form walks the tiles.
     constexpr size_t kMaxGridThreads = size_t(1) << 31;
@@ -128,10 +124,10 @@ int launch_pair_vec(T* out, const T* a, const T* b, size_t n, hipStream_t s) {
     } else {
         const unsigned grid = static_cast<unsigned>(ntiles);
         switch (unroll) {
-            case 1: pair_tile<Op, T, 1, NT><<<grid, block, 0, s>>>(out, a, b, n, sc1_from); break;
-            case 2: pair_tile<Op, T, 2, NT><<<grid, block, 0, s>>>(out, a, b, n, sc1_from); break;
-            case 4: pair_tile<Op, T, 4, NT><<<grid, block, 0, s>>>(out, a, b, n, sc1_from); break;
-            case 8: pair_tile<Op, T, 8, NT><<<grid, block, 0, s>>>(out, a, b, n, sc1_from); break;
+            case 1: pair_tile<Op, T, 1, NT><<<grid, block, 0, s>>>(out, a, b, n, sc1_k); break;
+            case 2: pair_tile<Op, T, 2, NT><<<grid, block, 0, s>>>(out, a, b, n, sc1_k); break;
+            case 4: pair_tile<Op, T, 4, NT><<<grid, block, 0, s>>>(out, a, b, n, sc1_k); break;
+            case 8: pair_tile<Op, T, 8, NT><<<grid, block, 0, s>>>(out, a, b, n, sc1_k); break;
             default: return fail(FMI_ERR_INVALID, "unroll must be 1, 2, 4 or 8");
         }
     }
@@ -1120,8 +1116,8 @@ int fmi_tune_set(int key, long long value) {
         case FMI_TUNE_FUSED_POLICY:
             if (value < 0 || value > 2) return fail(FMI_ERR_INVALID, "fused access policy must be 0, 1 or 2");
             break;
-        case FMI_TUNE_PAIR_TAIL_KIB:
-            if (value < 0 || value > (1ll << 30)) return fail(FMI_ERR_INVALID, "pair tail must be in [0, 2^30] KiB");
+        case FMI_TUNE_PAIR_SC1_OF_8:
+            if (value < 0 || value > 8) return fail(FMI_ERR_INVALID, "pair sc1 tiles per 8 must be in [0, 8]");
             break;
         default: return fail(FMI_ERR_INVALID, "unknown tuning key");
     }
@@ -1130,7 +1126,7 @@ int fmi_tune_set(int key, long long value) {
 }
 
 int fmi_tune_get(int key, long long* value) {
-    if (!value || key < 0 || key > FMI_TUNE_PAIR_TAIL_KIB) return fail(FMI_ERR_INVALID, "bad tuning query");
+    if (!value || key < 0 || key > FMI_TUNE_PAIR_SC1_OF_8) return fail(FMI_ERR_INVALID, "bad tuning query");
     *value = g_tune[key].load();
     return FMI_OK;
 }

@@ -189,7 +189,7 @@ __device__ __forceinline__ Lanes<T, W> combine(const Lanes<T, W>& a, const Lanes
 // policy: loads nt; the tree's one output stream sc1 (written lines leave the XCD L2 at once), the scan's
 // P output streams nt sc1. tools/microbench_cachepol.hip measured, on the same buffers, tree P = 8 3.3 %
 // and scan P = 8 4.6 % faster than global_load / global_store nt (bit-identical results). The pairwise
-// kernel keeps global nt accesses and stores only its last tiles with sc1 (pair_tile below).
+// kernel keeps global nt accesses and stores some of its tiles with sc1 (pair_tile below).
 inline constexpr int kAuxNT = 2, kAuxSC1 = 16;
 inline constexpr int kTreeStoreAux = kAuxSC1, kScanStoreAux = kAuxNT | kAuxSC1, kFusedLoadAux = kAuxNT;
 using b128 = unsigned int __attribute__((ext_vector_type(4)));
@@ -217,7 +217,7 @@ __device__ __forceinline__ void store_tile(void* bucket, size_t tile_byte, unsig
 // thread keeps 2U independent 16-B loads in flight before its first add.
 // ---------------------------------------------------------------------------------------------------
 // NT: cache policy bitmask — bit 0 nontemporal loads, bit 1 nontemporal stores. `sc1` (uniform per tile):
-// store this tile with sc1 instead (pair_tile's tail tiles, FMI_TUNE_PAIR_TAIL_KIB).
+// store this tile with sc1 instead (pair_tile's sc1 tiles, FMI_TUNE_PAIR_SC1_OF_8).
 template <class Op, class T, int U, int NT>
 __device__ __forceinline__ void pair_tile_body(T* out, const T* a, const T* b, size_t nvec, size_t tile, bool sc1 = false) {
     constexpr int W = kVecLanes<T>;
@@ -272,14 +272,14 @@ __device__ __forceinline__ void pair_tail(T* out, const T* a, const T* b, size_t
     }
 }
 
-// One-shot grid: one tile per workgroup. Pointers must be 16-B aligned. Whole tiles from `sc1_from` on
-// store with sc1 (default: none, the round-1 kernel the exploration tools compare against): the end of the launch then leaves little dirty data in the XCD L2s for the release to
-// write back (C3 i64 max 64 MiB: 31.9 -> 30.6 us, C2 -1 %; tools/microbench_tailsweep.hip).
+// One-shot grid: one tile per workgroup. Pointers must be 16-B aligned. Whole tiles t with t % 8 < sc1_k
+// store with sc1, the rest nontemporal (default 0: none, the round-1 kernel the exploration tools compare
+// against). Consecutive workgroups are dispatched to different XCDs, so sc1_k of the 8 XCDs store sc1
+// (FMI_TUNE_PAIR_SC1_OF_8; tools/ab_pair_sc1.py).
 template <class Op, class T, int U, int NT>
-__global__ void __launch_bounds__(1024) pair_tile(T* out, const T* a, const T* b, size_t n,
-                                                     size_t sc1_from = ~size_t(0)) {
+__global__ void __launch_bounds__(1024) pair_tile(T* out, const T* a, const T* b, size_t n, unsigned sc1_k = 0) {
     const size_t nvec = n / kVecLanes<T>;
-    pair_tile_body<Op, T, U, NT>(out, a, b, nvec, blockIdx.x, blockIdx.x >= sc1_from);
+    pair_tile_body<Op, T, U, NT>(out, a, b, nvec, blockIdx.x, (blockIdx.x & 7u) < sc1_k);
     pair_tail<Op, T>(out, a, b, n);
 }
 

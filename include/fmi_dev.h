@@ -335,11 +335,11 @@ typedef enum {
                                     loads nt with sc1 (tree) / nt sc1 (scan) stores; 0 = global_load /
                                     global_store nt; 1 = auto (default): 2 for trees of >= 4 and scans of
                                     >= 8 peers, 0 otherwise (tools/ab_fused_policy.py). Same bits always */
-    FMI_TUNE_PAIR_TAIL_KIB = 12   /* pairwise kernel (16-B aligned buckets): the last KiB of output of each
-                                    launch are stored with sc1 (the written lines leave the XCD L2 at once)
-                                    instead of nontemporal, so less dirty L2 data is left for the release at
-                                    the end of the launch; 0 = every tile nontemporal. Default 32768 (32 MiB,
-                                    tools/microbench_tailsweep.hip). Same bits always */
+    FMI_TUNE_PAIR_SC1_OF_8 = 12   /* pairwise kernel (16-B aligned buckets, one-shot tiles): tiles t with
+                                    t % 8 < k store with sc1 instead of nontemporal (k = 0..8). Consecutive
+                                    workgroups are dispatched to different XCDs, so k of the 8 XCDs store sc1.
+                                    Default 1 (tools/ab_pair_sc1.py, measured with no MALL re-use). Same bits
+                                    always */
 } fmi_tune_key_t;
 int fmi_tune_set(int key, long long value);
 int fmi_tune_get(int key, long long* value);

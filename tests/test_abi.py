@@ -145,12 +145,13 @@ def test_tuning_knobs_validate():
         assert fmi_amd.tune_get(fmi_amd.Tune.FUSED_POLICY) == v
     with pytest.raises(fmi_amd.FmiError):
         fmi_amd.tune_set(fmi_amd.Tune.FUSED_POLICY, 3)
-    assert fmi_amd.tune_get(fmi_amd.Tune.PAIR_TAIL_KIB) == 32768  # default (tools/microbench_tailsweep.hip)
-    for v in (0, 1, 32768):
-        fmi_amd.tune_set(fmi_amd.Tune.PAIR_TAIL_KIB, v)
-        assert fmi_amd.tune_get(fmi_amd.Tune.PAIR_TAIL_KIB) == v
-    with pytest.raises(fmi_amd.FmiError):
-        fmi_amd.tune_set(fmi_amd.Tune.PAIR_TAIL_KIB, -1)
+    assert fmi_amd.tune_get(fmi_amd.Tune.PAIR_SC1_OF_8) == 1  # default (tools/ab_pair_sc1.py)
+    for v in (0, 8, 1):
+        fmi_amd.tune_set(fmi_amd.Tune.PAIR_SC1_OF_8, v)
+        assert fmi_amd.tune_get(fmi_amd.Tune.PAIR_SC1_OF_8) == v
+    for bad in (-1, 9):
+        with pytest.raises(fmi_amd.FmiError):
+            fmi_amd.tune_set(fmi_amd.Tune.PAIR_SC1_OF_8, bad)
     for key in (fmi_amd.Tune.COMM_A2A, fmi_amd.Tune.COMM_GATHER):  # RCCL exchange realisations
         assert fmi_amd.tune_get(key) == 0
         fmi_amd.tune_set(key, 1)

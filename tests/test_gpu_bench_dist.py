@@ -58,7 +58,7 @@ def test_comm_allreduce_gloo_world2():
 def test_bench_py_proc_transport(world):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", str(world),
-           "--transport", "proc", "--steps", "4", "--warmup", "1", "--sets", "2", "--bucket-mib", "8",
+           "--transport", "proc", "--steps", "4", "--warmup", "1", "--dist-sets", "2", "--bucket-mib", "8",
            "--c4-mib", "16", "--c5-mib", "8", "--diag-deadline", "150"]
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=240,
                        env=dict(os.environ, FMI_PROC_TIMEOUT_S="90", OMP_NUM_THREADS="1"))

@@ -125,26 +125,25 @@ def test_reduce_pair_every_launch_variant(device, variant, unroll, block):
 
 
 @pytest.mark.parametrize("dtype", [np.float32, np.int64, np.int8], ids=lambda d: np.dtype(d).name)
-@pytest.mark.parametrize("tail_kib", [0, 1, 16, 48, 100, 32768])
-def test_reduce_pair_sc1_tail_keeps_bits(device, dtype, tail_kib):
-    """FMI_TUNE_PAIR_TAIL_KIB moves the boundary between the nontemporal tiles and the sc1-stored tail tiles
-    of one launch (none, one tile, a few, most, all); the ragged last tile and the < 16-B tail stay where they
-    are. Every position gives the oracle's bits, with the launch variants that honour the tail (one-shot
-    tiles at unroll 1 / 4 and 256 / 1024 threads)."""
-    n = 3 * 4096 * 16 // np.dtype(dtype).itemsize + 4099  # > 3 tiles of 64 KiB at unroll 4, ragged end
+@pytest.mark.parametrize("sc1_of_8", [0, 1, 3, 8])
+def test_reduce_pair_sc1_tiles_keep_bits(device, dtype, sc1_of_8):
+    """FMI_TUNE_PAIR_SC1_OF_8 picks which tiles of a launch store with sc1 (t % 8 < k: none, 1, 3 or all 8 of
+    every 8); the ragged last tile and the < 16-B tail included. Every choice gives the oracle's bits, with the
+    launch shapes that honour it (one-shot tiles at unroll 1 / 4, 256 / 1024 threads)."""
+    n = 12 * 4096 * 16 // np.dtype(dtype).itemsize + 4099  # 49 tiles of 16 KiB at unroll 4, ragged end
     a, b = inputs(dtype, n, 0), inputs(dtype, n, 1)
     with np.errstate(all="ignore"):
         want = orc.pairwise("max" if dtype == np.int64 else "sum", a, b)
-    keys = (Tune.PAIR_TAIL_KIB, Tune.PAIR_UNROLL, Tune.BLOCK)
+    keys = (Tune.PAIR_SC1_OF_8, Tune.PAIR_UNROLL, Tune.BLOCK)
     old = {k: fmi_amd.tune_get(k) for k in keys}
     try:
-        fmi_amd.tune_set(Tune.PAIR_TAIL_KIB, tail_kib)
+        fmi_amd.tune_set(Tune.PAIR_SC1_OF_8, sc1_of_8)
         for unroll, block in [(4, 256), (1, 256), (4, 1024)]:
             fmi_amd.tune_set(Tune.PAIR_UNROLL, unroll)
             fmi_amd.tune_set(Tune.BLOCK, block)
             da, db = dev(a), dev(b)
             fmi_amd.reduce_pair(Op.MAX if dtype == np.int64 else Op.SUM, da, db)
-            assert_bit_equal(da.numpy(), want, f"tail {tail_kib} KiB, unroll {unroll}, block {block}")
+            assert_bit_equal(da.numpy(), want, f"sc1 {sc1_of_8} of 8, unroll {unroll}, block {block}")
     finally:
         for k, v in old.items():
             fmi_amd.tune_set(k, v)

@@ -24,6 +24,9 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--mib", type=int, default=64)
     ap.add_argument("--launches", type=int, default=24)
+    ap.add_argument("--footprint-gib", type=float, default=1.5,
+                    help="rotating buckets per shape; the sc1-stored outputs stay in the 256 MB MALL, so the sets "
+                         "must hold well over 256 MB of outputs for no launch to re-read one from there")
     args = ap.parse_args()
     import fmi_amd
     from fmi_amd import Alg, Bucket, Op
@@ -42,7 +45,7 @@ def main():
     for name, dtype, op, alg, P, kind, mib in shapes:
         n = mib * MIB // np.dtype(dtype).itemsize
         per_set = (P + (P if kind == "scan" else 1)) * mib
-        nsets = max(2, -(-1536 // per_set))  # >= 1.5 GiB of buckets: no re-read from the 256 MB MALL
+        nsets = max(2, -(-int(args.footprint_gib * 1024) // per_set))
         sets = [[Bucket(n, dtype).fill_synthetic(7 + s, p) for p in range(P)] for s in range(nsets)]
         outs = [[Bucket(n, dtype) for _ in range(P if kind == "scan" else 1)] for _ in range(nsets)]
 
@@ -51,6 +54,13 @@ def main():
                 scan_peers(op, alg, outs[s], sets[s])
             else:
                 reduce_tree(op, alg, outs[s][0], sets[s])
+
+        pos = 0  # one running position over the sets: every set is re-used exactly nsets launches later
+
+        def next_launch():
+            nonlocal pos
+            launch(pos % nsets)
+            pos += 1
 
         bits = {}
         for pol in (0, 2):
@@ -63,12 +73,12 @@ def main():
         for r in range(args.rounds):
             for pol in ((0, 2) if r % 2 == 0 else (2, 0)):
                 tune_set(Tune.FUSED_POLICY, pol)
-                launch(0)
-                launch(1)
+                next_launch()
+                next_launch()
                 e0, e1 = Event(), Event()
                 e0.record()
                 for k in range(args.launches):
-                    launch(k % nsets)
+                    next_launch()
                 e1.record()
                 e1.sync()
                 times[pol].append(e0.elapsed_ms(e1) * 1e3 / args.launches)
