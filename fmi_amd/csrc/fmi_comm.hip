@@ -1486,33 +1486,7 @@ int fmi_comm_allreduce_host(fmi_comm_t comm, int op, int dtype, int alg, int pat
         chunk = std::max<size_t>(static_cast<size_t>(bytes) / esz, kShardAlign);
     }
     chunk = std::min(chunk, n);
-    // The pieces, in order: equal chunks, except that with FMI_TUNE_HOST_RAMP the first and the last full
-    // chunk are cut into 1/8, 1/8, 1/4, 1/2 (and the reverse), so the pipeline fills and drains on small
-    // pieces instead of leaving one whole chunk's H2D, and one D2H, alone on the link.
-    std::vector<std::pair<size_t, size_t>> pieces;  // (first element, elements)
-    {
-        long long ramp = 0;
-        (void)fmi_tune_get(FMI_TUNE_HOST_RAMP, &ramp);
-        const size_t full = n / chunk;
-        const size_t e8 = chunk / 8 / kShardAlign * kShardAlign;  // 1/8 chunk, shard-aligned
-        const bool cut = ramp != 0 && full >= 3 && e8 > 0;
-        size_t at = 0;
-        auto add = [&](size_t len) {
-            pieces.emplace_back(at, len);
-            at += len;
-        };
-        for (size_t k = 0; k < full; ++k) {
-            if (cut && k == 0) {
-                for (size_t len : {e8, e8, 2 * e8, chunk - 4 * e8}) add(len);
-            } else if (cut && k == full - 1) {
-                for (size_t len : {chunk - 4 * e8, 2 * e8, e8, e8}) add(len);
-            } else {
-                add(chunk);
-            }
-        }
-        if (at < n) add(n - at);
-    }
-    const size_t nchunks = pieces.size();
+    const size_t nchunks = (n + chunk - 1) / chunk;
     char* in[2] = {};
     char* out[2] = {};
     for (int j = 0; j < 2; ++j) {
@@ -1521,11 +1495,11 @@ int fmi_comm_allreduce_host(fmi_comm_t comm, int op, int dtype, int alg, int pat
     }
     const char* src = static_cast<const char*>(send);
     char* dst = static_cast<char*>(recv);
-    auto span = [&](size_t k) { return pieces[k].second; };
+    auto span = [&](size_t k) { return std::min(chunk, n - k * chunk); };
     auto load = [&](size_t k) -> int {
         const int j = static_cast<int>(k & 1);
         if (k >= 2) FMI_COMM_HIP(hipStreamWaitEvent(p.h2d, p.reduced[j], 0));
-        FMI_COMM_HIP(hipMemcpyAsync(in[j], src + pieces[k].first * esz, span(k) * esz, hipMemcpyDefault, p.h2d));
+        FMI_COMM_HIP(hipMemcpyAsync(in[j], src + k * chunk * esz, span(k) * esz, hipMemcpyDefault, p.h2d));
         FMI_COMM_HIP(hipEventRecord(p.loaded[j], p.h2d));
         return FMI_OK;
     };
@@ -1538,7 +1512,7 @@ int fmi_comm_allreduce_host(fmi_comm_t comm, int op, int dtype, int alg, int pat
         FMI_COMM_RC(allreduce_device(c, op, dtype, alg, path, in[j], out[j], span(k), p.cs));
         FMI_COMM_HIP(hipEventRecord(p.reduced[j], p.cs));
         FMI_COMM_HIP(hipStreamWaitEvent(p.d2h, p.reduced[j], 0));
-        FMI_COMM_HIP(hipMemcpyAsync(dst + pieces[k].first * esz, out[j], span(k) * esz, hipMemcpyDefault, p.d2h));
+        FMI_COMM_HIP(hipMemcpyAsync(dst + k * chunk * esz, out[j], span(k) * esz, hipMemcpyDefault, p.d2h));
         FMI_COMM_HIP(hipEventRecord(p.drained[j], p.d2h));
     }
     FMI_COMM_HIP(hipStreamSynchronize(p.d2h));

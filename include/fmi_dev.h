@@ -258,8 +258,7 @@ int fmi_comm_allreduce(fmi_comm_t comm, int op, int dtype, int alg, int path, co
 /* Host-ingress allreduce (BASELINE config C5): `send` / `recv` are HOST buckets, i.e. the channel recv
  * buffers FMI's transports deliver into (reference src/comm/Direct.cpp:36-45, PeerToPeer.cpp:110-129).
  * The bucket streams through the GPU in chunks of `chunk` elements (0 = FMI_TUNE_HOST_CHUNK bytes):
- * H2D of chunk k+1, the sharded allreduce of chunk k and D2H of chunk k-1 overlap on three streams
- * (FMI_TUNE_HOST_RAMP: the first and last chunk in smaller pieces).
+ * H2D of chunk k+1, the sharded allreduce of chunk k and D2H of chunk k-1 overlap on three streams.
  * Every rank must pass the same n and chunk. Page-locked buckets (fmi_host_pin_alloc) move at PCIe DMA
  * rate; pageable ones work but copy synchronously. Element-wise results are identical to
  * fmi_comm_allreduce over the whole bucket. Blocking: returns when `recv` holds the result. */
@@ -336,14 +335,11 @@ typedef enum {
                                     loads nt with sc1 (tree) / nt sc1 (scan) stores; 0 = global_load /
                                     global_store nt; 1 = auto (default): 2 for trees of >= 4 and scans of
                                     >= 8 peers, 0 otherwise (tools/ab_fused_policy.py). Same bits always */
-    FMI_TUNE_PAIR_SC1_OF_8 = 12,  /* pairwise kernel (16-B aligned buckets, one-shot tiles): tiles t with
+    FMI_TUNE_PAIR_SC1_OF_8 = 12   /* pairwise kernel (16-B aligned buckets, one-shot tiles): tiles t with
                                     t % 8 < k store with sc1 instead of nontemporal (k = 0..8). Consecutive
                                     workgroups are dispatched to different XCDs, so k of the 8 XCDs store sc1.
                                     Default 1 (tools/ab_pair_sc1.py, measured with no MALL re-use). Same bits
                                     always */
-    FMI_TUNE_HOST_RAMP = 13       /* fmi_comm_allreduce_host: 1 = the first and the last full chunk are cut
-                                    into 1/8, 1/8, 1/4, 1/2 of a chunk (and the reverse), so the pipeline
-                                    fills and drains on small pieces (default); 0 = equal chunks. Same bits */
 } fmi_tune_key_t;
 int fmi_tune_set(int key, long long value);
 int fmi_tune_get(int key, long long* value);

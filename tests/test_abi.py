@@ -152,9 +152,6 @@ def test_tuning_knobs_validate():
     for bad in (-1, 9):
         with pytest.raises(fmi_amd.FmiError):
             fmi_amd.tune_set(fmi_amd.Tune.PAIR_SC1_OF_8, bad)
-    assert fmi_amd.tune_get(fmi_amd.Tune.HOST_RAMP) == 1  # default: the host pipeline fills on small pieces
-    with pytest.raises(fmi_amd.FmiError):
-        fmi_amd.tune_set(fmi_amd.Tune.HOST_RAMP, 2)
     for key in (fmi_amd.Tune.COMM_A2A, fmi_amd.Tune.COMM_GATHER):  # RCCL exchange realisations
         assert fmi_amd.tune_get(key) == 0
         fmi_amd.tune_set(key, 1)

@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 
 import fmi_amd
-from fmi_amd import Bucket, Op, PinnedArray, Tune
+from fmi_amd import Bucket, Op, PinnedArray
 from fmi_amd.comm import Comm, Path, Transport, unique_id
 from oracle import fmi_oracle as orc
 from tests.test_gpu_parity import OPNAME, assert_bit_equal, inputs
@@ -290,26 +290,19 @@ def _host_allreduce(c, r, x, op, ordered, pinned, chunk):
 
 @pytest.mark.parametrize("N", [1, 2, 3, 8])
 @pytest.mark.parametrize("pinned", [True, False])
-@pytest.mark.parametrize("ramp", [1, 0])
-def test_comm_allreduce_host_pipeline(device, N, pinned, ramp):
+def test_comm_allreduce_host_pipeline(device, N, pinned):
     """Host-ingress allreduce (config C5 shape): host buckets stream through the GPU in chunks (ragged last
-    chunk, padded shards, slot reuse over > 2 chunks; FMI_TUNE_HOST_RAMP = 1 cuts the first and last full
-    chunk into 512 / 512 / 1024 / 2051-element pieces); every rank's host result equals the oracle's."""
+    chunk, padded shards, slot reuse over > 2 chunks); every rank's host result equals the oracle's."""
     n, chunk = 3 * 4099 + 17, 4099
-    old = fmi_amd.tune_get(Tune.HOST_RAMP)
-    fmi_amd.tune_set(Tune.HOST_RAMP, ramp)
-    try:
-        for dtype, op, ordered in ((np.float32, Op.SUM, False), (np.int64, Op.MAX, False),
-                                   (np.float64, Op.PROD, False), (np.float32, Op.SUM, True)):
-            xs = [inputs(dtype, n, r, seed=13) for r in range(N)]
-            res = run_ranks(N, lambda c, r: _host_allreduce(c, r, xs[r], op, ordered, pinned, chunk))
-            with np.errstate(all="ignore"):
-                want, _ = orc.allreduce(xs, orc.OPS[OPNAME[op]], commutative=not ordered, associative=not ordered)
-            for r in range(N):
-                assert_bit_equal(res[r][0], want[r], f"N={N} {op.name} ordered={ordered} rank {r}")
-                assert_bit_equal(res[r][1], xs[r], "send bucket untouched")
-    finally:
-        fmi_amd.tune_set(Tune.HOST_RAMP, old)
+    for dtype, op, ordered in ((np.float32, Op.SUM, False), (np.int64, Op.MAX, False), (np.float64, Op.PROD, False),
+                               (np.float32, Op.SUM, True)):
+        xs = [inputs(dtype, n, r, seed=13) for r in range(N)]
+        res = run_ranks(N, lambda c, r: _host_allreduce(c, r, xs[r], op, ordered, pinned, chunk))
+        with np.errstate(all="ignore"):
+            want, _ = orc.allreduce(xs, orc.OPS[OPNAME[op]], commutative=not ordered, associative=not ordered)
+        for r in range(N):
+            assert_bit_equal(res[r][0], want[r], f"N={N} {op.name} ordered={ordered} rank {r}")
+            assert_bit_equal(res[r][1], xs[r], "send bucket untouched")
 
 
 def test_comm_allreduce_host_default_chunk_matches_device(device):

@@ -4,6 +4,9 @@ interleaved, for a few chunk sizes; median wall time, result checked bit-exact (
 copy). After a 1 s pause, so no freed VRAM is being cleared on the copy engines.
 
     python tools/ab_host_ramp.py [--rounds 7] [--mib 1024] [--chunks 32,64,128]
+
+Needs the library of commit 3e69cb5 (FMI_TUNE_HOST_RAMP); the ramp was rejected and removed after this
+measurement (profiles/r02_c5_ramp_rejected.jsonl).
 """
 import argparse
 import json
