@@ -4,7 +4,8 @@
 
 N = 1 (config C2). One *step* = one pairwise combine a = a + b of two 256 MiB float32 peer buckets
 resident in HBM — the reference's `f.f(a, b)` (include/Communicator.h:180-189) on the device, rotating over
-4 buffer sets (2 GiB, beyond the 256 MiB Infinity Cache). value = 256 MiB / (wall time per step).
+16 buffer sets (8 GiB; the rotation runs on from the warm-up, so no step re-reads a bucket the 256 MB
+Infinity Cache still holds, see --sets). value = 256 MiB / (wall time per step).
 
 N > 1 (config C4's shape at the metric's bucket size). One *step* = the N-peer float32 sum-allreduce of
 256 MiB buckets, ONE FMI peer per GPU (one process per GPU), through the product C-ABI communicator
