@@ -38,6 +38,69 @@ def timed(fn, iters, rotate):
     return statistics.median(ms), min(ms)
 
 
+def timed_fresh(fn, iters, rotate, reps=5):
+    """No-re-use protocol ("store policy across the XCDs"): the buffer-set index runs on from the
+    warm-up, so every set comes back exactly `rotate` launches later, and callers size `rotate` so that well
+    over 256 MB of output is written between two uses of a set (sc1-stored lines stay in the MALL). Two
+    events around `iters` back-to-back launches, `reps` times; median and min of the per-launch means."""
+    pos = 0
+    for _ in range(3):
+        fn(pos % rotate)
+        pos += 1
+    fmi_amd.sync()
+    means = []
+    for _ in range(reps):
+        e0, e1 = Event(), Event()
+        e0.record()
+        for _ in range(iters):
+            fn(pos % rotate)
+            pos += 1
+        e1.record()
+        e1.sync()
+        means.append(e0.elapsed_ms(e1) / iters)
+        e0.destroy()
+        e1.destroy()
+    return statistics.median(means), min(means)
+
+
+def out_sets(out_bytes_per_launch, budget=1536 * MIB):
+    """Output buffer sets for timed_fresh: >= `budget` bytes of output between two uses of a set."""
+    return max(2, -(-budget // out_bytes_per_launch) + 1)
+
+
+def fused_fresh_rows(it):
+    """The fused P-way rows of DESIGN.md §5 under the no-re-use protocol: C3's scan and the P = 8 trees over
+    64 MiB buckets, trees over 1 GiB of input for P = 2 / 4 / 16 and the P > 16 programs, outputs rotating
+    over out_sets(...) buffers (inputs are only read, with nontemporal loads)."""
+    rows = [("C3 scan scan f32 P=8 x 64MiB", "scan", Alg.SCAN, 8, 64), ("C3 scan scan_ltr f32 P=8 x 64MiB", "scan", Alg.SCAN_LTR, 8, 64),
+            ("tree allreduce f32 P=8 x 64MiB", "tree", Alg.ALLREDUCE, 8, 64), ("tree reduce f32 P=8 x 64MiB", "tree", Alg.REDUCE, 8, 64),
+            ("tree reduce_ltr f32 P=8 x 64MiB", "tree", Alg.REDUCE_LTR, 8, 64)]
+    for P in (2, 4, 16, 24, 32, 48, 64):
+        rows.append((f"tree allreduce f32 P={P} x {1024 // P}MiB", "tree", Alg.ALLREDUCE, P, 1024 // P))
+    rows += [("tree reduce f32 P=64 x 16MiB", "tree", Alg.REDUCE, 64, 16), ("tree reduce_ltr f32 P=64 x 16MiB", "tree", Alg.REDUCE_LTR, 64, 16)]
+    for P in (24, 32, 64, 128):
+        rows.append((f"scan scan f32 P={P} x {1024 // P}MiB", "scan", Alg.SCAN, P, 1024 // P))
+    rows.append(("scan scan_ltr f32 P=64 x 16MiB", "scan", Alg.SCAN_LTR, 64, 16))
+    for name, kind, alg, P, mib in rows:
+        n = mib * MIB // 4
+        n_in = 2 if P * mib <= 512 else 1  # input sets: only read (nt), never in the MALL
+        ins = [[Bucket(n, np.float32).fill_synthetic(7 + s, p) for p in range(P)] for s in range(n_in)]
+        per_out = (P if kind == "scan" else 1) * mib * MIB
+        k_out = out_sets(per_out)
+        outs = [[Bucket(n, np.float32) for _ in range(P if kind == "scan" else 1)] for _ in range(k_out)]
+
+        def launch(k):
+            if kind == "scan":
+                fmi_amd.scan_peers(Op.SUM, alg, outs[k], ins[k % n_in])
+            else:
+                fmi_amd.reduce_tree(Op.SUM, alg, outs[k][0], ins[k % n_in], rank=P - 1 if alg == Alg.ALLREDUCE else 0)
+
+        med, mn = timed_fresh(launch, max(6, it // 3), k_out)
+        algo = (2 * P if kind == "scan" else P + 1) * n * 4
+        row(name + " (no re-use)", algo, med, mn, output_sets=k_out, input_sets=n_in)
+        del ins, outs
+
+
 def row(name, algo_bytes, med_ms, min_ms, **kw):
     gbs = algo_bytes / (med_ms * 1e-3) / 1e9
     r = dict(config=name, algo_bytes=algo_bytes, median_us=round(med_ms * 1e3, 2), min_us=round(min_ms * 1e3, 2),
@@ -128,6 +191,8 @@ def main():
     ap.add_argument("--c5-only", action="store_true", help="only the host-ingress allreduce rows")
     ap.add_argument("--wide-only", action="store_true", help="only the P > 16 tree rows")
     ap.add_argument("--op-sweep", action="store_true", help="only the op x dtype sweep of the P = 8 programs")
+    ap.add_argument("--fused-fresh", action="store_true",
+                    help="only the fused P-way rows under the no-re-use protocol (timed_fresh)")
     ap.add_argument("--torch-runtime", action="store_true",
                     help="import torch first, so the library binds to torch's bundled HIP runtime")
     args = ap.parse_args()
@@ -143,6 +208,9 @@ def main():
         return
     if args.op_sweep:
         op_sweep_rows(it)
+        return
+    if args.fused_fresh:
+        fused_fresh_rows(it)
         return
 
     # C2 and its siblings: pairwise combine, every dtype/op, 256 MiB buckets, 4 rotating sets
