@@ -83,6 +83,9 @@ def parse():
                     help="seconds everything after `value` (c4, c5, diagnostics) may take before the line is "
                          "printed without the rest of it")
     ap.add_argument("--diag-direct", action="store_true", help="N>1 diagnostics: also check and time path DIRECT")
+    ap.add_argument("--measure-deadline", type=float, default=900.0,
+                    help="N>1: seconds the measurement up to `value` (setup, warm-up, timed steps, self-check) may "
+                         "take; past it the rank names the phase it is stuck in on stderr and exits with status 3")
     ap.add_argument("--force-dist", action="store_true",
                     help="run the N>1 code path (fmi_comm over RCCL) even at world size 1 — plumbing check")
     ap.add_argument("--cpu-reps", type=int, default=30, help="adapter combines timed (≈10 s of CPU work)")
@@ -452,16 +455,41 @@ def bind_near_gpu(dev: int) -> dict:
         return {"bound": False, "error": f"{type(e).__name__}: {e}"}
 
 
+class _PhaseWatch:
+    """N > 1: which phase of the measurement this rank is in; if the measurement outlives its deadline (a rank
+    waiting forever in an exchange), say where on stderr and exit non-zero instead of hanging silently."""
+
+    def __init__(self, seconds, rank):
+        self.rank, self.phase, self.t0 = rank, "start", time.time()
+        self.timer = threading.Timer(seconds, self._expire)
+        self.timer.daemon = True
+        self.timer.start()
+
+    def enter(self, phase):
+        self.phase = phase
+
+    def _expire(self):
+        print(f"bench: rank {self.rank} still in phase '{self.phase}' after {time.time() - self.t0:.0f} s "
+              f"(--measure-deadline); exiting", file=sys.stderr, flush=True)
+        os._exit(3)
+
+    def done(self):
+        self.timer.cancel()
+
+
 def run_dist(args, world, rank, local_rank):
     # torch first: libfmi_dev.so then binds to the HIP runtime torch already loaded (one runtime per process,
     # shared streams/pointers with RCCL) — see DESIGN.md §Runtime.
     import torch
     import torch.distributed as dist
 
+    watch = _PhaseWatch(args.measure_deadline, rank)
+
     proc = args.transport == "proc"
     dev = local_rank % max(1, torch.cuda.device_count()) if proc else local_rank
     numa = bind_near_gpu(dev) if not args.no_numa_bind else {"bound": False, "disabled": True}
     torch.cuda.set_device(dev)
+    watch.enter("process group init")
     if proc:
         dist.init_process_group("gloo")
     else:
@@ -471,15 +499,20 @@ def run_dist(args, world, rank, local_rank):
     from fmi_amd.collectives import CommAllreduce
 
     fmi_amd.init(dev)
+    watch.enter("fmi_comm init (communicator id broadcast, RCCL init)")
     ar = CommAllreduce(dist.group.WORLD, path=args.path, transport=args.transport)
     n = args.bucket_mib * MIB // 4
     S = n * 4
+    watch.enter("warm-up and timed allreduces")
     step_ms, _, extra = ar.bench(n, steps=args.steps, warmup=args.warmup, sets=args.dist_sets, peers_per_gpu=1)
     out, seed = extra.pop("result")
     value = world * (S / GIB) / (step_ms * 1e-3)
+    watch.enter("self-check")
     check = ar.self_check(out, n, seed, tolerance=args.path == "rccl")
     out.free()
+    watch.enter("isolated shard-kernel timing")
     kern = ar.shard_kernel(n, launches=max(10, min(args.steps, 50)))
+    watch.done()
     live = extra.pop("shard_kernel_launches") > 0
     shard_ms = extra.pop("shard_kernel_avg_ms")
     roof = _roofline("tree_kernel", kern["algorithmic_bytes_per_launch"],

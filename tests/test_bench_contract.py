@@ -79,3 +79,15 @@ def test_c3_rows_find_their_pmc_profiles():
                       ("scan_kernel<fmi::dev::OpSum, float, 3, 8>", 16 * 64 * (1 << 20))):
         t, _ = bench.pmc_traffic(key)
         assert t is not None and abs(t / algo - 1) < 0.01, (key, t)
+
+
+def test_measure_deadline_names_the_phase_and_exits_nonzero():
+    """N > 1: a rank stuck before `value` reports its phase on stderr and exits with status 3 (run in a child
+    process: the watch ends the process)."""
+    code = ("import bench, time\n"
+            "w = bench._PhaseWatch(0.2, 5)\n"
+            "w.enter('warm-up and timed allreduces')\n"
+            "time.sleep(5)\n")
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True, timeout=60)
+    assert r.returncode == 3
+    assert "rank 5 still in phase 'warm-up and timed allreduces'" in r.stderr
