@@ -352,8 +352,103 @@ int tree_blocked(int op, int dtype, int alg, void* out, const void* const* ins, 
     }
 }
 
+// ----------------------------------------------------------------------------------------------------
+// Beyond one one-pass kernel (its pointer table holds 128 peers): superblocks of 128 peers. The programs
+// split at 128 exactly as they split at 16 (tree_blocked above), one level up:
+//   reduce_ltr / scan_ltr: segments of 127 peers continued from the previous segment's running value (the
+//     chain kernel with a carry-in): P + ceil((P - 128) / 127) bucket reads, instead of the blocked
+//     launches' P + 2 ceil((P - 16) / 15).
+//   reduce_no_order: binomial rounds 0..6 stay inside each superblock (the one-pass reduce over its <= 128
+//     peers), rounds 7+ are the reduce program over the ceil(P / 128) superblock values.
+// Every input is read once; the superblock values cost 2 ceil(P / 128) bucket passes. Measured over 1 GiB
+// of input (tools/ab_superblocks.py): reduce P = 256 / 300 15 / 11 % faster than the block launches,
+// reduce_ltr P = 256 25 %, scan_ltr P = 256 2 %. allreduce_no_order, P = 2^k, would split the same way
+// (rounds 0..6 inside superblocks, each the one-pass 128-peer allreduce for rank r % 128; rounds 7+ over
+// the superblock values for rank r / 128) but was 16-25 % SLOWER than the 16-peer block launches at
+// P = 256 / 512 (128 streams per one-pass kernel against 16 per launch), so allreduce keeps the launches.
+// ----------------------------------------------------------------------------------------------------
+constexpr int kSuperPeers = kMaxOnePassScanBlocks * sched::kScanBlock;  // 128
+
+// scan (outs[0..P)) or reduce (out) left to right over P > 128 peers. For reduce, `out` carries the running
+// value between segments, so it must not be one of the inputs a later segment reads (checked by the caller).
+int chain_superblocks(int op, int dtype, bool scan, void* const* outs, void* out, const void* const* ins, int P,
+                      size_t n, hipStream_t s) {
+    for (int k = 0; k < P;) {
+        BlockedScanPtrs ptrs{};
+        const bool carry = k > 0;
+        const int first = carry ? 1 : 0;
+        const int m = std::min(kSuperPeers - first, P - k);
+        if (carry) ptrs.in[0] = scan ? outs[k - 1] : out;
+        for (int j = 0; j < m; ++j) {
+            ptrs.in[first + j] = ins[k + j];
+            if (scan) ptrs.out[first + j] = outs[k + j];
+        }
+        if (!scan) ptrs.out[0] = out;
+        FMI_RC_TRY(launch_chain_one_pass(op, dtype, scan, m + first, ptrs, n, s, carry));
+        k += m;
+    }
+    return FMI_OK;
+}
+
+// reduce_no_order over up to 128 values (transformed ids, root 0): fused up to 16 peers, one pass beyond.
+int reduce_level(int op, int dtype, void* out, const void* const* vals, int P, size_t n, hipStream_t s) {
+    if (P == 1) {
+        if (out != vals[0]) FMI_HIP_TRY(hipMemcpyAsync(out, vals[0], n * dtype_size(dtype), hipMemcpyDeviceToDevice, s));
+        return FMI_OK;
+    }
+    if (P <= sched::kMaxFusedPeers) {
+        PeerPtrs ptrs{};
+        for (int p = 0; p < P; ++p) ptrs.in[p] = vals[p];
+        ptrs.out[0] = out;
+        return launch_fused_reduce(op, dtype, P, ptrs, n, s);
+    }
+    BlockedScanPtrs ptrs{};
+    for (int p = 0; p < P; ++p) ptrs.in[p] = vals[p];
+    ptrs.out[0] = out;
+    return launch_tree_blocks_one_pass(op, dtype, FMI_ALG_REDUCE, P, ptrs, n, 0, s);
+}
+
+bool tree_superblocks_cover(int op, int dtype, int alg, int P) {
+    if (alg != FMI_ALG_REDUCE || P <= kSuperPeers || P > kSuperPeers * kSuperPeers) return false;
+    const int S = (P + kSuperPeers - 1) / kSuperPeers;
+    const int last = P - (S - 1) * kSuperPeers;
+    return tree_blocks_one_pass_covers(op, dtype, alg, kSuperPeers) &&
+           (last <= sched::kMaxFusedPeers || tree_blocks_one_pass_covers(op, dtype, alg, last)) &&
+           (S <= sched::kMaxFusedPeers || tree_blocks_one_pass_covers(op, dtype, alg, S));
+}
+
+// reduce_no_order over P > 128 peers (transformed ids, root 0) as superblocks of 128.
+int reduce_superblocks(int op, int dtype, void* out, const void* const* ins, int P, size_t n, hipStream_t s) {
+    const int S = (P + kSuperPeers - 1) / kSuperPeers;
+    std::lock_guard<std::mutex> lk(g_mu);
+    const size_t stride = arena_stride(n, dtype_size(dtype));
+    FMI_RC_TRY(arena_acquire(stride * static_cast<size_t>(S), s));
+    char* base = static_cast<char*>(g_state.arena);
+    std::vector<const void*> vals(S);
+    int rc = FMI_OK;
+    for (int b = 0; b < S && rc == FMI_OK; ++b) {
+        const int lo = b * kSuperPeers;
+        const int m = std::min(kSuperPeers, P - lo);
+        if (m == 1) {  // a lone last peer is its own superblock value
+            vals[b] = ins[lo];
+            continue;
+        }
+        void* v = base + stride * static_cast<size_t>(b);
+        rc = reduce_level(op, dtype, v, ins + lo, m, n, s);
+        vals[b] = v;
+    }
+    if (rc == FMI_OK) rc = reduce_level(op, dtype, out, vals.data(), S, n, s);
+    FMI_HIP_TRY(hipEventRecord(g_state.arena_free, s));
+    return rc;
+}
+
 int run_tree_blocked(int op, int dtype, int alg, void* out, const void* const* ins, int P, int rank, size_t n,
                      hipStream_t s) {
+    if (g_tune[FMI_TUNE_BLOCKS_ONE_PASS].load() != 0 && P > kSuperPeers) {
+        if (alg == FMI_ALG_REDUCE_LTR && std::find(ins + kSuperPeers, ins + P, static_cast<const void*>(out)) == ins + P)
+            return chain_superblocks(op, dtype, false, nullptr, out, ins, P, n, s);
+        if (tree_superblocks_cover(op, dtype, alg, P)) return reduce_superblocks(op, dtype, out, ins, P, n, s);
+    }
     if (g_tune[FMI_TUNE_BLOCKS_ONE_PASS].load() != 0 && alg == FMI_ALG_REDUCE_LTR && P <= kMaxOnePassScanBlocks * 16) {
         BlockedScanPtrs ptrs{};
         for (int p = 0; p < P; ++p) ptrs.in[p] = ins[p];
@@ -461,6 +556,8 @@ int run_scan_blocked(int op, int dtype, int alg, void* const* outs, const void* 
                      hipStream_t s) {
     constexpr int BL = sched::kScanBlock;
     const int B = P / BL, r = P % BL;
+    if (alg == FMI_ALG_SCAN_LTR && P > kSuperPeers && g_tune[FMI_TUNE_BLOCKS_ONE_PASS].load() != 0)
+        return chain_superblocks(op, dtype, true, outs, nullptr, ins, P, n, s);
     if (alg == FMI_ALG_SCAN_LTR && P <= kMaxOnePassScanBlocks * BL && g_tune[FMI_TUNE_BLOCKS_ONE_PASS].load() != 0) {
         BlockedScanPtrs ptrs{};
         for (int p = 0; p < P; ++p) {

@@ -129,7 +129,9 @@ int launch_prefold_blocks_one_pass(int op, int dtype, int P, const BlockedScanPt
                                    hipStream_t s);
 // scan_ltr (scan = true: ptrs.out[0..P)) and reduce_ltr (ptrs.out[0]) over 2..128 peers in one pass, the running
 // value carried in registers (fmi_fused_chain.hip)
-int launch_chain_one_pass(int op, int dtype, bool scan, int P, const BlockedScanPtrs& ptrs, size_t n, hipStream_t s);
+// carry_in: ptrs.in[0] is an earlier segment's running value (scan: ptrs.out[0] is not written).
+int launch_chain_one_pass(int op, int dtype, bool scan, int P, const BlockedScanPtrs& ptrs, size_t n, hipStream_t s,
+                          bool carry_in = false);
 int launch_tree_blocks_one_pass(int op, int dtype, int alg, int P, const BlockedScanPtrs& ptrs, size_t n, int rank,
                                 hipStream_t s);
 

@@ -316,10 +316,12 @@ typedef enum {
                                        resident per CU (an LDS reservation enforces it); 0 = no cap. Default 64
                                        (fewer concurrent HBM streams at large P) */
     FMI_TUNE_BLOCKS_ONE_PASS = 7, /* P-way programs beyond 31 peers in one pass over every input (default 1):
-                                    scan_no_order over 32..143 peers, reduce_no_order over 17..128 peers,
+                                    scan_no_order over 32..143 peers, reduce_no_order over 17..128 peers
+                                    (beyond: superblocks of 128, one pass each, up to 16384 peers),
                                     allreduce_no_order over 32 / 48 / 64 / 80 / 96 / 112 / 128
                                     peers, scan_ltr and
-                                    reduce_ltr over 32..128 peers;
+                                    reduce_ltr over 32..128 peers (beyond: segments of 127 continued
+                                    from the running value, any P);
                                     0 = the blocked launches (block values through temps; the scan reads
                                     the inputs of blocks >= 1 twice). Same bits either way */
     FMI_TUNE_COMM_A2A = 8,        /* RCCL transport all-to-all: 0 = ncclAllToAll where librccl has it (default),

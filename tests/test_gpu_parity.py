@@ -458,10 +458,12 @@ def test_one_pass_blocked_scan_matches_blocked_launches(device, P):
         fmi_amd.tune_set(Tune.BLOCKS_ONE_PASS, old)
 
 
-@pytest.mark.parametrize("P", [17, 32, 37, 64, 100, 128])
+@pytest.mark.parametrize("P", [17, 32, 37, 64, 100, 128, 129, 255, 300])
 def test_one_pass_chain_matches_blocked_launches(device, P):
     """scan_ltr (32..128 peers) and reduce_ltr (17..128): the one-pass chain kernel (fmi_fused_chain.hip) and the
-    blocked launches give the oracle's left-to-right bits, every op x core dtype, ragged peer blocks, in place."""
+    blocked launches give the oracle's left-to-right bits, every op x core dtype, ragged peer blocks, in place.
+    Beyond 128 peers the chain runs in segments of 127 continued from the previous running value
+    (chain_superblocks)."""
     n = 2 * 4096 + 7
     old = fmi_amd.tune_get(Tune.BLOCKS_ONE_PASS)
     try:
@@ -496,12 +498,13 @@ def test_one_pass_chain_matches_blocked_launches(device, P):
         fmi_amd.tune_set(Tune.BLOCKS_ONE_PASS, old)
 
 
-@pytest.mark.parametrize("P", [17, 32, 33, 48, 64, 80, 100, 112, 128])
+@pytest.mark.parametrize("P", [17, 32, 33, 48, 64, 80, 100, 112, 128, 129, 256, 300, 512])
 def test_one_pass_blocked_tree_matches_blocked_launches(device, P):
     """reduce over 17..128 peers (ragged last blocks at 17, 33, 100) and allreduce over 32..128 peers (pre-fold of
     full blocks at 48, 80, 112; other P take the launches): the one-pass kernels (fmi_fused_tree_blocked.hip) and
     the blocked launches (FMI_TUNE_BLOCKS_ONE_PASS = 0) give the oracle's bits for every op x core dtype, several
-    roots / ranks, and in place (out = an input)."""
+    roots / ranks, and in place (out = an input). Beyond 128 peers reduce runs as superblocks of 128
+    (reduce_superblocks: 129 with a lone last peer, 256, 300, 512) and allreduce as the block launches."""
     n = 2 * 4096 + 3
     old = fmi_amd.tune_get(Tune.BLOCKS_ONE_PASS)
     try:
