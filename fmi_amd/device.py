@@ -323,8 +323,8 @@ def scan_peers(op: Op, alg: Alg, outs: Sequence[Bucket], ins: Sequence[Bucket], 
     """Peer-axis inclusive scan with the bracketing of reference scan_no_order / scan_ltr."""
     if len(outs) != len(ins):
         raise ValueError("scan_peers: one output bucket per peer")
-    for o in outs:
-        _check_peers(o, ins)
+    _check_peers(outs[0], ins)  # O(P): every bucket, in or out, against the first output
+    _check_peers(outs[0], outs)
     _lib.call("fmi_dev_scan_peers", int(op), int(outs[0].dtype), int(alg), _ptr_array(outs), _ptr_array(ins),
               len(ins), outs[0].n, _sptr(stream))
 

@@ -1,6 +1,6 @@
 """Probe of the many-peer, small-bucket scan regime: scan / scan_ltr time against P and bucket
-size, no-re-use protocol. `--short` runs only scan_ltr P = 64 and 256 at 4 MiB (for PMC passes); `--carved` runs those two with every
-bucket a view into one allocation per role (inputs, each output set) against separate allocations.
+size, no-re-use protocol. `--short` runs only scan_ltr P = 64 and 256 at 4 MiB; `--carved` runs those two with every bucket a view into
+one allocation per role (inputs, each output set) against separate allocations.
 
     python tools/probe_scan_cliff.py [--short]
 """
