@@ -361,8 +361,8 @@ int tree_blocked(int op, int dtype, int alg, void* out, const void* const* ins, 
 //   reduce_no_order: binomial rounds 0..6 stay inside each superblock (the one-pass reduce over its <= 128
 //     peers), rounds 7+ are the reduce program over the ceil(P / 128) superblock values.
 // Every input is read once; the superblock values cost 2 ceil(P / 128) bucket passes. Measured over 1 GiB
-// of input (tools/ab_superblocks.py): reduce P = 256 / 300 15 / 11 % faster than the block launches,
-// reduce_ltr P = 256 25 %, scan_ltr P = 256 2 %. allreduce_no_order, P = 2^k, would split the same way
+// of input (tools/ab_superblocks.py): reduce P = 256 / 300 13 / 9 % faster than the block launches,
+// reduce_ltr P = 256 25 %, scan_ltr P = 256 14 %. allreduce_no_order, P = 2^k, would split the same way
 // (rounds 0..6 inside superblocks, each the one-pass 128-peer allreduce for rank r % 128; rounds 7+ over
 // the superblock values for rank r / 128) but was 16-25 % SLOWER than the 16-peer block launches at
 // P = 256 / 512 (128 streams per one-pass kernel against 16 per launch), so allreduce keeps the launches.
