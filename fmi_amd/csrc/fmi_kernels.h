@@ -188,14 +188,16 @@ __device__ __forceinline__ Lanes<T, W> combine(const Lanes<T, W>& a, const Lanes
 // 64-bit address, so any bucket size) with the lane's 32-bit byte offset, and carries an explicit cache
 // policy: loads nt; the tree's one output stream sc1 (written lines leave the XCD L2 at once), the scan's
 // P output streams nt sc1. tools/microbench_cachepol.hip measured, on the same buffers, tree P = 8 3.3 %
-// and scan P = 8 4.6 % faster than global_load / global_store nt (bit-identical results). The pairwise
-// kernel keeps global nt accesses and stores some of its tiles with sc1 (pair_tile below).
+// and scan P = 8 4.6 % faster than global_load / global_store nt (bit-identical results) with few rotating
+// sets; with no set re-read from the MALL (tools/ab_fused_policy.py --footprint-gib 6) the scans keep ~2 %,
+// trees of 4 peers 2.4 %, trees of 8 / 16 are within 1 % either way. The pairwise kernel keeps global nt
+// accesses and stores some of its tiles with sc1 (pair_tile below).
 inline constexpr int kAuxNT = 2, kAuxSC1 = 16;
 inline constexpr int kTreeStoreAux = kAuxSC1, kScanStoreAux = kAuxNT | kAuxSC1, kFusedLoadAux = kAuxNT;
 using b128 = unsigned int __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const void* tile_base) {
-    // raw (stride 0) descriptor, 32-bit data format; num_records covers any 256-thread tile
+    // raw (stride 0) descriptor, 32-bit data format; num_records covers any tile (<= 64 KiB past its base)
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(tile_base), 0, 1 << 30, 0x00020000);
 }
 template <int AUX, class T, int W>
