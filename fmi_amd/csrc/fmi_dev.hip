@@ -365,7 +365,8 @@ int tree_blocked(int op, int dtype, int alg, void* out, const void* const* ins, 
 // reduce_ltr P = 256 25 %, scan_ltr P = 256 14 %. allreduce_no_order, P = 2^k, would split the same way
 // (rounds 0..6 inside superblocks, each the one-pass 128-peer allreduce for rank r % 128; rounds 7+ over
 // the superblock values for rank r / 128) but was 16-25 % SLOWER than the 16-peer block launches at
-// P = 256 / 512 (128 streams per one-pass kernel against 16 per launch), so allreduce keeps the launches.
+// P = 256 / 512 (128 streams per one-pass kernel against 16 per launch); allreduce splits at 64 instead
+// (allreduce_superblocks below).
 // ----------------------------------------------------------------------------------------------------
 constexpr int kSuperPeers = kMaxOnePassScanBlocks * sched::kScanBlock;  // 128
 
@@ -442,12 +443,62 @@ int reduce_superblocks(int op, int dtype, void* out, const void* const* ins, int
     return rc;
 }
 
+// allreduce_no_order over P = 2^k > 128 peers as superblocks of 64 peers (tools/ab_allreduce_super.py, 1 GiB of
+// input: P = 256 / 512 / 1024 19 / 24 / 4 % faster than the 16-peer block launches; superblocks of 128 were
+// slower than the launches, above): recursive-doubling rounds 0..5 stay inside each superblock — its
+// one-pass 64-peer allreduce for rank r % 64, the same for every superblock — and rounds 6+ are the
+// allreduce over the P / 64 superblock values for rank r / 64 (fused up to 16 values, one pass beyond).
+constexpr int kAllreduceSuper = 64;
+
+bool allreduce_superblocks_cover(int op, int dtype, int P) {
+    const int S = P / kAllreduceSuper;
+    return P > kSuperPeers && (P & (P - 1)) == 0 && S <= kSuperPeers &&
+           tree_blocks_one_pass_covers(op, dtype, FMI_ALG_ALLREDUCE, kAllreduceSuper) &&
+           (S <= sched::kMaxFusedPeers || tree_blocks_one_pass_covers(op, dtype, FMI_ALG_ALLREDUCE, S));
+}
+
+int allreduce_superblocks(int op, int dtype, void* out, const void* const* ins, int P, int rank, size_t n,
+                          hipStream_t s) {
+    const int S = P / kAllreduceSuper;
+    std::lock_guard<std::mutex> lk(g_mu);
+    const size_t stride = arena_stride(n, dtype_size(dtype));
+    FMI_RC_TRY(arena_acquire(stride * static_cast<size_t>(S), s));
+    char* base = static_cast<char*>(g_state.arena);
+    std::vector<const void*> vals(S);
+    int rc = FMI_OK;
+    for (int b = 0; b < S && rc == FMI_OK; ++b) {
+        BlockedScanPtrs ptrs{};
+        for (int p = 0; p < kAllreduceSuper; ++p) ptrs.in[p] = ins[b * kAllreduceSuper + p];
+        void* v = base + stride * static_cast<size_t>(b);
+        ptrs.out[0] = v;
+        rc = launch_tree_blocks_one_pass(op, dtype, FMI_ALG_ALLREDUCE, kAllreduceSuper, ptrs, n, rank % kAllreduceSuper, s);
+        vals[b] = v;
+    }
+    if (rc == FMI_OK) {
+        if (S <= sched::kMaxFusedPeers) {
+            PeerPtrs ptrs{};
+            for (int b = 0; b < S; ++b) ptrs.in[b] = vals[b];
+            ptrs.out[0] = out;
+            rc = launch_fused_allreduce(op, dtype, S, ptrs, n, rank / kAllreduceSuper, s);
+        } else {
+            BlockedScanPtrs ptrs{};
+            for (int b = 0; b < S; ++b) ptrs.in[b] = vals[b];
+            ptrs.out[0] = out;
+            rc = launch_tree_blocks_one_pass(op, dtype, FMI_ALG_ALLREDUCE, S, ptrs, n, rank / kAllreduceSuper, s);
+        }
+    }
+    FMI_HIP_TRY(hipEventRecord(g_state.arena_free, s));
+    return rc;
+}
+
 int run_tree_blocked(int op, int dtype, int alg, void* out, const void* const* ins, int P, int rank, size_t n,
                      hipStream_t s) {
     if (g_tune[FMI_TUNE_BLOCKS_ONE_PASS].load() != 0 && P > kSuperPeers) {
         if (alg == FMI_ALG_REDUCE_LTR && std::find(ins + kSuperPeers, ins + P, static_cast<const void*>(out)) == ins + P)
             return chain_superblocks(op, dtype, false, nullptr, out, ins, P, n, s);
         if (tree_superblocks_cover(op, dtype, alg, P)) return reduce_superblocks(op, dtype, out, ins, P, n, s);
+        if (alg == FMI_ALG_ALLREDUCE && allreduce_superblocks_cover(op, dtype, P))
+            return allreduce_superblocks(op, dtype, out, ins, P, rank, n, s);
     }
     if (g_tune[FMI_TUNE_BLOCKS_ONE_PASS].load() != 0 && alg == FMI_ALG_REDUCE_LTR && P <= kMaxOnePassScanBlocks * 16) {
         BlockedScanPtrs ptrs{};

@@ -504,7 +504,8 @@ def test_one_pass_blocked_tree_matches_blocked_launches(device, P):
     full blocks at 48, 80, 112; other P take the launches): the one-pass kernels (fmi_fused_tree_blocked.hip) and
     the blocked launches (FMI_TUNE_BLOCKS_ONE_PASS = 0) give the oracle's bits for every op x core dtype, several
     roots / ranks, and in place (out = an input). Beyond 128 peers reduce runs as superblocks of 128
-    (reduce_superblocks: 129 with a lone last peer, 256, 300, 512) and allreduce as the block launches."""
+    (reduce_superblocks: 129 with a lone last peer, 256, 300, 512), allreduce over 2^k peers as superblocks
+    of 64 (allreduce_superblocks: 256, 512; other P the block launches)."""
     n = 2 * 4096 + 3
     old = fmi_amd.tune_get(Tune.BLOCKS_ONE_PASS)
     try:
