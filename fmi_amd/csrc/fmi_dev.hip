@@ -420,8 +420,6 @@ bool tree_superblocks_cover(int op, int dtype, int alg, int P) {
 
 // reduce_no_order over P > 128 peers (transformed ids, root 0) as superblocks of 128.
 int reduce_superblocks(int op, int dtype, void* out, const void* const* ins, int P, size_t n, hipStream_t s) {
-    const char* env = std::getenv("FMI_RED_SUPER");  // EXPERIMENT: superblock size
-    const int kSuperPeers = env ? std::atoi(env) : fmi::dev::kSuperPeers;
     const int S = (P + kSuperPeers - 1) / kSuperPeers;
     std::lock_guard<std::mutex> lk(g_mu);
     const size_t stride = arena_stride(n, dtype_size(dtype));
