@@ -452,7 +452,8 @@ constexpr int kAllreduceSuper = 64;
 
 bool allreduce_superblocks_cover(int op, int dtype, int P) {
     const int S = P / kAllreduceSuper;
-    return P > kSuperPeers && (P & (P - 1)) == 0 && S <= kSuperPeers &&
+    const int lo = std::getenv("FMI_AR128") ? kSuperPeers - 1 : kSuperPeers;  // EXPERIMENT: P = 128 too
+    return P > lo && (P & (P - 1)) == 0 && S <= kSuperPeers &&
            tree_blocks_one_pass_covers(op, dtype, FMI_ALG_ALLREDUCE, kAllreduceSuper) &&
            (S <= sched::kMaxFusedPeers || tree_blocks_one_pass_covers(op, dtype, FMI_ALG_ALLREDUCE, S));
 }
@@ -493,7 +494,7 @@ int allreduce_superblocks(int op, int dtype, void* out, const void* const* ins, 
 
 int run_tree_blocked(int op, int dtype, int alg, void* out, const void* const* ins, int P, int rank, size_t n,
                      hipStream_t s) {
-    if (g_tune[FMI_TUNE_BLOCKS_ONE_PASS].load() != 0 && P > kSuperPeers) {
+    if (g_tune[FMI_TUNE_BLOCKS_ONE_PASS].load() != 0 && P >= kSuperPeers) {
         if (alg == FMI_ALG_REDUCE_LTR && std::find(ins + kSuperPeers, ins + P, static_cast<const void*>(out)) == ins + P)
             return chain_superblocks(op, dtype, false, nullptr, out, ins, P, n, s);
         if (tree_superblocks_cover(op, dtype, alg, P)) return reduce_superblocks(op, dtype, out, ins, P, n, s);
