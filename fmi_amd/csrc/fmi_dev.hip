@@ -443,17 +443,17 @@ int reduce_superblocks(int op, int dtype, void* out, const void* const* ins, int
     return rc;
 }
 
-// allreduce_no_order over P = 2^k > 128 peers as superblocks of 64 peers (tools/ab_allreduce_super.py, 1 GiB of
-// input: P = 256 / 512 / 1024 19 / 24 / 4 % faster than the 16-peer block launches; superblocks of 128 were
-// slower than the launches, above): recursive-doubling rounds 0..5 stay inside each superblock — its
+// allreduce_no_order over P = 2^k >= 128 peers as superblocks of 64 peers (tools/ab_allreduce_super.py, 1 GiB of
+// input: P = 256 / 512 / 1024 19 / 24 / 4 % faster than the 16-peer block launches; P = 128 28-31 % faster
+// than its one-pass 128-peer kernel, tools/ab_allreduce128.py; superblocks of 128 were slower than the
+// launches, above): recursive-doubling rounds 0..5 stay inside each superblock — its
 // one-pass 64-peer allreduce for rank r % 64, the same for every superblock — and rounds 6+ are the
 // allreduce over the P / 64 superblock values for rank r / 64 (fused up to 16 values, one pass beyond).
 constexpr int kAllreduceSuper = 64;
 
 bool allreduce_superblocks_cover(int op, int dtype, int P) {
     const int S = P / kAllreduceSuper;
-    const int lo = std::getenv("FMI_AR128") ? kSuperPeers - 1 : kSuperPeers;  // EXPERIMENT: P = 128 too
-    return P > lo && (P & (P - 1)) == 0 && S <= kSuperPeers &&
+    return P >= kSuperPeers && (P & (P - 1)) == 0 && S <= kSuperPeers &&
            tree_blocks_one_pass_covers(op, dtype, FMI_ALG_ALLREDUCE, kAllreduceSuper) &&
            (S <= sched::kMaxFusedPeers || tree_blocks_one_pass_covers(op, dtype, FMI_ALG_ALLREDUCE, S));
 }

@@ -319,7 +319,7 @@ typedef enum {
                                     scan_no_order over 32..143 peers, reduce_no_order over 17..128 peers
                                     (beyond: superblocks of 128, one pass each, up to 16384 peers),
                                     allreduce_no_order over 32 / 48 / 64 / 80 / 96 / 112 / 128
-                                    peers (beyond, 2^k peers: superblocks of 64), scan_ltr and
+                                    peers (2^k >= 128 peers: superblocks of 64), scan_ltr and
                                     reduce_ltr over 32..128 peers (beyond: segments of 127 continued
                                     from the running value, any P);
                                     0 = the blocked launches (block values through temps; the scan reads

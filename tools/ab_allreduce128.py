@@ -1,5 +1,6 @@
 """allreduce_no_order over exactly 128 peers: the one-pass 128-peer kernel against two superblocks of 64 plus
-a 2-value allreduce, through a temporary FMI_AR128 switch read only by the library of its commit;
+a 2-value allreduce, through a temporary FMI_AR128 switch read only by the library of commit "allreduce P=128
+measured with a temporary switch" (the superblocks became the default for P = 128 right after);
 no-re-use protocol, interleaved, bit identity checked."""
 import json, os, sys, numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__)))); sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
