@@ -2,7 +2,8 @@
 the i64 max pairwise combine of 64 MiB buckets, the f32 peer-axis scan over 8 peers x 64 MiB, and the fused
 8-peer allreduce tree over the same buckets. Each kernel name appears at one launch shape only, so the
 per-kernel PMC medians are per-launch figures. Buffers rotate over sets larger than the 256 MiB Infinity
-Cache.
+Cache; the pair kernel's over 64 sets, so no launch re-reads a bucket whose sc1-stored tiles the MALL may
+still hold ("store policy across the XCDs"; with 4 sets its trace median read 30.7 us).
 
     rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d DIR -- python3 tools/c3_kernels.py
 """
@@ -26,10 +27,11 @@ def main():
     args = ap.parse_args()
     fmi_amd.init(0)
     n64 = 64 * MIB // 8
+    nsets = 64
     pairs = [(Bucket(n64, np.int64).fill_synthetic(42 + s, 0), Bucket(n64, np.int64).fill_synthetic(42 + s, 1))
-             for s in range(4)]
+             for s in range(nsets)]
     for k in range(args.iters):
-        a, b = pairs[k % 4]
+        a, b = pairs[k % nsets]
         fmi_amd.reduce_pair(Op.MAX, a, b)
     fmi_amd.sync()
     del pairs
