@@ -92,14 +92,19 @@ def parse():
     return ap.parse_args()
 
 
-def pmc_traffic(kernel_substr: str):
-    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary."""
+def pmc_traffic(kernel_substr: str, algo_bytes: int):
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary: the entry whose
+    instantiation contains `kernel_substr` AND whose launch moved `algo_bytes` algorithmic bytes (within
+    1 %). One instantiation is profiled at several shapes (the 8-way tree at N = 8's 32 MiB shards and at
+    C3's 64 MiB buckets): a launch of another shape reports nothing rather than another launch's bytes."""
     path = os.path.join(ROOT, "profiles", "pmc_summary.json")
     if not os.path.exists(path):
         return None, None
     try:
         data = json.load(open(path))
-        hits = [k for k in data.get("kernels", []) if kernel_substr in k.get("kernel", "")]
+        hits = [k for k in data.get("kernels", []) if kernel_substr in k.get("kernel", "")
+                and k.get("algorithmic_bytes_per_launch")
+                and abs(k["algorithmic_bytes_per_launch"] / algo_bytes - 1) < 0.01]
     except Exception:
         return None, None
     if len(hits) != 1:  # absent, or ambiguous (several instantiations match): report nothing rather than a wrong kernel's bytes
@@ -233,12 +238,13 @@ def c2_kernel_signature():
     return f"{form}<fmi::dev::OpSum, float, {fmi_amd.tune_get(Tune.PAIR_UNROLL)}, {nt}>"
 
 
-def _roofline(kernel, algo_bytes, kernel_avg_ms, source, extra=None, pmc_key=None, profiled_shape=True):
-    """profiled_shape: the run uses the bucket size the committed PMC profiles were taken at (the default
-    256 MiB); otherwise the PMC bytes belong to another launch size and traffic is null."""
+def _roofline(kernel, algo_bytes, kernel_avg_ms, source, extra=None, pmc_key=None):
+    """traffic: the committed PMC bytes of exactly this instantiation at exactly this launch shape
+    (pmc_traffic); null when no profile of that launch is committed (e.g. a non-default --bucket-mib)."""
     achieved = algo_bytes / (kernel_avg_ms * 1e-3) / 1e9
-    traffic, traffic_src = pmc_traffic(pmc_key or kernel) if profiled_shape else (
-        None, "not reported: the committed PMC profiles are of the default 256 MiB bucket, this run uses another size")
+    traffic, traffic_src = pmc_traffic(pmc_key or kernel, algo_bytes)
+    if traffic is None:
+        traffic_src = "not reported: no committed PMC profile of this instantiation at this launch shape"
     r = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kernel,
          "kernel_avg_us": round(kernel_avg_ms * 1e3, 2), "algorithmic_bytes_per_launch": algo_bytes,
@@ -295,8 +301,7 @@ def run_single(args):
         b.free()
     roof = _roofline("pair_tile", 3 * nbytes, kernel_avg_ms,
                      "HIP events bracketing the K timed launches on the library stream",
-                     {"kernel_avg_us_isolated": round(isolated_us, 2)}, pmc_key=c2_kernel_signature(),
-                     profiled_shape=args.bucket_mib == 256)
+                     {"kernel_avg_us_isolated": round(isolated_us, 2)}, pmc_key=c2_kernel_signature())
     line = _headline(args, (nbytes / GIB) / (step_ms * 1e-3), step_ms,
                      "C2: 1-GPU pairwise float32 sum-reduce of two 256 MiB device-resident peer buckets",
                      "single GPU (2 peers resident)", n, roof)
@@ -361,7 +366,7 @@ def c3_single(reps: int = 60) -> dict:
         b.free()
 
     def row(ms, algo, key):
-        traffic, src = pmc_traffic(key)  # the committed PMC profile of exactly this instantiation
+        traffic, src = pmc_traffic(key, algo)  # the committed PMC profile of exactly this launch
         return {"kernel_avg_us": round(ms * 1e3, 2), "algorithmic_bytes": algo,
                 "GB_s": round(algo / (ms * 1e-3) / 1e9, 1), "frac": round(algo / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                 "traffic": traffic, "traffic_source": src}
@@ -523,8 +528,7 @@ def run_dist(args, world, rank, local_rank):
                       "timed region (N = 1: the allreduce launches no kernel)"),
                      {"launch_shape": kern["kernel"], "kernel_avg_us_isolated": kern["kernel_avg_us"],
                       "note": "the allreduce step is xGMI-bound (xgmi_roofline); this is its HBM-bound kernel"},
-                     pmc_key=f"tree_kernel<fmi::dev::OpSum, float, 0, {world}, false>",
-                     profiled_shape=args.bucket_mib == 256)
+                     pmc_key=f"tree_kernel<fmi::dev::OpSum, float, 0, {world}, false>")
     path_desc = {"tree": "all-to-all + fused tree kernel + all-gather (bit-exact)",
                  "rccl": "RCCL reduce-scatter + all-gather", "direct": "fused tree over IPC-mapped peer windows"}
     line = _headline(args, value, step_ms,

@@ -56,29 +56,53 @@ def test_defaults_are_the_contract(monkeypatch):
 
 
 def test_roofline_traffic_is_the_launched_kernels():
-    """roofline.traffic comes from the committed PMC summary of exactly the kernel the line measures: C2's
-    default pair_tile<OpSum, float, 4, 3> (not another pair_tile instantiation, e.g. C3's i64 max), and the
-    N>1 shard kernel per world size; PMC bytes within 1 % of the algorithmic bytes. A key matching several
-    instantiations reports nothing rather than a wrong kernel's bytes."""
+    """roofline.traffic comes from the committed PMC summary of exactly the launch the line measures: C2's
+    default pair_tile<OpSum, float, 4, 3> at 256 MiB (not another pair_tile instantiation, e.g. C3's i64
+    max), and the N>1 shard kernel per world size at its shard size; PMC bytes within 1 % of the algorithmic
+    bytes. A key matching several instantiations reports nothing rather than a wrong kernel's bytes."""
     import fmi_amd
 
     fmi_amd.load()
     key = bench.c2_kernel_signature()
     assert key == "pair_tile<fmi::dev::OpSum, float, 4, 3>"
-    traffic, src = bench.pmc_traffic(key)
     algo = 3 * 256 * (1 << 20)
+    traffic, src = bench.pmc_traffic(key, algo)
     assert traffic is not None and abs(traffic / algo - 1) < 0.01, (traffic, src)
-    assert bench.pmc_traffic("pair_tile") == (None, None)  # ambiguous
+    assert bench.pmc_traffic("pair_tile", 3 * 64 * (1 << 20)) != (None, None)  # only C3's i64 max is 64 MiB
+    assert bench.pmc_traffic("tree_kernel", 9 * 32 * (1 << 20)) != (None, None)
+    assert bench.pmc_traffic("synth_kernel", 64 * (1 << 20)) == (None, None)  # ambiguous: f32 and i64
     for world, shard_mib in ((2, 128), (4, 64), (8, 32)):
-        t, _ = bench.pmc_traffic(f"tree_kernel<fmi::dev::OpSum, float, 0, {world}, false>")
-        assert t is not None and abs(t / ((world + 1) * shard_mib * (1 << 20)) - 1) < 0.01, (world, t)
+        shard_algo = (world + 1) * shard_mib * (1 << 20)
+        t, _ = bench.pmc_traffic(f"tree_kernel<fmi::dev::OpSum, float, 0, {world}, false>", shard_algo)
+        assert t is not None and abs(t / shard_algo - 1) < 0.01, (world, t)
 
 
-def test_c3_rows_find_their_pmc_profiles():
-    for key, algo in (("pair_tile<fmi::dev::OpMax, long, 4, 3>", 3 * 64 * (1 << 20)),
-                      ("scan_kernel<fmi::dev::OpSum, float, 3, 8>", 16 * 64 * (1 << 20))):
-        t, _ = bench.pmc_traffic(key)
-        assert t is not None and abs(t / algo - 1) < 0.01, (key, t)
+def test_same_instantiation_at_another_shape_is_not_returned():
+    """The 8-way tree is profiled at two shapes (N = 8's 32 MiB shards, C3's 64 MiB buckets): each lookup gets
+    its own shape's bytes, and a shape with no profile (e.g. --bucket-mib 64 at N = 8: 8 MiB shards) gets
+    nothing, never the other shape's bytes."""
+    key = "tree_kernel<fmi::dev::OpSum, float, 0, 8, false>"
+    t32, _ = bench.pmc_traffic(key, 9 * 32 * (1 << 20))
+    t64, _ = bench.pmc_traffic(key, 9 * 64 * (1 << 20))
+    assert t32 is not None and t64 is not None and abs(t64 / t32 - 2) < 0.01
+    assert bench.pmc_traffic(key, 9 * 8 * (1 << 20)) == (None, None)
+    r = bench._roofline("pair_tile", 3 * 64 * (1 << 20), 0.05, "test",
+                        pmc_key="pair_tile<fmi::dev::OpSum, float, 4, 3>")  # C2's kernel at a non-default size
+    assert r["traffic"] is None and r["traffic_source"].startswith("not reported")
+
+
+def test_pmc_merge_keeps_both_shapes(tmp_path):
+    """tools/pmc_summarize.py: a merge replaces an entry only by a profile of the same instantiation AND shape."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from pmc_summarize import algorithmic_bytes, same_launch
+
+    name = "void fmi::dev::tree_kernel<fmi::dev::OpSum, float, 0, 8, false>(fmi::dev::PeerPtrs, unsigned long, int, int)"
+    a = {"kernel": name, "algorithmic_bytes_per_launch": algorithmic_bytes(name, 32 * (1 << 20) + 128)}
+    b = {"kernel": name, "algorithmic_bytes_per_launch": algorithmic_bytes(name, 64 * (1 << 20))}
+    assert a["algorithmic_bytes_per_launch"] == 9 * 32 * (1 << 20)
+    assert not same_launch(a, b) and same_launch(a, dict(a))
+    assert algorithmic_bytes("void fmi::dev::scan_kernel<fmi::dev::OpSum, float, 3, 8>(x)", 512 << 20) == 1 << 30
+    assert algorithmic_bytes("void fmi::dev::pair_tile<fmi::dev::OpMax, long, 4, 3>(x)", 64 << 20) == 192 << 20
 
 
 def test_measure_deadline_names_the_phase_and_exits_nonzero():

@@ -15,7 +15,38 @@ import glob
 import json
 import os
 import shutil
+import re
 import statistics
+
+
+def algorithmic_bytes(kernel: str, write_bytes: float):
+    """Algorithmic HBM bytes of one launch, from the launch's output bytes, which every
+    kernel here writes exactly once: pair a = a (+) b reads 2 and writes 1 bucket (3 x out); the fused P-way
+    tree reads P buckets and writes one (P + 1 x out); the peer-axis scan reads P and writes P (2 x out); the
+    synthetic-input generator only writes (1 x out); a buffer copy reads and writes (2 x out). The output is
+    rounded to whole 4 KiB pages first (a WRITE_SIZE median carries a few hundred stray bytes). None for a
+    kernel of another shape."""
+    out = round(write_bytes / 4096) * 4096
+    m = re.search(r"tree_kernel<[^,]+, [^,]+, \d+, (\d+),", kernel)
+    if m:
+        return (int(m.group(1)) + 1) * out
+    if "pair_tile<" in kernel or "pair_stride<" in kernel:
+        return 3 * out
+    if "scan_kernel<" in kernel:
+        return 2 * out
+    if "synth_kernel<" in kernel:
+        return out
+    if "copyBuffer" in kernel:
+        return 2 * out
+    return None
+
+
+def same_launch(a: dict, b: dict) -> bool:
+    """Two PMC entries describe the same launch: the same instantiation (name up to the parameter list) AND
+    the same algorithmic bytes — the N = 8 shard tree (32 MiB shards) and C3's 8-peer tree (64 MiB buckets)
+    are one instantiation at two shapes and must both stay."""
+    return (a["kernel"].split("(")[0] == b["kernel"].split("(")[0]
+            and a.get("algorithmic_bytes_per_launch") == b.get("algorithmic_bytes_per_launch"))
 
 
 def _rows(path_glob):
@@ -36,7 +67,8 @@ def main():
     ap.add_argument("--no-default", action="store_true",
                     help="do not overwrite profiles/pmc_summary.json (the file bench.py reads for C2)")
     ap.add_argument("--merge", action="store_true",
-                    help="add these kernels to profiles/pmc_summary.json (replacing same-name entries) instead of "
+                    help="add these kernels to profiles/pmc_summary.json (replacing entries of the same instantiation "
+                         "and shape) instead of "
                          "overwriting it: e.g. the N > 1 shard kernels beside C2's pair kernel")
     ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                                   "profiles"))
@@ -70,6 +102,7 @@ def main():
             "hbm_read_bytes_per_launch": int(round(2 * f_kib * 1024)),
             "hbm_write_bytes_per_launch": int(round(w_kib * 1024)),
             "hbm_bytes_per_launch": int(round(2 * f_kib * 1024 + w_kib * 1024)),
+            "algorithmic_bytes_per_launch": algorithmic_bytes(name, w_kib * 1024),
             "trace": durations.get(name),
         })
     summary = {
@@ -83,10 +116,9 @@ def main():
     default = os.path.join(args.out, "pmc_summary.json")
     if args.merge and os.path.exists(default):
         merged = json.load(open(default))
-        # same instantiation = same name up to the parameter list (a kernel whose arguments changed replaces
-        # its old entry instead of standing beside it)
-        names = {k["kernel"].split("(")[0] for k in kernels}
-        merged["kernels"] = [k for k in merged["kernels"] if k["kernel"].split("(")[0] not in names] + kernels
+        # an entry is replaced only by a profile of the same launch (instantiation AND shape, same_launch);
+        # the same instantiation at another shape stands beside it
+        merged["kernels"] = [k for k in merged["kernels"] if not any(same_launch(k, n) for n in kernels)] + kernels
         merged.setdefault("merged", []).append({"source": summary["source"], "command": args.command})
         with open(default, "w") as f:
             json.dump(merged, f, indent=1)
