@@ -306,6 +306,7 @@ def run_single(args):
                      "C2: 1-GPU pairwise float32 sum-reduce of two 256 MiB device-resident peer buckets",
                      "single GPU (2 peers resident)", n, roof)
     line["config"]["peers"] = 2
+    line["allreduce_1peer"] = one_peer_allreduce(n)
     if not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args)
     if not args.no_c3:
@@ -321,6 +322,39 @@ def run_single(args):
         except Exception as e:  # reported, never fails the measured line
             line["c5"] = f"failed: {type(e).__name__}: {e}"
     print(json.dumps(line), flush=True)
+
+
+def one_peer_allreduce(n: int, launches: int = 20) -> dict:
+    """The N = 1 point of the N > 1 curve's own workload: fmi_comm_allreduce of one 256 MiB bucket on a
+    one-rank communicator — the reference's P = 1 allreduce (PeerToPeer.cpp:96-130 with P = 1) is a copy
+    of the bucket into recvbuf (2·S HBM bytes). Events around back-to-back calls on the library stream."""
+    import numpy as np
+
+    from fmi_amd import Bucket, Event, Op
+    from fmi_amd.comm import Comm, Transport, unique_id
+
+    comm = Comm(unique_id(Transport.LOCAL), 1, 0)
+    src, dst = Bucket(n, np.float32).fill_synthetic(11, 0), Bucket(n, np.float32)
+    try:
+        comm.allreduce(Op.SUM, src, dst)
+        e0, e1 = Event(), Event()
+        e0.record()
+        for _ in range(launches):
+            comm.allreduce(Op.SUM, src, dst)
+        e1.record()
+        e1.sync()
+        ms = e0.elapsed_ms(e1) / launches
+        e0.destroy()
+        e1.destroy()
+        ok = bool(np.array_equal(src.view(0, 4096).numpy().view(np.uint32), dst.view(0, 4096).numpy().view(np.uint32)))
+    finally:
+        src.free()
+        dst.free()
+        comm.destroy()
+    S = n * 4
+    return {"workload": f"fmi_comm_allreduce, 1 rank, {S >> 20} MiB f32 (the reference's P = 1 allreduce: a copy)",
+            "ms": round(ms, 4), "GiB_s_reduced_buckets": round(S / GIB / (ms * 1e-3), 2),
+            "hbm_frac": round(2 * S / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "result_ok": ok, "launches": launches}
 
 
 C3_PAIR_SETS = 64  # 63 x 8 MiB of sc1 tile writes between two uses of a set (see --sets)
@@ -506,6 +540,11 @@ def run_dist(args, world, rank, local_rank):
     fmi_amd.init(dev)
     watch.enter("fmi_comm init (communicator id broadcast, RCCL init)")
     ar = CommAllreduce(dist.group.WORLD, path=args.path, transport=args.transport)
+    watch.enter("topology check")
+    topo = ar.topology()
+    if not topo["ok"]:  # RCCL did not see `world` ranks, or two ranks share a GPU: the line would be wrong
+        print("bench: topology check FAILED: " + json.dumps(topo), file=sys.stderr, flush=True)
+        os._exit(1)
     n = args.bucket_mib * MIB // 4
     S = n * 4
     watch.enter("warm-up and timed allreduces")
@@ -536,6 +575,7 @@ def run_dist(args, world, rank, local_rank):
                      f"(a {args.bucket_mib} MiB device-resident bucket) per GPU, through fmi_comm_allreduce",
                      f"{world} GPUs, one peer per GPU, buckets sharded {world} ways; path {args.path}: "
                      f"{path_desc[args.path]}; transport {args.transport}", n, roof)
+    line["config"]["topology"] = topo
     line["config"].update({"rotating_sets": args.dist_sets, "numa_binding_rank0": numa, "peers": world,
                            "path": args.path, "transport": args.transport,
                            "algbw_GiB_s": extra["algbw_GiB_s"], "busbw_GiB_s": extra["busbw_GiB_s"],
@@ -571,8 +611,13 @@ def run_dist(args, world, rank, local_rank):
 
 
 def after_value(args, ar, world, dist, line, proc):
-    """Config C4 at its own size, config C5, then the diagnostics — each max over ranks, recorded into
-    `line` as it completes (a deadline prints whatever is there)."""
+    """The single-GPU anchor, config C4 at its own size, config C5, then the diagnostics — each max over
+    ranks, recorded into `line` as it completes (a deadline prints whatever is there)."""
+    if ar.rank == 0:  # the same N x S allreduce on ONE GPU (no exchange): separates xGMI cost from HBM cost
+        line["local_equivalent"] = ar.local_equivalent(args.bucket_mib * MIB // 4)
+        line["local_equivalent"]["value_over_local"] = round(line["value"] / line["local_equivalent"][
+            "GiB_s_reduced_buckets"], 4)
+    dist.barrier()
     n4 = args.c4_mib * MIB // 4
     steps4, warm4 = max(5, args.steps // 10), 2
     c4 = line["c4"] = {"workload": f"C4: {world} peers x {args.c4_mib} MiB f32 sum-allreduce, one peer per GPU",
@@ -676,15 +721,58 @@ def replicated_pairs(args, ar) -> dict:
             "steps": steps}
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def relay(cmd, env=None) -> int:
+    """Run `cmd` as a CHILD process (never exec: this process may not replace itself once anything touched the
+    GPU, and nothing here has) and relay its output: JSON lines go to our stdout as they arrive, everything else
+    to stderr, so the one line rank 0 prints stays the only stdout line. Returns the child's exit status
+    (non-zero when any rank failed: torch.distributed.run exits non-zero then)."""
+    child = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, bufsize=1, env=env)
+    try:
+        for line in child.stdout:
+            out = sys.stdout if line.lstrip().startswith("{") else sys.stderr
+            out.write(line)
+            out.flush()
+        return child.wait()
+    except BaseException:
+        child.kill()
+        child.wait()
+        raise
+
+
+def launch_ranks(n: int, argv) -> int:
+    """`python bench.py --gpus N` (N > 1) started without a launcher: start N ranks, one per GPU, under
+    torch.distributed.run on this node (rendezvous on 127.0.0.1) as a child process, relay rank 0's line, and
+    return non-zero if any rank failed. Runs before torch or fmi_amd is imported."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + list(argv)
+    print("bench: --gpus %d without a launcher: starting %s" % (n, " ".join(cmd)), file=sys.stderr, flush=True)
+    env = dict(os.environ, FMI_BENCH_LAUNCHED="1")
+    return relay(cmd, env)
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        if os.environ.get("FMI_BENCH_LAUNCHED"):  # a launched rank without WORLD_SIZE: never recurse
+            raise SystemExit("bench: launched rank has no WORLD_SIZE")
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     if world != args.gpus:
         if args.gpus > 1 and world == 1:
-            raise SystemExit(f"--gpus {args.gpus} needs torch.distributed.run with {args.gpus} processes")
+            raise SystemExit(f"--gpus {args.gpus} needs {args.gpus} processes (launched with WORLD_SIZE=1)")
         args.gpus = world
+    if os.environ.get("FMI_BENCH_TEST_FAIL_RANK") == str(rank) and world > 1:  # CPU test of the launcher's status
+        raise SystemExit(f"bench: rank {rank} failing on purpose (FMI_BENCH_TEST_FAIL_RANK)")
     if world > 1 or args.force_dist:
         run_dist(args, world, rank, local_rank)
     else:

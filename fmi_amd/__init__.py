@@ -7,14 +7,14 @@ Layout:
   fmi_amd/device.py          Python handle over the C-ABI (ctypes)
   fmi_amd/collectives.py     multi-GPU sharded allreduce over torch.distributed (RCCL over xGMI)
 """
-from ._lib import FmiError, LIB_PATH, load  # noqa: F401
+from ._lib import FmiError, LIB_PATH, Timeout, load  # noqa: F401
 from .device import (  # noqa: F401
     Alg, Bucket, DType, Event, Graph, HostRegistration, Op, PinnedArray, Stream, Tune, combine, describe,
-    device_count, finalize, host_reduce_pair, init, reduce_pair, reduce_pair_batch, reduce_tree, scan_peers, schedule_expr, sync, tune_get, tune_set,
+    device_count, finalize, host_reduce_pair, init, pci_bus_id, reduce_pair, reduce_pair_batch, reduce_tree, scan_peers, schedule_expr, sync, tune_get, tune_set,
 )
 
 __all__ = [
     "Alg", "Bucket", "DType", "Event", "FmiError", "Graph", "HostRegistration", "LIB_PATH", "Op", "PinnedArray", "Stream",
-    "Tune", "combine", "describe", "device_count", "finalize", "host_reduce_pair", "init", "load", "reduce_pair", "reduce_pair_batch",
+    "Timeout", "Tune", "combine", "describe", "device_count", "finalize", "host_reduce_pair", "init", "load", "pci_bus_id", "reduce_pair", "reduce_pair_batch",
     "reduce_tree", "scan_peers", "schedule_expr", "sync", "tune_get", "tune_set",
 ]

@@ -22,6 +22,7 @@ FMI_ERR_NO_DEVICE = -3
 FMI_ERR_UNSUPPORTED = -4
 FMI_ERR_ALLOC = -5
 FMI_ERR_COMM = -6
+FMI_ERR_TIMEOUT = -7
 
 _STATUS_NAMES = {
     FMI_ERR_INVALID: "FMI_ERR_INVALID",
@@ -30,6 +31,7 @@ _STATUS_NAMES = {
     FMI_ERR_UNSUPPORTED: "FMI_ERR_UNSUPPORTED",
     FMI_ERR_ALLOC: "FMI_ERR_ALLOC",
     FMI_ERR_COMM: "FMI_ERR_COMM",
+    FMI_ERR_TIMEOUT: "FMI_ERR_TIMEOUT",
 }
 
 
@@ -39,6 +41,14 @@ class FmiError(RuntimeError):
     def __init__(self, status: int, message: str):
         super().__init__(f"{_STATUS_NAMES.get(status, status)}: {message}")
         self.status = status
+
+
+class Timeout(FmiError):
+    """A peer did not arrive within the communicator's timeout (FMI_ERR_TIMEOUT): the reference's
+    FMI::Utils::Timeout (include/utils/Common.h:11-15). The communicator is aborted; destroy it."""
+
+    def __init__(self, message: str = "Timeout was reached"):
+        super().__init__(FMI_ERR_TIMEOUT, message)
 
 
 _c = ctypes
@@ -55,6 +65,7 @@ SIGNATURES = {
     "fmi_dev_finalize": (_i, []),
     "fmi_dev_sync": (_i, []),
     "fmi_dev_describe": (_i, [_c.c_char_p, _sz]),
+    "fmi_dev_pci_bus_id": (_i, [_i, _c.c_char_p, _sz]),
     "fmi_dev_alloc": (_i, [_c.POINTER(_vp), _sz]),
     "fmi_dev_free": (_i, [_vp]),
     "fmi_host_pin_alloc": (_i, [_c.POINTER(_vp), _sz]),
@@ -86,8 +97,11 @@ SIGNATURES = {
     "fmi_host_reduce_pair": (_i, [_i, _i, _vp, _vp, _sz]),
     "fmi_comm_unique_id": (_i, [_i, _vp, _sz]),
     "fmi_comm_init": (_i, [_c.POINTER(_vp), _vp, _i, _i]),
+    "fmi_comm_init_timeout": (_i, [_c.POINTER(_vp), _vp, _i, _i, _c.c_double]),
     "fmi_comm_destroy": (_i, [_vp]),
     "fmi_comm_size": (_i, [_vp, _c.POINTER(_i), _c.POINTER(_i)]),
+    "fmi_comm_sync": (_i, [_vp, _vp]),
+    "fmi_comm_query": (_i, [_vp, _c.POINTER(_i), _c.POINTER(_i), _c.POINTER(_i)]),
     "fmi_comm_window_alloc": (_i, [_vp, _sz, _c.POINTER(_vp)]),
     "fmi_comm_window_free": (_i, [_vp, _vp]),
     "fmi_comm_timing": (_i, [_vp, _i]),
@@ -144,6 +158,8 @@ def last_error() -> str:
 
 
 def check(status: int) -> None:
+    if status == FMI_ERR_TIMEOUT:
+        raise Timeout(last_error())
     if status != FMI_OK:
         raise FmiError(status, last_error())
 

@@ -261,6 +261,69 @@ class CommAllreduce:
         dist.broadcast_object_list(box, src=0, group=self.group)
         self.comm = Comm(box[0], self.world, self.rank)
 
+    def topology(self) -> dict:
+        """What every rank runs on, all-gathered: the transport's own view of the communicator (RCCL:
+        ncclCommCount / ncclCommUserRank / ncclCommCuDevice through fmi_comm_query), the torch device ordinal
+        and the GPU's PCI bus id. ok: the transport saw exactly `world` ranks, each rank at its own index,
+        and (RCCL) no two ranks share a GPU. PROC ranks may share one GPU by design: labelled, not an error."""
+        from . import device as fdev
+
+        q = self.comm.query()
+        dev = torch.cuda.current_device()
+        mine = {"rank": self.rank, "transport_count": q["count"], "transport_rank": q["rank"],
+                "transport_device": q["device"], "torch_device": dev, "pci_bus_id": fdev.pci_bus_id(dev)}
+        every = [None] * self.world
+        dist.all_gather_object(every, mine, group=self.group)
+        counts = sorted({e["transport_count"] for e in every})
+        pci = [e["pci_bus_id"] for e in every]
+        distinct = len(set(pci)) == len(pci)
+        ranks_ok = counts == [self.world] and all(e["transport_rank"] == e["rank"] for e in every)
+        shared_ok = self.transport == "proc"  # several PROC ranks on one GPU is what the transport is for
+        res = {"transport": self.transport, "rccl_ranks": counts[0] if len(counts) == 1 else counts,
+               "ranks": [{k: e[k] for k in ("transport_rank", "transport_device", "torch_device", "pci_bus_id")}
+                         for e in every],
+               "distinct_gpus": distinct, "ok": bool(ranks_ok and (distinct or shared_ok))}
+        if self.transport != "rccl":
+            res["rccl_ranks"] = None
+            res["transport_ranks"] = counts[0] if len(counts) == 1 else counts
+        if not distinct and shared_ok:
+            res["note"] = "PROC transport: ranks share GPUs by design (single-GPU runs of the N > 1 path)"
+        return res
+
+    def local_equivalent(self, n: int, launches: int = 10, sets: int = 2) -> dict:
+        """The like-for-like single-GPU anchor of the N > 1 line: the same world-peer f32 sum-allreduce of
+        n-element buckets computed on ONE GPU (this rank's) by the fused kernel (fmi_dev_reduce_tree,
+        allreduce_no_order order, every bucket resident in this GPU's HBM): HBM-bound, (N + 1)·S algorithmic
+        bytes per launch. `GiB_s_reduced_buckets` = N·S / t, the unit of the line's `value`. Rotating sets;
+        mean of back-to-back launches on the library stream (HIP events)."""
+        import numpy as np
+
+        from . import device as fdev
+
+        N = self.world
+        ins = [[fdev.Bucket(n, np.float32).fill_synthetic(42 + s, p) for p in range(N)] for s in range(sets)]
+        out = fdev.Bucket(n, np.float32)
+        for s in range(sets):
+            fdev.reduce_tree(Op.SUM, Alg.ALLREDUCE, out, ins[s])
+        fdev.sync()
+        e0, e1 = fdev.Event(), fdev.Event()
+        e0.record()
+        for k in range(launches):
+            fdev.reduce_tree(Op.SUM, Alg.ALLREDUCE, out, ins[k % sets])
+        e1.record()
+        e1.sync()
+        ms = e0.elapsed_ms(e1) / launches
+        e0.destroy()
+        e1.destroy()
+        for b in [out] + [x for s in ins for x in s]:
+            b.free()
+        S = n * 4
+        return {"workload": f"{N} peers x {S >> 20} MiB f32 sum-allreduce on ONE GPU (fused {N}-way kernel, "
+                            f"fmi_dev_reduce_tree): what the N-GPU step computes, without the exchange",
+                "ms": round(ms, 4), "GiB_s_reduced_buckets": round(N * S / 2 ** 30 / (ms * 1e-3), 2),
+                "hbm_frac": round((N + 1) * S / (ms * 1e-3) / 8e12, 4) if N > 1 else None,
+                "launches": launches, "rotating_sets": sets}
+
     def max_over_ranks(self, *vals: float) -> List[float]:
         t = torch.tensor(vals, dtype=torch.float64, device=self._red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)

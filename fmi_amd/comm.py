@@ -15,6 +15,8 @@ from typing import Optional
 from . import _lib
 import numpy as np
 
+from ._lib import Timeout  # noqa: F401 - FMI_ERR_TIMEOUT, the reference's FMI::Utils::Timeout
+
 from .device import NP_DTYPE, Alg, Bucket, Op, _sptr, dtype_of
 
 ID_BYTES = 128
@@ -45,12 +47,14 @@ def _p(x) -> Optional[int]:
 
 
 class Comm:
-    def __init__(self, uid: bytes, nranks: int, rank: int):
+    def __init__(self, uid: bytes, nranks: int, rank: int, timeout_s: Optional[float] = None):
+        """timeout_s: how long any wait for the peers may last (init rendezvous, barriers, sync); None = the
+        library default (FMI_COMM_TIMEOUT_S, else 300 s). Expiry raises Timeout and aborts the communicator."""
         if len(uid) != ID_BYTES:
             raise ValueError("communicator id must be 128 bytes")
         h = ctypes.c_void_p()
         self._id = ctypes.create_string_buffer(uid, ID_BYTES)
-        _lib.call("fmi_comm_init", ctypes.byref(h), self._id, nranks, rank)
+        _lib.call("fmi_comm_init_timeout", ctypes.byref(h), self._id, nranks, rank, float(timeout_s or 0.0))
         self.handle = h.value
         self.nranks = nranks
         self.rank = rank
@@ -66,6 +70,18 @@ class Comm:
                 _lib.load().fmi_comm_destroy(self.handle)
         except Exception:
             pass
+
+    def sync(self, stream=None) -> None:
+        """Wait for the collectives enqueued on `stream` (None = library stream) within the communicator's
+        timeout; raises Timeout (the communicator is then aborted) or FmiError on a transport error."""
+        _lib.call("fmi_comm_sync", self.handle, _sptr(stream))
+
+    def query(self) -> dict:
+        """What the transport reports about this rank: RCCL's own rank count, rank and device
+        (ncclCommCount / ncclCommUserRank / ncclCommCuDevice); the communicator's for LOCAL / PROC."""
+        cnt, rk, dev = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        _lib.call("fmi_comm_query", self.handle, ctypes.byref(cnt), ctypes.byref(rk), ctypes.byref(dev))
+        return {"count": cnt.value, "rank": rk.value, "device": dev.value}
 
     def timing(self, enable: bool) -> None:
         """Record an event pair around every shard-kernel launch of the collectives (fmi_comm_timing)."""

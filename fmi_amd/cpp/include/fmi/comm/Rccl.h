@@ -36,13 +36,19 @@ public:
     //! broadcasts it, every peer initialises its rank. transport: FMI_TRANSPORT_RCCL (one process per GPU),
     //! FMI_TRANSPORT_PROC (peers are processes of one node, e.g. several sharing one GPU) or
     //! FMI_TRANSPORT_LOCAL (peers are threads of one process sharing one GPU).
+    //! timeout_s bounds every wait for the peers (the init rendezvous, barriers, each collective's
+    //! completion); on expiry the call throws Utils::Timeout, as the reference's channels do
+    //! (src/comm/Direct.cpp:28-30), and the channel is unusable. <= 0: the library default
+    //! (FMI_COMM_TIMEOUT_S, else 300 s).
     static std::shared_ptr<Rccl> connect(Channel& bootstrap, Utils::peer_num peer, Utils::peer_num num_peers,
-                                         int transport = FMI_TRANSPORT_RCCL, double link_gb_s = 300.) {
+                                         int transport = FMI_TRANSPORT_RCCL, double link_gb_s = 300.,
+                                         double timeout_s = 0.) {
         std::array<char, FMI_COMM_ID_BYTES> id{};
         if (peer == 0) Dev::check(fmi_comm_unique_id(transport, id.data(), id.size()), "fmi_comm_unique_id");
         bootstrap.bcast({id.data(), id.size()}, 0);
         fmi_comm_t comm = nullptr;
-        Dev::check(fmi_comm_init(&comm, id.data(), static_cast<int>(num_peers), static_cast<int>(peer)), "fmi_comm_init");
+        Dev::check(fmi_comm_init_timeout(&comm, id.data(), static_cast<int>(num_peers), static_cast<int>(peer), timeout_s),
+                   "fmi_comm_init");
         auto ch = std::shared_ptr<Rccl>(new Rccl(comm, link_gb_s));
         ch->set_peer_id(peer);
         ch->set_num_peers(num_peers);
@@ -198,9 +204,11 @@ private:
             throw std::runtime_error("Rccl channel needs a built-in reduction op (Function<T>(Utils::Op::...))");
         return f.device;
     }
-    static void run(int status, const char* what) {
+    // FMI collectives are blocking: wait for completion within the communicator's timeout
+    // (FMI_ERR_TIMEOUT -> Utils::Timeout, Dev::check)
+    void run(int status, const char* what) const {
         Dev::check(status, what);
-        Dev::check(fmi_stream_sync(nullptr), "fmi_stream_sync");  // FMI collectives are blocking
+        Dev::check(fmi_comm_sync(comm_, nullptr), "fmi_comm_sync");
     }
     static void mirror(const channel_data& sendbuf, const channel_data& recvbuf) {
         if (sendbuf.buf != recvbuf.buf)

@@ -1,8 +1,9 @@
 // FMI::Dev — C++ RAII layer over the C-ABI in include/fmi_dev.h (libfmi_dev.so, gfx950).
 //
-// Error convention: every C-ABI status != 0 becomes a std::runtime_error carrying
-// fmi_last_error(), the exception type the reference itself throws for usage errors
-// (reference include/Communicator.h:90,114,138).
+// Error convention: a C-ABI FMI_ERR_TIMEOUT becomes FMI::Utils::Timeout (reference
+// include/utils/Common.h:11-15, what its channels throw when a peer stays away, src/comm/Direct.cpp:28-30);
+// every other status != 0 a std::runtime_error carrying fmi_last_error(), the exception type the reference
+// itself throws for usage errors (reference include/Communicator.h:90,114,138).
 #ifndef FMI_AMD_DEV_DEVICE_H
 #define FMI_AMD_DEV_DEVICE_H
 
@@ -15,11 +16,13 @@
 #include <utility>
 #include <vector>
 
+#include "../utils/Common.h"
 #include "fmi_dev.h"  // C-ABI: add -I<repo>/include
 
 namespace FMI::Dev {
 
 inline void check(int status, const char* what) {
+    if (status == FMI_ERR_TIMEOUT) throw Utils::Timeout();
     if (status != FMI_OK) throw std::runtime_error(std::string(what) + ": " + fmi_last_error());
 }
 

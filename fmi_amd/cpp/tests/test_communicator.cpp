@@ -780,6 +780,51 @@ GPU_TEST(rccl_channel_collectives_local_transport) {
     }
 }
 
+// A peer that never arrives: the Rccl channel's collective throws FMI::Utils::Timeout once its timeout
+// passes, as the reference's channels do when a peer stays away (src/comm/Direct.cpp:28-30,40-42), and the
+// channel is unusable (std::runtime_error) until destroyed. LOCAL transport (peers = threads on one GPU).
+GPU_TEST(rccl_channel_absent_peer_raises_timeout) {
+    Dev::init(0);
+    auto mailbox = std::make_shared<FMI::Comm::Mailbox>();
+    const std::size_t n = 4096;
+    bool timed_out = false, unusable = false;
+    double waited_s = 0;
+    std::string error;
+    auto member = [&](peer_num p, bool participate) {
+        try {
+            Communicator c(p, 2, "", "timeout-test");
+            auto loop = std::make_shared<FMI::Comm::Loopback>(mailbox, std::chrono::seconds(60));
+            c.register_channel("Loopback", loop);
+            c.register_channel("Rccl", FMI::Comm::Rccl::connect(*loop, p, 2, FMI_TRANSPORT_LOCAL, 300., 1.0));
+            if (!participate) return;  // joined the communicator, never calls the collective
+            Data<Dev::Bucket<float>> a(synth_f32(n, 3, p)), r(n);
+            const auto t0 = std::chrono::steady_clock::now();
+            try {
+                c.allreduce(a, r, Function<Dev::Bucket<float>>(Op::sum));
+            } catch (const FMI::Utils::Timeout&) {
+                timed_out = true;
+            }
+            waited_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+            try {
+                c.allreduce(a, r, Function<Dev::Bucket<float>>(Op::sum));
+            } catch (const FMI::Utils::Timeout&) {
+            } catch (const std::runtime_error&) {
+                unusable = true;  // the aborted communicator refuses further work
+            }
+        } catch (const std::exception& e) {
+            error = e.what();
+        }
+    };
+    std::thread present(member, 0u, true), absent(member, 1u, false);
+    present.join();
+    absent.join();
+    if (!error.empty()) std::fprintf(stderr, "  threw: %s\n", error.c_str());
+    CHECK(error.empty());
+    CHECK(timed_out);
+    CHECK(waited_s >= 0.9 && waited_s < 30.0);
+    CHECK(unusable);
+}
+
 GPU_TEST(policy_routes_device_buckets_to_rccl) {
     Dev::init(0);
     std::map<std::string, std::shared_ptr<FMI::Comm::Channel>> chans;

@@ -84,6 +84,15 @@ struct RcclApi {
     ncclResult_t (*AllToAll)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t);
     // optional: a second communicator for the pipelined allreduce (FMI_TUNE_COMM_PIPELINE)
     ncclResult_t (*CommSplit)(ncclComm_t, int, int, ncclComm_t*, ncclConfig_t*);
+    // optional: bounded waits (non-blocking init, asynchronous errors, abort on timeout) and introspection
+    ncclResult_t (*CommInitRankConfig)(ncclComm_t*, int, ncclUniqueId, int, ncclConfig_t*);
+    ncclResult_t (*CommGetAsyncError)(ncclComm_t, ncclResult_t*);
+    ncclResult_t (*CommAbort)(ncclComm_t);
+    ncclResult_t (*CommFinalize)(ncclComm_t);
+    ncclResult_t (*CommCount)(const ncclComm_t, int*);
+    ncclResult_t (*CommUserRank)(const ncclComm_t, int*);
+    ncclResult_t (*CommCuDevice)(const ncclComm_t, int*);
+    bool bounded() const { return CommInitRankConfig && CommGetAsyncError && CommAbort; }
 };
 
 const RcclApi* rccl_api() {
@@ -119,6 +128,15 @@ const RcclApi* rccl_api() {
 #undef FMI_RCCL_SYM
         api.AllToAll = reinterpret_cast<decltype(api.AllToAll)>(dlsym(h, "ncclAllToAll"));
         api.CommSplit = reinterpret_cast<decltype(api.CommSplit)>(dlsym(h, "ncclCommSplit"));
+#define FMI_RCCL_OPT(name) api.name = reinterpret_cast<decltype(api.name)>(dlsym(h, "nccl" #name));
+        FMI_RCCL_OPT(CommInitRankConfig)
+        FMI_RCCL_OPT(CommGetAsyncError)
+        FMI_RCCL_OPT(CommAbort)
+        FMI_RCCL_OPT(CommFinalize)
+        FMI_RCCL_OPT(CommCount)
+        FMI_RCCL_OPT(CommUserRank)
+        FMI_RCCL_OPT(CommCuDevice)
+#undef FMI_RCCL_OPT
         ok = true;
     });
     if (!ok) {
@@ -141,10 +159,82 @@ int nccl_fail(const RcclApi* api, const char* what, ncclResult_t r) {
 // ---------------------------------------------------------------------------------------------------
 // transports
 // ---------------------------------------------------------------------------------------------------
+using Clock = std::chrono::steady_clock;
+
+double env_seconds(const char* name, double fallback) {
+    const char* e = std::getenv(name);
+    if (!e || !*e) return fallback;
+    const double v = std::atof(e);
+    return v > 0 ? v : fallback;
+}
+
+// The default timeout of a communicator (fmi_comm_init): FMI_COMM_TIMEOUT_S, then (PROC) the older
+// FMI_PROC_TIMEOUT_S, then 300 s.
+double default_timeout_s(bool proc) {
+    return env_seconds("FMI_COMM_TIMEOUT_S", proc ? env_seconds("FMI_PROC_TIMEOUT_S", 300.0) : 300.0);
+}
+
+// Poll with back-off: spin ~1k times, then sleep 5 us, then 200 us between checks.
+void backoff(int k) {
+    if (k < 1000) return;
+    std::this_thread::sleep_for(std::chrono::microseconds(k < 10000 ? 5 : 200));
+}
+
 class Transport {
 public:
     Transport(int n, int rank) : n_(n), rank_(rank) {}
     virtual ~Transport() = default;
+
+    // ---- bounded waits (reference FMI::Utils::Timeout semantics) ----
+    void set_timeout(double seconds) { timeout_s_ = seconds; }
+    double timeout_s() const { return timeout_s_; }
+    bool aborted() const { return aborted_; }
+    // An asynchronous error of the transport (a peer's connection failed), FMI_OK if none.
+    virtual int poll() { return FMI_OK; }
+    // Give up on the peers: release what waits for them (RCCL: ncclCommAbort ends its kernels). Idempotent.
+    virtual void abort() { aborted_ = true; }
+    // Abort and report a timeout.
+    int timed_out(const std::string& what) {
+        abort();
+        return fail(FMI_ERR_TIMEOUT, "Timeout was reached: " + what + " (no peer progress within " +
+                                         std::to_string(timeout_s_) + " s; communicator aborted)");
+    }
+    // Wait for the work on s within the timeout, watching for transport errors.
+    int wait_stream(hipStream_t s, const char* what) {
+        const auto t0 = Clock::now();
+        for (int k = 0;; ++k) {
+            const hipError_t e = hipStreamQuery(s);
+            if (e == hipSuccess) return FMI_OK;
+            if (e != hipErrorNotReady) return fail(FMI_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+            if (int rc = poll()) {
+                abort();
+                return rc;
+            }
+            if (std::chrono::duration<double>(Clock::now() - t0).count() > timeout_s_) {
+                const int rc = timed_out(what);
+                drain(s, 10.0);  // the aborted transport's kernels end; do not leave them running
+                return rc;
+            }
+            backoff(k);
+        }
+    }
+    // Bounded wait for s (after an abort: never block forever). True if it drained.
+    static bool drain(hipStream_t s, double seconds) {
+        const auto t0 = Clock::now();
+        for (int k = 0;; ++k) {
+            const hipError_t e = hipStreamQuery(s);
+            if (e != hipErrorNotReady) return e == hipSuccess;
+            if (std::chrono::duration<double>(Clock::now() - t0).count() > seconds) return false;
+            backoff(k);
+        }
+    }
+    // What the transport reports about itself (fmi_comm_query).
+    virtual int query(int* count, int* rank, int* device) {
+        *count = n_;
+        *rank = rank_;
+        FMI_COMM_HIP(hipGetDevice(device));
+        return FMI_OK;
+    }
     // recv[j*bytes ...] = rank j's send[rank*bytes ...]
     virtual int all_to_all(const char* send, char* recv, size_t bytes, hipStream_t s) = 0;
     // recv[j*bytes ...] = rank j's send[0 .. bytes)
@@ -201,6 +291,8 @@ public:
 protected:
     int n_;
     int rank_;
+    double timeout_s_ = 300.0;
+    bool aborted_ = false;
 };
 
 // RCCL element type of a dtype; false for the 16-bit integers, which RCCL has no reduction type for.
@@ -227,24 +319,85 @@ ncclRedOp_t nccl_op(int op) {
     }
 }
 
+// An RCCL call of this transport: ncclInProgress (a non-blocking communicator still connecting or enqueuing)
+// is waited out within the timeout, any other failure is returned.
+#define FMI_RCCL(call)                                      \
+    do {                                                    \
+        const int rc_ = ck(api_->call, #call);              \
+        if (rc_ != FMI_OK) return rc_;                      \
+    } while (0)
+
 class RcclTransport final : public Transport {
 public:
-    RcclTransport(const RcclApi* api, ncclComm_t comm, int n, int rank) : Transport(n, rank), api_(api), comm_(comm) {}
+    // nonblocking: the communicator was made with config.blocking = 0 (fmi_comm_init with a librccl that has
+    // ncclCommInitRankConfig / ncclCommGetAsyncError / ncclCommAbort): every wait for the peers is bounded.
+    RcclTransport(const RcclApi* api, ncclComm_t comm, int n, int rank, bool nonblocking)
+        : Transport(n, rank), api_(api), comm_(comm), nonblocking_(nonblocking) {}
     ~RcclTransport() override {
-        (void)api_->CommDestroy(comm_);
         if (token_) (void)hipFree(token_);
+        if (aborted_ || !comm_) return;  // ncclCommAbort released it
+        if (nonblocking_ && api_->CommFinalize) {
+            // flush, bounded: a peer that never arrives must not hang the destructor
+            const ncclResult_t r = api_->CommFinalize(comm_);
+            if ((r != ncclSuccess && r != ncclInProgress) || wait_ready("ncclCommFinalize") != FMI_OK) {
+                abort();
+                return;
+            }
+        }
+        (void)api_->CommDestroy(comm_);
+    }
+
+    // Wait until the communicator has no operation in progress (non-blocking init / connect / enqueue).
+    int wait_ready(const char* what) {
+        if (!nonblocking_) return FMI_OK;
+        const auto t0 = Clock::now();
+        for (int k = 0;; ++k) {
+            ncclResult_t st = ncclSuccess;
+            const ncclResult_t r = api_->CommGetAsyncError(comm_, &st);
+            if (r != ncclSuccess) return nccl_fail(api_, "ncclCommGetAsyncError", r);
+            if (st == ncclSuccess) return FMI_OK;
+            if (st != ncclInProgress) {
+                abort();
+                return fail(FMI_ERR_COMM, std::string(what) + ": " + api_->GetErrorString(st) + " (communicator aborted)");
+            }
+            if (std::chrono::duration<double>(Clock::now() - t0).count() > timeout_s_) return timed_out(what);
+            backoff(k);
+        }
+    }
+    int poll() override {
+        if (!nonblocking_ || aborted_) return FMI_OK;
+        ncclResult_t st = ncclSuccess;
+        if (api_->CommGetAsyncError(comm_, &st) != ncclSuccess) return FMI_OK;
+        if (st == ncclSuccess || st == ncclInProgress) return FMI_OK;
+        return fail(FMI_ERR_COMM, std::string("RCCL asynchronous error: ") + api_->GetErrorString(st) +
+                                      " (communicator aborted)");
+    }
+    void abort() override {
+        if (!aborted_ && api_->CommAbort && comm_) (void)api_->CommAbort(comm_);
+        aborted_ = true;
+    }
+    int query(int* count, int* rank, int* device) override {
+        if (!api_->CommCount || !api_->CommUserRank) return Transport::query(count, rank, device);
+        FMI_RCCL(CommCount(comm_, count));
+        FMI_RCCL(CommUserRank(comm_, rank));
+        if (api_->CommCuDevice) {
+            FMI_RCCL(CommCuDevice(comm_, device));
+        } else {
+            FMI_COMM_HIP(hipGetDevice(device));
+        }
+        return FMI_OK;
     }
 
     int all_to_all(const char* send, char* recv, size_t bytes, hipStream_t s) override {
         if (api_->AllToAll && tune(FMI_TUNE_COMM_A2A) == 0) {
-            FMI_NCCL(api_, AllToAll(send, recv, bytes, ncclUint8, comm_, s));
+            FMI_RCCL(AllToAll(send, recv, bytes, ncclUint8, comm_, s));
             return FMI_OK;
         }
         return run_plan(plan::all_to_all(n_, rank_, bytes), send, recv, s);
     }
     int all_gather(const char* send, char* recv, size_t bytes, hipStream_t s) override {
         if (tune(FMI_TUNE_COMM_GATHER) == 0) {
-            FMI_NCCL(api_, AllGather(send, recv, bytes, ncclUint8, comm_, s));
+            FMI_RCCL(AllGather(send, recv, bytes, ncclUint8, comm_, s));
             return FMI_OK;
         }
         return run_plan(plan::all_gather(n_, rank_, bytes), send, recv, s);  // one link per peer, no ring
@@ -269,32 +422,31 @@ public:
         return run_plan(plan::scatter(n_, rank_, bytes, root), send, recv, s);
     }
     int bcast(char* buf, size_t bytes, int root, hipStream_t s) override {
-        FMI_NCCL(api_, Broadcast(buf, buf, bytes, ncclUint8, root, comm_, s));
+        FMI_RCCL(Broadcast(buf, buf, bytes, ncclUint8, root, comm_, s));
         return FMI_OK;
     }
     int send(const char* buf, size_t bytes, int peer, hipStream_t s) override {
-        FMI_NCCL(api_, Send(buf, bytes, ncclUint8, peer, comm_, s));
+        FMI_RCCL(Send(buf, bytes, ncclUint8, peer, comm_, s));
         return FMI_OK;
     }
     int recv(char* buf, size_t bytes, int peer, hipStream_t s) override {
-        FMI_NCCL(api_, Recv(buf, bytes, ncclUint8, peer, comm_, s));
+        FMI_RCCL(Recv(buf, bytes, ncclUint8, peer, comm_, s));
         return FMI_OK;
     }
     int barrier(hipStream_t s) override {
         if (!token_) FMI_COMM_HIP(hipMalloc(&token_, sizeof(int)));
-        FMI_NCCL(api_, AllReduce(token_, token_, 1, ncclInt32, ncclSum, comm_, s));
-        FMI_COMM_HIP(hipStreamSynchronize(s));
-        return FMI_OK;
+        FMI_RCCL(AllReduce(token_, token_, 1, ncclInt32, ncclSum, comm_, s));
+        return wait_stream(s, "barrier");
     }
     int reduce_scatter(int op, int dtype, const void* send, void* recv, size_t count, hipStream_t s) override {
         ncclDataType_t t;
         if (!nccl_type(dtype, &t)) return fail(FMI_ERR_UNSUPPORTED, "path RCCL: RCCL has no 16-bit integer reductions");
-        FMI_NCCL(api_, ReduceScatter(send, recv, count, t, nccl_op(op), comm_, s));
+        FMI_RCCL(ReduceScatter(send, recv, count, t, nccl_op(op), comm_, s));
         return FMI_OK;
     }
     int barrier_async(hipStream_t s) override {
         if (!token_) FMI_COMM_HIP(hipMalloc(&token_, sizeof(int)));
-        FMI_NCCL(api_, AllReduce(token_, token_, 1, ncclInt32, ncclSum, comm_, s));
+        FMI_RCCL(AllReduce(token_, token_, 1, ncclInt32, ncclSum, comm_, s));
         return FMI_OK;
     }
     // IPC handles travel by all-gather; the peer mappings are opened with lazy peer access (xGMI). A final
@@ -309,9 +461,9 @@ public:
         int flag = 0;
         int rc = [&]() -> int {
             FMI_COMM_HIP(hipMemcpyAsync(d + n_ * H, &mine, H, hipMemcpyHostToDevice, s));
-            FMI_NCCL(api_, AllGather(d + n_ * H, d, H, ncclUint8, comm_, s));
+            FMI_RCCL(AllGather(d + n_ * H, d, H, ncclUint8, comm_, s));
             FMI_COMM_HIP(hipMemcpyAsync(all.data(), d, n_ * H, hipMemcpyDeviceToHost, s));
-            FMI_COMM_HIP(hipStreamSynchronize(s));
+            FMI_COMM_RC(wait_stream(s, "window (handle exchange)"));
             peers.assign(n_, nullptr);
             peers[rank_] = base;
             for (int j = 0; j < n_ && ok; ++j) {
@@ -323,12 +475,12 @@ public:
             int* f = reinterpret_cast<int*>(d + (n_ + 1) * H);
             const int mine_ok = ok ? 1 : 0;
             FMI_COMM_HIP(hipMemcpyAsync(f, &mine_ok, sizeof(int), hipMemcpyHostToDevice, s));
-            FMI_NCCL(api_, AllReduce(f, f + 1, 1, ncclInt32, ncclMin, comm_, s));
+            FMI_RCCL(AllReduce(f, f + 1, 1, ncclInt32, ncclMin, comm_, s));
             FMI_COMM_HIP(hipMemcpyAsync(&flag, f + 1, sizeof(int), hipMemcpyDeviceToHost, s));
-            FMI_COMM_HIP(hipStreamSynchronize(s));
+            FMI_COMM_RC(wait_stream(s, "window (map result)"));
             return FMI_OK;
         }();
-        (void)hipFree(d);
+        if (!aborted_) (void)hipFree(d);  // after an abort the stream may not have drained: leak, never free in use
         if (rc != FMI_OK || flag != 1) {
             unmap_window(peers);
             peers.clear();
@@ -343,8 +495,13 @@ public:
     int split(std::unique_ptr<Transport>* out) override {
         if (!api_->CommSplit) return fail(FMI_ERR_UNSUPPORTED, "librccl lacks ncclCommSplit");
         ncclComm_t nc = nullptr;
-        FMI_NCCL(api_, CommSplit(comm_, 0, rank_, &nc, nullptr));
-        *out = std::make_unique<RcclTransport>(api_, nc, n_, rank_);
+        // a non-blocking parent makes a non-blocking child (config inherited): wait on the child
+        const ncclResult_t r = api_->CommSplit(comm_, 0, rank_, &nc, nullptr);
+        if (r != ncclSuccess && r != ncclInProgress) return nccl_fail(api_, "ncclCommSplit", r);
+        auto child = std::make_unique<RcclTransport>(api_, nc, n_, rank_, nonblocking_);
+        child->set_timeout(timeout_s_);
+        FMI_COMM_RC(child->wait_ready("ncclCommSplit"));
+        *out = std::move(child);
         return FMI_OK;
     }
     int agree_max(int64_t* vals, int k, hipStream_t s) override {
@@ -352,24 +509,29 @@ public:
         FMI_COMM_HIP(hipMalloc(&d, kAgreeMax * sizeof(int64_t)));
         const int rc = [&]() -> int {
             FMI_COMM_HIP(hipMemcpyAsync(d, vals, k * sizeof(int64_t), hipMemcpyHostToDevice, s));
-            FMI_NCCL(api_, AllReduce(d, d, k, ncclInt64, ncclMax, comm_, s));
+            FMI_RCCL(AllReduce(d, d, k, ncclInt64, ncclMax, comm_, s));
             FMI_COMM_HIP(hipMemcpyAsync(vals, d, k * sizeof(int64_t), hipMemcpyDeviceToHost, s));
-            FMI_COMM_HIP(hipStreamSynchronize(s));
-            return FMI_OK;
+            return wait_stream(s, "agree");
         }();
-        (void)hipFree(d);
+        if (!aborted_) (void)hipFree(d);
         return rc;
     }
 
 private:
+    int ck(ncclResult_t r, const char* what) {
+        if (r == ncclSuccess) return FMI_OK;
+        if (r == ncclInProgress) return wait_ready(what);
+        return nccl_fail(api_, what, r);
+    }
+
     // One group of the plan's sends and receives (RCCL pairs them per peer in posting order), then the
     // local part on the stream.
     int run_plan(const plan::Plan& p, const char* send, char* recv, hipStream_t s) {
         if (!p.sends.empty() || !p.recvs.empty()) {
-            FMI_NCCL(api_, GroupStart());
-            for (const plan::Xfer& x : p.sends) FMI_NCCL(api_, Send(send + x.off, x.len, ncclUint8, x.peer, comm_, s));
-            for (const plan::Xfer& x : p.recvs) FMI_NCCL(api_, Recv(recv + x.off, x.len, ncclUint8, x.peer, comm_, s));
-            FMI_NCCL(api_, GroupEnd());
+            FMI_RCCL(GroupStart());
+            for (const plan::Xfer& x : p.sends) FMI_RCCL(Send(send + x.off, x.len, ncclUint8, x.peer, comm_, s));
+            for (const plan::Xfer& x : p.recvs) FMI_RCCL(Recv(recv + x.off, x.len, ncclUint8, x.peer, comm_, s));
+            FMI_RCCL(GroupEnd());
         }
         if (p.copy_len && recv + p.copy_dst != send + p.copy_src)
             FMI_COMM_HIP(hipMemcpyAsync(recv + p.copy_dst, send + p.copy_src, p.copy_len, hipMemcpyDeviceToDevice, s));
@@ -377,6 +539,7 @@ private:
     }
     const RcclApi* api_;
     ncclComm_t comm_;
+    bool nonblocking_;
     void* token_ = nullptr;
 };
 
@@ -396,16 +559,17 @@ struct Hub {
     };
     std::map<std::pair<int, int>, std::deque<Msg*>> box;
 
-    void barrier() {
+    // false: not every rank arrived before the deadline
+    bool barrier(Clock::time_point deadline) {
         std::unique_lock<std::mutex> lk(mu);
         const uint64_t g = generation;
         if (++arrived == n) {
             arrived = 0;
             ++generation;
             cv.notify_all();
-        } else {
-            cv.wait(lk, [&] { return generation != g; });
+            return true;
         }
+        return cv.wait_until(lk, deadline, [&] { return generation != g; });
     }
 };
 
@@ -456,9 +620,20 @@ public:
         FMI_COMM_HIP(hipStreamSynchronize(s));
         Hub::Msg msg{buf, bytes, false};
         std::unique_lock<std::mutex> lk(hub_->mu);
-        hub_->box[{rank_, peer}].push_back(&msg);
+        auto& q = hub_->box[{rank_, peer}];
+        q.push_back(&msg);
         hub_->cv.notify_all();
-        hub_->cv.wait(lk, [&] { return msg.done; });  // rendezvous: the receiver has copied it
+        // rendezvous: the receiver has copied it
+        if (!hub_->cv.wait_until(lk, deadline(), [&] { return msg.done; })) {
+            const auto it = std::find(q.begin(), q.end(), &msg);
+            if (it == q.end()) {  // the receiver took it and is copying: it is alive, let it finish
+                hub_->cv.wait(lk, [&] { return msg.done; });
+                return FMI_OK;
+            }
+            q.erase(it);  // never leave a pointer to this frame behind
+            lk.unlock();
+            return timed_out("local transport send to rank " + std::to_string(peer));
+        }
         return FMI_OK;
     }
     int recv(char* buf, size_t bytes, int peer, hipStream_t s) override {
@@ -466,7 +641,10 @@ public:
         {
             std::unique_lock<std::mutex> lk(hub_->mu);
             auto& q = hub_->box[{peer, rank_}];
-            hub_->cv.wait(lk, [&] { return !q.empty(); });
+            if (!hub_->cv.wait_until(lk, deadline(), [&] { return !q.empty(); })) {
+                lk.unlock();
+                return timed_out("local transport recv from rank " + std::to_string(peer));
+            }
             msg = q.front();
             q.pop_front();
         }
@@ -486,7 +664,7 @@ public:
     }
     int barrier(hipStream_t s) override {
         FMI_COMM_HIP(hipStreamSynchronize(s));
-        hub_->barrier();
+        if (!hub_->barrier(deadline())) return timed_out("local transport barrier");
         return FMI_OK;
     }
     int barrier_async(hipStream_t s) override { return barrier(s); }
@@ -562,7 +740,7 @@ private:
             std::lock_guard<std::mutex> lk(hub_->mu);
             hub_->ptrs[rank_] = mine;
         }
-        hub_->barrier();
+        if (!hub_->barrier(deadline())) return timed_out("local transport exchange (published)");
         std::vector<const char*> all;
         {
             std::lock_guard<std::mutex> lk(hub_->mu);
@@ -570,9 +748,13 @@ private:
         }
         int rc = work(all);
         const hipError_t e = hipStreamSynchronize(s);
-        hub_->barrier();
+        if (!hub_->barrier(deadline())) return timed_out("local transport exchange (consumed)");
         if (rc == FMI_OK && e != hipSuccess) rc = hip_err("local transport exchange", e);
         return rc;
+    }
+
+    Clock::time_point deadline() const {
+        return Clock::now() + std::chrono::duration_cast<Clock::duration>(std::chrono::duration<double>(timeout_s_));
     }
 
     std::shared_ptr<Hub> hub_;
@@ -832,21 +1014,15 @@ private:
         return wait_until([&] { return ctrl_->generation.load(std::memory_order_acquire) != g; }, what);
     }
 
-    // Spin, then back off to short sleeps; give up after FMI_PROC_TIMEOUT_S (default 300 s) so a dead
-    // peer surfaces as an error instead of a hang.
+    // Spin, then back off to short sleeps; give up after the communicator's timeout (FMI_COMM_TIMEOUT_S /
+    // FMI_PROC_TIMEOUT_S, default 300 s) so a dead peer surfaces as FMI_ERR_TIMEOUT instead of a hang.
     template <class Pred>
     int wait_until(Pred&& ready, const char* what) {
-        static const double limit = [] {
-            const char* e = std::getenv("FMI_PROC_TIMEOUT_S");
-            return e ? std::atof(e) : 300.0;
-        }();
-        const auto t0 = std::chrono::steady_clock::now();
+        const auto t0 = Clock::now();
         for (int k = 0; !ready(); ++k) {
-            if (k < 1000) continue;
-            std::this_thread::sleep_for(std::chrono::microseconds(k < 10000 ? 5 : 200));
-            if ((k & 255) == 0 &&
-                std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > limit)
-                return fail(FMI_ERR_COMM, std::string("PROC transport: timed out waiting for peers (") + what + ")");
+            backoff(k);
+            if (k >= 1000 && (k & 255) == 0 && std::chrono::duration<double>(Clock::now() - t0).count() > timeout_s_)
+                return timed_out(std::string("PROC transport: waiting for peers (") + what + ")");
         }
         return FMI_OK;
     }
@@ -901,13 +1077,16 @@ struct Window {
 struct ChunkPipe {
     std::unique_ptr<Transport> t2;  // nullptr with LOCAL / PROC: their exchanges are host-synchronous
     bool split_done = false;
+    bool no_split = false;  // the transport cannot split (librccl without ncclCommSplit): never pipeline
     hipStream_t gs = nullptr;  // all-gathers
     hipEvent_t reduced[2] = {}, gathered[2] = {}, start = nullptr;
     bool ready = false;
 
     int init(Transport* t) {
         if (!split_done) {
-            FMI_COMM_RC(t->split(&t2));
+            const int rc = t->split(&t2);
+            if (rc == FMI_ERR_UNSUPPORTED) no_split = true;  // every rank loads the same librccl: all fall back
+            if (rc != FMI_OK) return rc;
             split_done = true;
         }
         if (ready) return FMI_OK;
@@ -976,6 +1155,28 @@ struct Comm {
     std::map<char*, Window> windows;  // keyed by this rank's base
 
     ~Comm() {
+        if (t && t->aborted()) {
+            // A timed-out or failed communicator: no peer is waited for again. Its device memory may still
+            // be referenced by work that never drained: free only if everything drained within a bound,
+            // otherwise leak it (and the streams) rather than free memory a kernel may still touch.
+            bool drained = Transport::drain(library_stream(), 10.0);
+            for (hipStream_t st : {pipe.cs, pipe.h2d, pipe.d2h, chunks.gs})
+                if (st) drained = Transport::drain(st, 10.0) && drained;
+            if (!drained) {
+                pipe.cs = pipe.h2d = pipe.d2h = chunks.gs = nullptr;
+                for (void*& b : buf) b = nullptr;
+                windows.clear();
+                return;
+            }
+            for (void* b : buf)
+                if (b) (void)hipFree(b);
+            for (auto& [base, w] : windows) {
+                t->unmap_window(w.peers);
+                if (w.shards) (void)hipFree(w.shards);
+                (void)hipFree(base);
+            }
+            return;
+        }
         if (pipe.cs) (void)hipStreamSynchronize(pipe.cs);
         if (chunks.gs) (void)hipStreamSynchronize(chunks.gs);
         // Windows are read by the peers: wait until every rank is done with them (communicators are torn
@@ -1027,11 +1228,16 @@ size_t shard_elems(size_t n, int ranks) {
     return (per + kShardAlign - 1) / kShardAlign * kShardAlign;
 }
 
+int aborted_error() {
+    return fail(FMI_ERR_COMM, "communicator was aborted (a timeout or a transport error); destroy it");
+}
+
 int check_common(fmi_comm_t comm, int op, int dtype) {
     if (!comm) return fail(FMI_ERR_INVALID, "null communicator");
     if (op < FMI_OP_SUM || op > FMI_OP_MIN) return fail(FMI_ERR_INVALID, "unknown op " + std::to_string(op));
     if (dtype_size(dtype) == 0) return fail(FMI_ERR_INVALID, "unknown dtype " + std::to_string(dtype));
     if (!library_stream()) return fail(FMI_ERR_NO_DEVICE, "fmi_dev_init has not been called");
+    if (static_cast<Comm*>(comm)->t->aborted()) return aborted_error();
     return FMI_OK;
 }
 
@@ -1216,9 +1422,14 @@ int allreduce_device(Comm* c, int op, int dtype, int alg, int path, const void* 
     }
     if (path == FMI_PATH_TREE && !per_rank) {
         const long long K = tune(FMI_TUNE_COMM_PIPELINE);
-        // worth it only for chunks of at least 1 MiB per rank
-        if (K >= 2 && n * esz / static_cast<size_t>(K) >= (size_t(1) << 20) * static_cast<size_t>(N))
-            return allreduce_tree_pipelined(c, op, dtype, alg, send, recv, n, s, static_cast<size_t>(K));
+        // worth it only for chunks of at least 1 MiB per rank; without a second communicator the unpipelined
+        // path below runs (same bits)
+        if (K >= 2 && n * esz / static_cast<size_t>(K) >= (size_t(1) << 20) * static_cast<size_t>(N) &&
+            !c->chunks.no_split) {
+            const int rc = c->chunks.init(c->t.get());
+            if (rc == FMI_OK) return allreduce_tree_pipelined(c, op, dtype, alg, send, recv, n, s, static_cast<size_t>(K));
+            if (rc != FMI_ERR_UNSUPPORTED) return rc;
+        }
     }
     const size_t shard = shard_elems(n, N);
     const size_t padded = shard * N;
@@ -1284,6 +1495,8 @@ int allreduce_device(Comm* c, int op, int dtype, int alg, int path, const void* 
     return FMI_OK;
 }
 
+int comm_init(fmi_comm_t* comm, const void* id, int nranks, int rank, double timeout_s);
+
 int check_allreduce_args(int alg, int path) {
     if (alg != FMI_ALG_ALLREDUCE && alg != FMI_ALG_REDUCE_LTR)
         return fail(FMI_ERR_INVALID, "allreduce: alg must be ALLREDUCE or REDUCE_LTR");
@@ -1301,7 +1514,7 @@ using namespace fmi::dev;
 
 extern "C" {
 
-int fmi_comm_unique_id(int transport, void* id, size_t len) {
+static int comm_unique_id_impl(int transport, void* id, size_t len) {
     if (!id || len < FMI_COMM_ID_BYTES) return fail(FMI_ERR_INVALID, "id buffer must hold FMI_COMM_ID_BYTES");
     std::memset(id, 0, FMI_COMM_ID_BYTES);
     if (transport == FMI_TRANSPORT_LOCAL) {
@@ -1328,6 +1541,19 @@ int fmi_comm_unique_id(int transport, void* id, size_t len) {
 }
 
 int fmi_comm_init(fmi_comm_t* comm, const void* id, int nranks, int rank) {
+    return fmi_comm_init_timeout(comm, id, nranks, rank, 0.0);
+}
+
+int fmi_comm_init_timeout(fmi_comm_t* comm, const void* id, int nranks, int rank, double timeout_s) {
+    return guarded("fmi_comm_init", [&] { return comm_init(comm, id, nranks, rank, timeout_s); });
+}
+
+}  // extern "C"
+
+namespace fmi::dev {
+namespace {
+
+int comm_init(fmi_comm_t* comm, const void* id, int nranks, int rank, double timeout_s) {
     if (!comm || !id) return fail(FMI_ERR_INVALID, "null argument");
     if (nranks < 1 || rank < 0 || rank >= nranks) return fail(FMI_ERR_INVALID, "rank out of range");
     if (nranks > fmi::sched::kMaxPeers)  // value ids of a P = nranks program must fit 31 bits
@@ -1347,8 +1573,10 @@ int fmi_comm_init(fmi_comm_t* comm, const void* id, int nranks, int rank) {
         }
         if (hub->n != nranks) return fail(FMI_ERR_INVALID, "local communicator joined with a different size");
         c->t = std::make_unique<LocalTransport>(hub, nranks, rank);
+        c->t->set_timeout(timeout_s > 0 ? timeout_s : default_timeout_s(false));
     } else if (std::memcmp(id, kProcMagic, 8) == 0) {
         auto t = std::make_unique<ProcTransport>(nranks, rank);
+        t->set_timeout(timeout_s > 0 ? timeout_s : default_timeout_s(true));
         FMI_COMM_RC(t->join(id));
         c->t = std::move(t);
     } else {
@@ -1357,12 +1585,37 @@ int fmi_comm_init(fmi_comm_t* comm, const void* id, int nranks, int rank) {
         ncclUniqueId uid;
         std::memcpy(&uid, id, FMI_COMM_ID_BYTES);
         ncclComm_t nc = nullptr;
-        FMI_NCCL(api, CommInitRank(&nc, nranks, uid, rank));
-        c->t = std::make_unique<RcclTransport>(api, nc, nranks, rank);
+        const double limit = timeout_s > 0 ? timeout_s : default_timeout_s(false);
+        // Non-blocking init, polled against the timeout (a peer that never joins ends in FMI_ERR_TIMEOUT and
+        // ncclCommAbort, not a hang). FMI_COMM_BLOCKING=1, or a librccl without the config / async-error /
+        // abort entry points, takes the blocking ncclCommInitRank (unbounded).
+        const char* blocking = std::getenv("FMI_COMM_BLOCKING");
+        if (api->bounded() && !(blocking && blocking[0] == '1')) {
+            ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+            cfg.blocking = 0;
+            const ncclResult_t r = api->CommInitRankConfig(&nc, nranks, uid, rank, &cfg);
+            if (r != ncclSuccess && r != ncclInProgress) {
+                if (nc) (void)api->CommAbort(nc);
+                return nccl_fail(api, "ncclCommInitRankConfig", r);
+            }
+            auto t = std::make_unique<RcclTransport>(api, nc, nranks, rank, true);
+            t->set_timeout(limit);
+            FMI_COMM_RC(t->wait_ready("ncclCommInitRankConfig (waiting for every rank to join)"));
+            c->t = std::move(t);
+        } else {
+            FMI_NCCL(api, CommInitRank(&nc, nranks, uid, rank));
+            c->t = std::make_unique<RcclTransport>(api, nc, nranks, rank, false);
+            c->t->set_timeout(limit);
+        }
     }
     *comm = c.release();
     return FMI_OK;
 }
+
+}  // namespace
+}  // namespace fmi::dev
+
+extern "C" {
 
 int fmi_comm_destroy(fmi_comm_t comm) {
     delete static_cast<Comm*>(comm);
@@ -1377,42 +1630,53 @@ int fmi_comm_size(fmi_comm_t comm, int* nranks, int* rank) {
     return FMI_OK;
 }
 
-int fmi_comm_window_alloc(fmi_comm_t comm, size_t bytes, void** ptr) {
+static int comm_window_alloc_impl(fmi_comm_t comm, size_t bytes, void** ptr) {
     if (!comm || !ptr) return fail(FMI_ERR_INVALID, "null argument");
     if (!library_stream()) return fail(FMI_ERR_NO_DEVICE, "fmi_dev_init has not been called");
     Comm* c = static_cast<Comm*>(comm);
     std::lock_guard<std::mutex> lk(c->mu);
+    if (c->t->aborted()) return aborted_error();
     bytes = std::max<size_t>(256, (bytes + 255) / 256 * 256);
+    const int N = c->t->n();
+    // Everything this rank needs is allocated BEFORE the collective mapping and its success goes into the
+    // mapping's all-or-nothing flag; the table fill after it is agreed on by every rank too, so either every
+    // rank holds the window or every rank has released it (no peer keeps a mapping of a freed base).
     char* base = nullptr;
-    const bool ok = hipMalloc(&base, 2 * bytes) == hipSuccess;
     Window w;
     w.bytes = bytes;
-    const int rc = c->t->map_window(ok ? base : nullptr, ok, w.peers, library_stream());
-    if (rc != FMI_OK) {
+    bool ok = hipMalloc(&base, 2 * bytes) == hipSuccess;
+    ok = ok && hipMalloc(&w.shards, static_cast<size_t>(N) * sizeof(char*)) == hipSuccess;
+    auto release = [&] {
+        if (w.shards) (void)hipFree(w.shards);
         if (base) (void)hipFree(base);
+    };
+    int rc = c->t->map_window(ok ? base : nullptr, ok, w.peers, library_stream());
+    if (rc != FMI_OK) {
+        release();
         return rc;
     }
-    // The gather's table of reduced-shard areas (any number of ranks). A failure here is local, after the
-    // collective mapping succeeded everywhere: this rank fails; the peers still hold a usable window.
     std::vector<char*> table(w.peers.size());
     for (size_t j = 0; j < table.size(); ++j) table[j] = w.peers[j] + bytes;
-    hipError_t e = hipMalloc(&w.shards, table.size() * sizeof(char*));
-    if (e == hipSuccess) e = hipMemcpy(w.shards, table.data(), table.size() * sizeof(char*), hipMemcpyHostToDevice);
-    if (e != hipSuccess) {
-        if (w.shards) (void)hipFree(w.shards);
+    const hipError_t e = hipMemcpy(w.shards, table.data(), table.size() * sizeof(char*), hipMemcpyHostToDevice);
+    int64_t failed[1] = {e == hipSuccess ? 0 : 1};
+    rc = c->t->agree_max(failed, 1, library_stream());
+    if (rc != FMI_OK || failed[0] != 0) {
         c->t->unmap_window(w.peers);
-        (void)hipFree(base);
-        return fail(FMI_ERR_ALLOC, std::string("window shard table: ") + hipGetErrorString(e));
+        release();
+        if (rc != FMI_OK) return rc;
+        return fail(FMI_ERR_ALLOC, e != hipSuccess ? std::string("window shard table: ") + hipGetErrorString(e)
+                                                   : std::string("window shard table: failed on another rank"));
     }
     c->windows[base] = std::move(w);
     *ptr = base;
     return FMI_OK;
 }
 
-int fmi_comm_window_free(fmi_comm_t comm, void* ptr) {
+static int comm_window_free_impl(fmi_comm_t comm, void* ptr) {
     if (!comm || !ptr) return fail(FMI_ERR_INVALID, "null argument");
     Comm* c = static_cast<Comm*>(comm);
     std::lock_guard<std::mutex> lk(c->mu);
+    if (c->t->aborted()) return aborted_error();  // the window goes with the communicator
     auto it = c->windows.find(static_cast<char*>(ptr));
     if (it == c->windows.end()) return fail(FMI_ERR_INVALID, "not a window of this communicator");
     // No peer may still be reading it, and this rank must be done reading the peers' windows: a path
@@ -1454,7 +1718,7 @@ int fmi_comm_timing_read(fmi_comm_t comm, float* total_ms, int* launches) {
     return FMI_OK;
 }
 
-int fmi_comm_allreduce(fmi_comm_t comm, int op, int dtype, int alg, int path, const void* send, void* recv, size_t n,
+static int comm_allreduce_impl(fmi_comm_t comm, int op, int dtype, int alg, int path, const void* send, void* recv, size_t n,
                        fmi_stream_t stream) {
     FMI_COMM_RC(check_common(comm, op, dtype));
     FMI_COMM_RC(check_allreduce_args(alg, path));
@@ -1469,7 +1733,7 @@ int fmi_comm_allreduce(fmi_comm_t comm, int op, int dtype, int alg, int path, co
 // pipe.h2d and chunk k-1 drains on pipe.d2h. Slot reuse is ordered by events: a load into slot j waits
 // until the allreduce that read it has finished (reduced), an allreduce into slot j waits until the
 // previous result in it has drained to the host.
-int fmi_comm_allreduce_host(fmi_comm_t comm, int op, int dtype, int alg, int path, const void* send, void* recv,
+static int comm_allreduce_host_impl(fmi_comm_t comm, int op, int dtype, int alg, int path, const void* send, void* recv,
                             size_t n, size_t chunk) {
     FMI_COMM_RC(check_common(comm, op, dtype));
     FMI_COMM_RC(check_allreduce_args(alg, path));
@@ -1515,12 +1779,11 @@ int fmi_comm_allreduce_host(fmi_comm_t comm, int op, int dtype, int alg, int pat
         FMI_COMM_HIP(hipMemcpyAsync(dst + k * chunk * esz, out[j], span(k) * esz, hipMemcpyDefault, p.d2h));
         FMI_COMM_HIP(hipEventRecord(p.drained[j], p.d2h));
     }
-    FMI_COMM_HIP(hipStreamSynchronize(p.d2h));
-    FMI_COMM_HIP(hipStreamSynchronize(p.cs));
-    return FMI_OK;
+    FMI_COMM_RC(c->t->wait_stream(p.d2h, "fmi_comm_allreduce_host"));
+    return c->t->wait_stream(p.cs, "fmi_comm_allreduce_host");
 }
 
-int fmi_comm_reduce(fmi_comm_t comm, int op, int dtype, int alg, const void* send, void* recv, size_t n, int root,
+static int comm_reduce_impl(fmi_comm_t comm, int op, int dtype, int alg, const void* send, void* recv, size_t n, int root,
                     fmi_stream_t stream) {
     FMI_COMM_RC(check_common(comm, op, dtype));
     if (alg != FMI_ALG_REDUCE && alg != FMI_ALG_REDUCE_LTR)
@@ -1569,9 +1832,9 @@ int fmi_comm_reduce(fmi_comm_t comm, int op, int dtype, int alg, const void* sen
 // kReducePartials kernel: N reads, N writes) -> all-to-all back into each rank's `send`; the root then
 // copies its value (the result) into recv. reduce_ltr leaves every sendbuf intact (:44-57), so it is the
 // plain reduce.
-int fmi_comm_reduce_sendbuf(fmi_comm_t comm, int op, int dtype, int alg, void* send, void* recv, size_t n, int root,
+static int comm_reduce_sendbuf_impl(fmi_comm_t comm, int op, int dtype, int alg, void* send, void* recv, size_t n, int root,
                             fmi_stream_t stream) {
-    if (alg == FMI_ALG_REDUCE_LTR) return fmi_comm_reduce(comm, op, dtype, alg, send, recv, n, root, stream);
+    if (alg == FMI_ALG_REDUCE_LTR) return comm_reduce_impl(comm, op, dtype, alg, send, recv, n, root, stream);
     FMI_COMM_RC(check_common(comm, op, dtype));
     if (alg != FMI_ALG_REDUCE) return fail(FMI_ERR_INVALID, "reduce: alg must be REDUCE or REDUCE_LTR");
     Comm* c = static_cast<Comm*>(comm);
@@ -1624,7 +1887,7 @@ int fmi_comm_reduce_sendbuf(fmi_comm_t comm, int op, int dtype, int alg, void* s
     return FMI_OK;
 }
 
-int fmi_comm_scan(fmi_comm_t comm, int op, int dtype, int alg, const void* send, void* recv, size_t n,
+static int comm_scan_impl(fmi_comm_t comm, int op, int dtype, int alg, const void* send, void* recv, size_t n,
                   fmi_stream_t stream) {
     FMI_COMM_RC(check_common(comm, op, dtype));
     if (alg != FMI_ALG_SCAN && alg != FMI_ALG_SCAN_LTR) return fail(FMI_ERR_INVALID, "scan: alg must be SCAN or SCAN_LTR");
@@ -1675,41 +1938,126 @@ int fmi_comm_scan(fmi_comm_t comm, int op, int dtype, int alg, const void* send,
     if (!library_stream()) return fail(FMI_ERR_NO_DEVICE, "fmi_dev_init has not been called"); \
     Comm* c = static_cast<Comm*>(comm);                                           \
     std::lock_guard<std::mutex> lk(c->mu);                                        \
+    if (c->t->aborted()) return aborted_error();                                  \
     hipStream_t s = resolve_stream(stream);
 
-int fmi_comm_bcast(fmi_comm_t comm, void* buf, size_t bytes, int root, fmi_stream_t stream) {
+static int comm_bcast_impl(fmi_comm_t comm, void* buf, size_t bytes, int root, fmi_stream_t stream) {
     FMI_COMM_PRELUDE();
     if (root < 0 || root >= c->t->n()) return fail(FMI_ERR_INVALID, "root out of range");
     return c->t->bcast(static_cast<char*>(buf), bytes, root, s);
 }
 
-int fmi_comm_gather(fmi_comm_t comm, const void* send, void* recv, size_t bytes, int root, fmi_stream_t stream) {
+static int comm_gather_impl(fmi_comm_t comm, const void* send, void* recv, size_t bytes, int root, fmi_stream_t stream) {
     FMI_COMM_PRELUDE();
     if (root < 0 || root >= c->t->n()) return fail(FMI_ERR_INVALID, "root out of range");
     return c->t->gather(static_cast<const char*>(send), static_cast<char*>(recv), bytes, root, s);
 }
 
-int fmi_comm_scatter(fmi_comm_t comm, const void* send, void* recv, size_t bytes, int root, fmi_stream_t stream) {
+static int comm_scatter_impl(fmi_comm_t comm, const void* send, void* recv, size_t bytes, int root, fmi_stream_t stream) {
     FMI_COMM_PRELUDE();
     if (root < 0 || root >= c->t->n()) return fail(FMI_ERR_INVALID, "root out of range");
     return c->t->scatter(static_cast<const char*>(send), static_cast<char*>(recv), bytes, root, s);
 }
 
-int fmi_comm_send(fmi_comm_t comm, const void* buf, size_t bytes, int peer, fmi_stream_t stream) {
+static int comm_send_impl(fmi_comm_t comm, const void* buf, size_t bytes, int peer, fmi_stream_t stream) {
     FMI_COMM_PRELUDE();
     if (peer < 0 || peer >= c->t->n()) return fail(FMI_ERR_INVALID, "peer out of range");
     return c->t->send(static_cast<const char*>(buf), bytes, peer, s);
 }
 
-int fmi_comm_recv(fmi_comm_t comm, void* buf, size_t bytes, int peer, fmi_stream_t stream) {
+static int comm_recv_impl(fmi_comm_t comm, void* buf, size_t bytes, int peer, fmi_stream_t stream) {
     FMI_COMM_PRELUDE();
     if (peer < 0 || peer >= c->t->n()) return fail(FMI_ERR_INVALID, "peer out of range");
     return c->t->recv(static_cast<char*>(buf), bytes, peer, s);
 }
 
-int fmi_comm_barrier(fmi_comm_t comm, fmi_stream_t stream) {
+static int comm_barrier_impl(fmi_comm_t comm, fmi_stream_t stream) {
     FMI_COMM_PRELUDE();
     return c->t->barrier(s);
+}
+
+
+// ---- entry points: no C++ exception crosses the C-ABI (guarded) ----
+int fmi_comm_window_alloc(fmi_comm_t comm, size_t bytes, void** ptr) {
+    return guarded("fmi_comm_window_alloc", [&] { return comm_window_alloc_impl(comm, bytes, ptr); });
+}
+
+int fmi_comm_window_free(fmi_comm_t comm, void* ptr) {
+    return guarded("fmi_comm_window_free", [&] { return comm_window_free_impl(comm, ptr); });
+}
+
+int fmi_comm_allreduce(fmi_comm_t comm, int op, int dtype, int alg, int path, const void* send, void* recv, size_t n,
+                       fmi_stream_t stream) {
+    return guarded("fmi_comm_allreduce", [&] { return comm_allreduce_impl(comm, op, dtype, alg, path, send, recv, n, stream); });
+}
+
+int fmi_comm_allreduce_host(fmi_comm_t comm, int op, int dtype, int alg, int path, const void* send, void* recv,
+                            size_t n, size_t chunk) {
+    return guarded("fmi_comm_allreduce_host", [&] { return comm_allreduce_host_impl(comm, op, dtype, alg, path, send, recv, n, chunk); });
+}
+
+int fmi_comm_reduce(fmi_comm_t comm, int op, int dtype, int alg, const void* send, void* recv, size_t n, int root,
+                    fmi_stream_t stream) {
+    return guarded("fmi_comm_reduce", [&] { return comm_reduce_impl(comm, op, dtype, alg, send, recv, n, root, stream); });
+}
+
+int fmi_comm_reduce_sendbuf(fmi_comm_t comm, int op, int dtype, int alg, void* send, void* recv, size_t n, int root,
+                            fmi_stream_t stream) {
+    return guarded("fmi_comm_reduce_sendbuf", [&] { return comm_reduce_sendbuf_impl(comm, op, dtype, alg, send, recv, n, root, stream); });
+}
+
+int fmi_comm_scan(fmi_comm_t comm, int op, int dtype, int alg, const void* send, void* recv, size_t n,
+                  fmi_stream_t stream) {
+    return guarded("fmi_comm_scan", [&] { return comm_scan_impl(comm, op, dtype, alg, send, recv, n, stream); });
+}
+
+int fmi_comm_bcast(fmi_comm_t comm, void* buf, size_t bytes, int root, fmi_stream_t stream) {
+    return guarded("fmi_comm_bcast", [&] { return comm_bcast_impl(comm, buf, bytes, root, stream); });
+}
+
+int fmi_comm_gather(fmi_comm_t comm, const void* send, void* recv, size_t bytes, int root, fmi_stream_t stream) {
+    return guarded("fmi_comm_gather", [&] { return comm_gather_impl(comm, send, recv, bytes, root, stream); });
+}
+
+int fmi_comm_scatter(fmi_comm_t comm, const void* send, void* recv, size_t bytes, int root, fmi_stream_t stream) {
+    return guarded("fmi_comm_scatter", [&] { return comm_scatter_impl(comm, send, recv, bytes, root, stream); });
+}
+
+int fmi_comm_send(fmi_comm_t comm, const void* buf, size_t bytes, int peer, fmi_stream_t stream) {
+    return guarded("fmi_comm_send", [&] { return comm_send_impl(comm, buf, bytes, peer, stream); });
+}
+
+int fmi_comm_recv(fmi_comm_t comm, void* buf, size_t bytes, int peer, fmi_stream_t stream) {
+    return guarded("fmi_comm_recv", [&] { return comm_recv_impl(comm, buf, bytes, peer, stream); });
+}
+
+int fmi_comm_barrier(fmi_comm_t comm, fmi_stream_t stream) {
+    return guarded("fmi_comm_barrier", [&] { return comm_barrier_impl(comm, stream); });
+}
+
+int fmi_comm_unique_id(int transport, void* id, size_t len) {
+    return guarded("fmi_comm_unique_id", [&] { return comm_unique_id_impl(transport, id, len); });
+}
+
+int fmi_comm_sync(fmi_comm_t comm, fmi_stream_t stream) {
+    return guarded("fmi_comm_sync", [&]() -> int {
+        if (!comm) return fail(FMI_ERR_INVALID, "null communicator");
+        if (!library_stream()) return fail(FMI_ERR_NO_DEVICE, "fmi_dev_init has not been called");
+        Comm* c = static_cast<Comm*>(comm);
+        std::lock_guard<std::mutex> lk(c->mu);
+        if (c->t->aborted()) return aborted_error();
+        return c->t->wait_stream(resolve_stream(stream), "fmi_comm_sync");
+    });
+}
+
+int fmi_comm_query(fmi_comm_t comm, int* count, int* rank, int* device) {
+    return guarded("fmi_comm_query", [&]() -> int {
+        if (!comm || !count || !rank || !device) return fail(FMI_ERR_INVALID, "null argument");
+        Comm* c = static_cast<Comm*>(comm);
+        std::lock_guard<std::mutex> lk(c->mu);
+        if (c->t->aborted()) return aborted_error();
+        return c->t->query(count, rank, device);
+    });
 }
 
 }  // extern "C"

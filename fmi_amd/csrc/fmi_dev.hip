@@ -171,6 +171,13 @@ int launch_combine(int op, int dtype, void* out, const void* a, const void* b, s
 // has drained; the caller records g_state.arena_free on s after its last launch touching the arena.
 // ----------------------------------------------------------------------------------------------------
 int arena_acquire(size_t need, hipStream_t s) {
+    // The arena is ordered by an event recorded outside any graph: a captured call would record arena_free
+    // inside the graph, and its replays would write the arena unordered against later direct calls.
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    FMI_HIP_TRY(hipStreamIsCapturing(s, &cap));
+    if (cap != hipStreamCaptureStatusNone)
+        return fail(FMI_ERR_UNSUPPORTED, "this call needs the library's scratch arena (unaligned or 8/16-bit buckets, "
+                                         "or a P-way program beyond the fused kernels) and cannot be captured in a graph");
     if (!g_state.arena_free) FMI_HIP_TRY(hipEventCreateWithFlags(&g_state.arena_free, hipEventDisableTiming));
     if (g_state.arena_bytes < need) {
         FMI_HIP_TRY(hipEventSynchronize(g_state.arena_free));  // previous users have drained
@@ -803,6 +810,17 @@ int fmi_dev_describe(char* buf, size_t len) {
     return FMI_OK;
 }
 
+int fmi_dev_pci_bus_id(int device, char* buf, size_t len) {
+    if (!buf || len == 0) return fail(FMI_ERR_INVALID, "null buffer");
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || device < 0 || device >= count)
+        return fail(FMI_ERR_NO_DEVICE, "no device " + std::to_string(device));
+    char id[64] = {};
+    FMI_HIP_TRY(hipDeviceGetPCIBusId(id, sizeof(id), device));
+    std::snprintf(buf, len, "%s", id);
+    return FMI_OK;
+}
+
 // ---- memory ----------------------------------------------------------------------------------------
 int fmi_dev_alloc(void** ptr, size_t bytes) {
     if (!ptr) return fail(FMI_ERR_INVALID, "ptr is null");
@@ -1052,8 +1070,8 @@ int fmi_dev_combine(int op, int dtype, void* out, const void* a, const void* b, 
     return launch_combine(op, dtype, out, a, b, n, resolve(stream));
 }
 
-int fmi_dev_reduce_tree(int op, int dtype, int alg, void* out, const void* const* ins, int P, int rank, size_t n,
-                        fmi_stream_t stream) {
+static int reduce_tree_impl(int op, int dtype, int alg, void* out, const void* const* ins, int P, int rank, size_t n,
+                            fmi_stream_t stream) {
     if (int rc = check_peer_args(op, dtype, P)) return rc;
     if (alg != FMI_ALG_ALLREDUCE && alg != FMI_ALG_REDUCE && alg != FMI_ALG_REDUCE_LTR)
         return fail(FMI_ERR_INVALID, "fmi_dev_reduce_tree: alg must be ALLREDUCE, REDUCE or REDUCE_LTR");
@@ -1088,8 +1106,8 @@ int fmi_dev_reduce_tree(int op, int dtype, int alg, void* out, const void* const
     return run_program_stepwise(op, dtype, prog, outs, 1, &value, order.data(), n, s);
 }
 
-int fmi_dev_scan_peers(int op, int dtype, int alg, void* const* outs, const void* const* ins, int P, size_t n,
-                       fmi_stream_t stream) {
+static int scan_peers_impl(int op, int dtype, int alg, void* const* outs, const void* const* ins, int P, size_t n,
+                           fmi_stream_t stream) {
     if (int rc = check_peer_args(op, dtype, P)) return rc;
     if (alg != FMI_ALG_SCAN && alg != FMI_ALG_SCAN_LTR)
         return fail(FMI_ERR_INVALID, "fmi_dev_scan_peers: alg must be SCAN or SCAN_LTR");
@@ -1215,7 +1233,7 @@ int fmi_dev_fill_synthetic(int dtype, void* buf, size_t n, uint64_t seed, uint32
     return fmi_dev_fill_synthetic_at(dtype, buf, n, seed, peer, 0, stream);
 }
 
-int fmi_schedule_expr(int alg, int P, int rank, char* buf, size_t len) {
+static int schedule_expr_impl(int alg, int P, int rank, char* buf, size_t len) {
     if (!buf || len == 0) return fail(FMI_ERR_INVALID, "null buffer");
     if (P < 1 || P > sched::kMaxPeers) return fail(FMI_ERR_INVALID, "P out of range");
     if (rank < 0 || rank >= P) return fail(FMI_ERR_INVALID, "rank out of range");
@@ -1226,6 +1244,20 @@ int fmi_schedule_expr(int alg, int P, int rank, char* buf, size_t len) {
     if (e.size() + 1 > len) return fail(FMI_ERR_INVALID, "buffer too small (" + std::to_string(e.size() + 1) + " needed)");
     std::memcpy(buf, e.c_str(), e.size() + 1);
     return FMI_OK;
+}
+
+int fmi_dev_reduce_tree(int op, int dtype, int alg, void* out, const void* const* ins, int P, int rank, size_t n,
+                        fmi_stream_t stream) {
+    return guarded("fmi_dev_reduce_tree", [&] { return reduce_tree_impl(op, dtype, alg, out, ins, P, rank, n, stream); });
+}
+
+int fmi_dev_scan_peers(int op, int dtype, int alg, void* const* outs, const void* const* ins, int P, size_t n,
+                       fmi_stream_t stream) {
+    return guarded("fmi_dev_scan_peers", [&] { return scan_peers_impl(op, dtype, alg, outs, ins, P, n, stream); });
+}
+
+int fmi_schedule_expr(int alg, int P, int rank, char* buf, size_t len) {
+    return guarded("fmi_schedule_expr", [&] { return schedule_expr_impl(alg, P, rank, buf, len); });
 }
 
 int fmi_tune_set(int key, long long value) {

@@ -5,6 +5,8 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <exception>
+#include <new>
 #include <string>
 
 #include "../../include/fmi_dev.h"
@@ -14,6 +16,22 @@ namespace fmi::dev {
 
 // Records a failure message for fmi_last_error() and returns `code`.
 int fail(int code, const std::string& msg);
+
+// Runs a C-ABI entry point's body: no C++ exception may cross the extern "C" boundary (it would call
+// std::terminate in the caller). std::bad_alloc (e.g. a host program or expression for millions of peers)
+// becomes FMI_ERR_ALLOC, anything else FMI_ERR_INVALID, with the message for fmi_last_error().
+template <class F>
+int guarded(const char* what, F&& body) noexcept {
+    try {
+        return body();
+    } catch (const std::bad_alloc&) {
+        return fail(FMI_ERR_ALLOC, std::string(what) + ": out of host memory");
+    } catch (const std::exception& e) {
+        return fail(FMI_ERR_INVALID, std::string(what) + ": " + e.what());
+    } catch (...) {
+        return fail(FMI_ERR_INVALID, std::string(what) + ": unknown exception");
+    }
+}
 
 // The library's default stream (what a NULL fmi_stream_t means); nullptr before fmi_dev_init.
 hipStream_t library_stream();

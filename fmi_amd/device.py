@@ -123,6 +123,13 @@ def describe() -> str:
     return buf.value.decode()
 
 
+def pci_bus_id(device: int) -> str:
+    """PCI bus id of a visible device ("dddd:bb:dd.f")."""
+    buf = ctypes.create_string_buffer(64)
+    _lib.call("fmi_dev_pci_bus_id", int(device), buf, len(buf))
+    return buf.value.decode()
+
+
 class Bucket:
     """A device-resident bucket of `n` elements of `dtype` (owns its HBM allocation unless `view`)."""
 

@@ -37,8 +37,9 @@ from .comm import Comm, Transport, unique_id
 from .device import Alg, Bucket, Op
 
 
-class Timeout(Exception):
-    """Mirrors FMI::Utils::Timeout (reference include/utils/Common.h:11-15)."""
+# FMI::Utils::Timeout (reference include/utils/Common.h:11-15): raised when the communicator id does not
+# appear in time and by every device wait the communicator bounds (FMI_ERR_TIMEOUT; "max_timeout" ms).
+Timeout = _lib.Timeout
 
 
 class datatypes(enum.IntEnum):  # noqa: N801 - reference spelling (python/fmi_python.cpp:28-33)
@@ -124,7 +125,7 @@ class Communicator:
         self._id_path = os.path.join(params.get("rendezvous_dir", "/tmp"), f"fmi_amd_{comm_name}.id")
         timeout_s = float(params.get("max_timeout", 60000)) / 1000.0
         uid = self._rendezvous(transport, timeout_s)
-        self._comm = Comm(uid, self.num_peers, self.peer_id)
+        self._comm = Comm(uid, self.num_peers, self.peer_id, timeout_s=timeout_s)
 
     # ---- setup ------------------------------------------------------------------------------------
     @staticmethod
@@ -195,12 +196,12 @@ class Communicator:
     # ---- point to point / data movement ------------------------------------------------------------
     def send(self, data, dest: int, t: types) -> None:
         self._comm.send(Bucket.from_numpy(self._array(data, t)), dest)
-        _dev.sync()
+        self._comm.sync()
 
     def recv(self, src: int, t: types):
         b = Bucket(self._count(t), _NP[t.type])
         self._comm.recv(b, src)
-        _dev.sync()
+        self._comm.sync()
         return self._py(b.numpy(), t)
 
     def bcast(self, data, root: int, t: types):
@@ -209,7 +210,7 @@ class Communicator:
         else:
             b = Bucket(self._count(t), _NP[t.type])
         self._comm.bcast(b, root)
-        _dev.sync()
+        self._comm.sync()
         return self._py(b.numpy(), t)
 
     def barrier(self) -> None:
@@ -220,7 +221,7 @@ class Communicator:
         send = Bucket.from_numpy(mine)
         recv = Bucket(mine.size * self.num_peers, mine.dtype) if self.peer_id == root else None
         self._comm.gather(send, recv, root)
-        _dev.sync()
+        self._comm.sync()
         return recv.numpy().tolist() if recv is not None else []
 
     def scatter(self, data, root: int, t: types):
@@ -232,7 +233,7 @@ class Communicator:
         send = Bucket.from_numpy(self._array(data, t)) if self.peer_id == root else None
         recv = Bucket(per, _NP[t.type])
         self._comm.scatter(send, recv, root)
-        _dev.sync()
+        self._comm.sync()
         return recv.numpy().tolist()
 
     # ---- reductions (reference python/PythonCommunicator.cpp:173-278) -----------------------------
@@ -250,7 +251,7 @@ class Communicator:
         allb = Bucket(n * self.num_peers, mine.dtype)
         self._comm.gather(send, allb if self.peer_id == 0 else None, 0)
         self._comm.bcast(allb, 0)
-        _dev.sync()
+        self._comm.sync()
         flat = allb.numpy()
         return [flat[p * n:(p + 1) * n] for p in range(self.num_peers)]
 
@@ -279,7 +280,7 @@ class Communicator:
         send = Bucket.from_numpy(mine)
         recv = Bucket(mine.size, mine.dtype) if self.peer_id == root else None
         self._comm.reduce(Op(int(f.op)), send, recv, root, ordered=ordered)
-        _dev.sync()
+        self._comm.sync()
         return self._py(recv.numpy(), t) if recv is not None else self._py(np.zeros_like(mine), t)
 
     def allreduce(self, data, f: func, t: types):
@@ -305,7 +306,7 @@ class Communicator:
             return self._custom(f, t, values, _dev.schedule_expr(alg, self.num_peers, self.peer_id))
         send, recv = Bucket.from_numpy(mine), Bucket(mine.size, mine.dtype)
         self._comm.scan(Op(int(f.op)), send, recv, ordered=ordered)
-        _dev.sync()
+        self._comm.sync()
         return self._py(recv.numpy(), t)
 
     def hint(self, h: hints) -> None:

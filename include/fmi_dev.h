@@ -47,7 +47,11 @@ typedef enum {
     FMI_ERR_NO_DEVICE = -3,   /* no gfx950 device visible / fmi_dev_init not called */
     FMI_ERR_UNSUPPORTED = -4, /* combination not implemented */
     FMI_ERR_ALLOC = -5,       /* device or pinned allocation failed */
-    FMI_ERR_COMM = -6         /* a communicator / transport (RCCL) call failed */
+    FMI_ERR_COMM = -6,        /* a communicator / transport (RCCL) call failed */
+    FMI_ERR_TIMEOUT = -7      /* a peer did not arrive within the communicator's timeout (the reference's
+                                 FMI::Utils::Timeout, include/utils/Common.h:11-15, raised by its channels
+                                 when a peer stays away, src/comm/Direct.cpp:28-30,40-42). The communicator
+                                 is aborted: later calls on it fail with FMI_ERR_COMM; destroy it. */
 } fmi_status_t;
 
 /* ---- op / dtype / algorithm descriptors -------------------------------------------------------- */
@@ -92,6 +96,9 @@ int fmi_dev_finalize(void);
 int fmi_dev_sync(void);
 /* Device name + arch string (e.g. "AMD Instinct MI355X gfx950"), NUL-terminated into buf. */
 int fmi_dev_describe(char* buf, size_t len);
+/* PCI bus id ("dddd:bb:dd.f") of a visible device, NUL-terminated into buf (hipDeviceGetPCIBusId): with
+ * fmi_comm_query, lets the ranks of a communicator show they sit on distinct GPUs. */
+int fmi_dev_pci_bus_id(int device, char* buf, size_t len);
 
 /* ---- memory (replaces the reference's new[]/std::vector bucket storage, include/comm/Data.h:50-97) */
 int fmi_dev_alloc(void** ptr, size_t bytes);
@@ -235,9 +242,26 @@ typedef enum { FMI_PATH_TREE = 0, FMI_PATH_RCCL = 1, FMI_PATH_DIRECT = 2 } fmi_p
 /* A fresh communicator id (FMI_COMM_ID_BYTES) made by one rank and handed to the others by any host
  * channel (FMI: Communicator::bcast over the host channel, reference include/Communicator.h:43-47). */
 int fmi_comm_unique_id(int transport, void* id, size_t len);
+/* Timeouts. Every wait of a communicator for its peers is bounded by its timeout: the rendezvous of
+ * fmi_comm_init (RCCL: non-blocking ncclCommInitRankConfig, polled), the transport's own host-side waits
+ * (PROC / LOCAL barriers and mailboxes, RCCL barriers and window setup) and fmi_comm_sync. On expiry the
+ * call returns FMI_ERR_TIMEOUT and the communicator is aborted (RCCL: ncclCommAbort, which also ends its
+ * kernels still waiting for the absent peer). fmi_comm_init uses FMI_COMM_TIMEOUT_S from the environment
+ * (seconds; for PROC also FMI_PROC_TIMEOUT_S), default 300; fmi_comm_init_timeout takes it explicitly
+ * (timeout_s <= 0: that default). An asynchronous transport error seen while waiting (RCCL
+ * ncclCommGetAsyncError: a peer's connection failed) also aborts the communicator, with FMI_ERR_COMM. */
 int fmi_comm_init(fmi_comm_t* comm, const void* id, int nranks, int rank);
+int fmi_comm_init_timeout(fmi_comm_t* comm, const void* id, int nranks, int rank, double timeout_s);
 int fmi_comm_destroy(fmi_comm_t comm);
 int fmi_comm_size(fmi_comm_t comm, int* nranks, int* rank);
+/* Wait until the work enqueued on `stream` (NULL = library stream) has completed — the blocking point of
+ * the collectives, which enqueue asynchronously — within the communicator's timeout, polling the transport
+ * for asynchronous errors (FMI_ERR_TIMEOUT / FMI_ERR_COMM as above). */
+int fmi_comm_sync(fmi_comm_t comm, fmi_stream_t stream);
+/* What the transport itself reports: RCCL ncclCommCount / ncclCommUserRank / ncclCommCuDevice (the device
+ * RCCL bound this rank to); LOCAL / PROC the communicator's size, rank and the calling thread's device.
+ * Lets a caller prove the topology it runs on (bench.py: RCCL saw N ranks on N distinct GPUs). */
+int fmi_comm_query(fmi_comm_t comm, int* count, int* rank, int* device);
 /* Symmetric window for FMI_PATH_DIRECT (collective: every rank calls it with the same `bytes`). Returns a
  * device bucket of `bytes` that every peer of the communicator can read directly (RCCL transport: HIP IPC
  * handles exchanged by all-gather, mapped with peer access over xGMI). All-or-nothing: if any rank cannot
@@ -325,14 +349,20 @@ typedef enum {
                                     0 = the blocked launches (block values through temps; the scan reads
                                     the inputs of blocks >= 1 twice). Same bits either way */
     FMI_TUNE_COMM_A2A = 8,        /* RCCL transport all-to-all: 0 = ncclAllToAll where librccl has it (default),
-                                    1 = grouped ncclSend / ncclRecv to every peer. Same bytes either way */
+                                    1 = grouped ncclSend / ncclRecv to every peer. Same bytes either way.
+                                    EVERY rank of a communicator must use the same value: the two forms post
+                                    different RCCL operations, and ranks that disagree hang (until the
+                                    communicator's timeout) */
     FMI_TUNE_COMM_GATHER = 9,     /* RCCL transport all-gather: 0 = ncclAllGather (default), 1 = grouped
                                     ncclSend / ncclRecv of this rank's shard to every peer (each peer link
-                                    carries one shard, no ring). Same bytes either way */
-    FMI_TUNE_COMM_PIPELINE = 10,  /* path TREE allreduce in K chunks (0 or 1 = off, default; 2..64): chunk k's
+                                    carries one shard, no ring). Same bytes either way. EVERY rank must use the
+                                    same value (as FMI_TUNE_COMM_A2A) */
+    FMI_TUNE_COMM_PIPELINE = 10,  /* EXPERIMENTAL (not yet run over RCCL with more than one rank). Path TREE
+                                    allreduce in K chunks (0 or 1 = off, default; 2..64): chunk k's
                                     all-gather runs on a second stream and communicator (ncclCommSplit)
                                     while chunk k + 1's all-to-all and kernel run; chunks of >= 1 MiB per
-                                    rank only. Same bits (element-wise); every rank must set the same K */
+                                    rank only. A librccl without ncclCommSplit runs the unpipelined path.
+                                    Same bits (element-wise); EVERY rank must set the same K */
     FMI_TUNE_FUSED_POLICY = 11,   /* fused P-way kernels (tree, scan; <= 16 peers), 16-B accesses: 2 = buffer
                                     loads nt with sc1 (tree) / nt sc1 (scan) stores; 0 = global_load /
                                     global_store nt; 1 = auto (default): 2 for trees of >= 4 and scans of

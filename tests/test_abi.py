@@ -98,7 +98,8 @@ c.destroy()
 
 def test_proc_transport_join_and_timeout():
     """PROC ids carry their magic; N processes join one shared-memory segment (a host barrier) and the
-    name is unlinked once all hold it; a rank whose peers never arrive fails with an error, not a hang."""
+    name is unlinked once all hold it; a rank whose peers never arrive raises the reference's Timeout
+    (FMI_ERR_TIMEOUT -> fmi_amd.Timeout, include/utils/Common.h:11-15), not a hang."""
     import subprocess
     import sys
 
@@ -115,7 +116,8 @@ def test_proc_transport_join_and_timeout():
     env["FMI_PROC_TIMEOUT_S"] = "1"
     lone = subprocess.run([sys.executable, "-c", _PROC_JOIN, b.hex(), "2", "0"], cwd=ROOT, env=env,
                           capture_output=True, text=True, timeout=120)
-    assert lone.returncode != 0 and "timed out waiting for peers" in lone.stderr
+    assert lone.returncode != 0 and "Timeout was reached" in lone.stderr, lone.stderr
+    assert "fmi_amd._lib.Timeout: FMI_ERR_TIMEOUT" in lone.stderr and "waiting for peers (join)" in lone.stderr
     assert not os.path.exists("/dev/shm/fmi_proc_%016x" % int.from_bytes(b[8:16], "little"))
 
 

@@ -115,3 +115,29 @@ def test_measure_deadline_names_the_phase_and_exits_nonzero():
     r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True, timeout=60)
     assert r.returncode == 3
     assert "rank 5 still in phase 'warm-up and timed allreduces'" in r.stderr
+
+
+def test_relay_keeps_one_stdout_line_and_the_exit_status(capsys):
+    """bench.relay: the child's JSON line reaches stdout, its other output goes to stderr, and a failing
+    child's status comes back unchanged."""
+    code = "import sys; print('rank 1 log'); print('{\"metric\": \"m\", \"value\": 1}'); sys.exit(5)"
+    rc = bench.relay([sys.executable, "-c", code])
+    cap = capsys.readouterr()
+    assert rc == 5
+    assert cap.out.strip().splitlines() == ['{"metric": "m", "value": 1}']
+    assert "rank 1 log" in cap.err
+
+
+def test_gpus_n_without_launcher_starts_ranks_and_fails_loudly():
+    """`python bench.py --gpus 2` with no WORLD_SIZE starts 2 ranks under torch.distributed.run itself (a child
+    process, no exec). Here one rank is made to fail before it touches anything (FMI_BENCH_TEST_FAIL_RANK):
+    the launcher must return non-zero and print no line."""
+    env = dict(os.environ, FMI_BENCH_TEST_FAIL_RANK="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "FMI_BENCH_LAUNCHED"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--transport", "proc",
+                        "--bucket-mib", "1"], cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0
+    assert r.stdout.strip() == ""
+    assert "without a launcher: starting" in r.stderr and "torch.distributed.run" in r.stderr
+    assert "FMI_BENCH_TEST_FAIL_RANK" in r.stderr

@@ -8,7 +8,11 @@ ranks on one GPU).
   the reference's 2-peer allreduce (src/comm/PeerToPeer.cpp:96-130), and the self-check must reject a result
   checked against the wrong buckets.
 - test_bench_py_proc_transport[world 2, 3, 4, 8]: bench.py itself under torch.distributed.run; its JSON line must
-  carry a passing self_check (headline and C4 TREE) and a correct C5 result.
+  carry a passing self_check (headline and C4 TREE), a correct C5 result, the topology every rank reported
+  (PROC: shared GPU, labelled) and the single-GPU anchor `local_equivalent`.
+- test_bench_py_launches_its_own_ranks: `python bench.py --gpus 2 …` with no launcher starts its ranks itself
+  and prints the same one self-checked line.
+- test_bench_py_force_dist_rccl_world1: the RCCL transport's own rank count (ncclCommCount) in the line.
 """
 import json
 import os
@@ -75,3 +79,55 @@ def test_bench_py_proc_transport(world):
     assert "every shard-kernel launch of the K timed allreduces" in line["roofline"]["kernel_avg_source"]
     assert line["config"]["peers"] == world and line["config"]["transport"] == "proc"
     assert "replicated_pairs" in line["diagnostics"]
+    _check_topology_and_anchor(line, world, "proc")
+
+
+def _check_topology_and_anchor(line, world, transport):
+    topo = line["config"]["topology"]
+    assert topo["ok"] and topo["transport"] == transport and len(topo["ranks"]) == world, topo
+    assert [r["transport_rank"] for r in topo["ranks"]] == list(range(world)), topo
+    assert all(r["pci_bus_id"] for r in topo["ranks"]), topo
+    if transport == "proc":
+        assert topo["transport_ranks"] == world and topo["rccl_ranks"] is None
+        assert world == 1 or (not topo["distinct_gpus"] and "share GPUs by design" in topo["note"]), topo
+    else:
+        assert topo["rccl_ranks"] == world and topo["distinct_gpus"], topo
+    le = line["local_equivalent"]
+    assert le["ms"] > 0 and le["GiB_s_reduced_buckets"] > 0 and le["value_over_local"] > 0, le
+    assert f"{world} peers" in le["workload"]
+
+
+def test_bench_py_launches_its_own_ranks():
+    """No torch.distributed.run: bench.py starts the 2 ranks itself (a child launcher, never exec) and relays
+    rank 0's one line; the line is the same self-checked N > 1 line as the torchrun form."""
+    env = dict(os.environ, FMI_PROC_TIMEOUT_S="90", OMP_NUM_THREADS="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "FMI_BENCH_LAUNCHED"):
+        env.pop(k, None)
+    cmd = [sys.executable, "bench.py", "--gpus", "2", "--transport", "proc", "--steps", "4", "--warmup", "1",
+           "--dist-sets", "2", "--bucket-mib", "8", "--c4-mib", "16", "--c5-mib", "8", "--diag-deadline", "150",
+           "--no-diagnostics"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = r.stdout.strip().splitlines()
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["value"] > 0 and line["self_check"]["ok"]
+    assert "without a launcher: starting" in r.stderr
+    _check_topology_and_anchor(line, 2, "proc")
+
+
+def test_bench_py_force_dist_rccl_world1():
+    """The N > 1 code path over the RCCL transport at world size 1 (the only RCCL world a 1-GPU box has):
+    the line carries RCCL's own rank count and the 1-GPU anchor."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--force-dist",
+           "--steps", "4", "--warmup", "1", "--dist-sets", "2", "--bucket-mib", "8", "--c4-mib", "16",
+           "--c5-mib", "8", "--no-diagnostics"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=240,
+                       env=dict(os.environ, OMP_NUM_THREADS="1"))
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    assert line["config"]["topology"]["rccl_ranks"] == 1
+    _check_topology_and_anchor(line, 1, "rccl")

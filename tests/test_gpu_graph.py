@@ -80,6 +80,28 @@ def test_graph_capture_of_a_synchronising_call_fails_loudly(device):
     s.destroy()
 
 
+def test_graph_capture_of_an_arena_call_is_refused(device):
+    """A call that needs the library's scratch arena (here an unaligned 4-peer reduce_tree, which runs the
+    program as pairwise passes through arena temps) is refused while its stream is capturing: the arena's
+    ordering event would be recorded inside the graph and its replays would race later direct calls
+    (include/fmi_dev.h). FMI_ERR_UNSUPPORTED, and the stream works afterwards."""
+    from fmi_amd import Alg
+
+    s = Stream()
+    n = 4099
+    base = [Bucket.from_numpy(np.full(n + 1, p + 1, np.float32)) for p in range(4)]
+    ins = [b.view(1, n) for b in base]  # 4-byte offset: not 16-B aligned
+    out = Bucket(n, np.float32)
+    with pytest.raises(fmi_amd.FmiError, match="FMI_ERR_UNSUPPORTED.*graph"):
+        Graph.capture(s, lambda: fmi_amd.reduce_tree(Op.SUM, Alg.ALLREDUCE, out, ins, stream=s))
+    s.destroy()
+    s = Stream()
+    fmi_amd.reduce_tree(Op.SUM, Alg.ALLREDUCE, out, ins, stream=s)
+    s.sync()
+    assert np.all(out.numpy() == 10.0)
+    s.destroy()
+
+
 @pytest.mark.parametrize("dtype", [np.float32, np.int64, np.uint8, np.float64], ids=lambda d: np.dtype(d).name)
 def test_pair_batch_matches_separate_combines(device, dtype):
     """fmi_dev_reduce_pair_batch: many buckets of mixed sizes (empty, below one 16-B lane group, ragged,
