@@ -83,6 +83,9 @@ def parse():
                     help="seconds everything after `value` (c4, c5, diagnostics) may take before the line is "
                          "printed without the rest of it")
     ap.add_argument("--diag-direct", action="store_true", help="N>1 diagnostics: also check and time path DIRECT")
+    ap.add_argument("--diag-pipeline", action="store_true",
+                    help="N>1 diagnostics: also time the EXPERIMENTAL pipelined allreduce (FMI_TUNE_COMM_PIPELINE 4 / 8: "
+                         "two RCCL communicators in flight at once, not yet run across GPUs)")
     ap.add_argument("--measure-deadline", type=float, default=900.0,
                     help="N>1: seconds the measurement up to `value` (setup, warm-up, timed steps, self-check) may "
                          "take; past it the rank names the phase it is stuck in on stderr and exits with status 3")
@@ -663,9 +666,11 @@ def after_value(args, ar, world, dist, line, proc):
 def exchange_variants(args, ar) -> dict:
     """The headline step (path TREE, 256 MiB per peer) with each RCCL realisation of its two exchanges:
     ncclAllToAll or grouped send/recv for the all-to-all (FMI_TUNE_COMM_A2A), ncclAllGather or grouped
-    send/recv of the shard to every peer for the all-gather (FMI_TUNE_COMM_GATHER), and the allreduce
-    pipelined in 4 or 8 chunks (FMI_TUNE_COMM_PIPELINE: chunk k's all-gather on a second communicator while
-    chunk k+1's all-to-all runs). Same bytes, same result bits (self-checked); the step time decides the
+    send/recv of the shard to every peer for the all-gather (FMI_TUNE_COMM_GATHER), and, with
+    --diag-pipeline only, the allreduce pipelined in 4 or 8 chunks (FMI_TUNE_COMM_PIPELINE: chunk k's
+    all-gather on a second communicator while chunk k+1's all-to-all runs — experimental: two RCCL
+    communicators in flight at once have not run across GPUs yet). Every rank sets the same values (the
+    loop is the same on every rank). Same bytes, same result bits (self-checked); the step time decides the
     default. Max over ranks."""
     import fmi_amd
     from fmi_amd import Tune
@@ -673,7 +678,9 @@ def exchange_variants(args, ar) -> dict:
     n = args.bucket_mib * MIB // 4
     steps = max(10, args.steps // 10)
     out = {}
-    variants = [(a2a, gather, 0) for a2a in (0, 1) for gather in (0, 1)] + [(0, 0, 4), (0, 0, 8)]
+    variants = [(a2a, gather, 0) for a2a in (0, 1) for gather in (0, 1)]
+    if args.diag_pipeline:
+        variants += [(0, 0, 4), (0, 0, 8)]
     try:
         for a2a, gather, chunks in variants:
             fmi_amd.tune_set(Tune.COMM_A2A, a2a)
