@@ -274,21 +274,7 @@ class CommAllreduce:
                 "transport_device": q["device"], "torch_device": dev, "pci_bus_id": fdev.pci_bus_id(dev)}
         every = [None] * self.world
         dist.all_gather_object(every, mine, group=self.group)
-        counts = sorted({e["transport_count"] for e in every})
-        pci = [e["pci_bus_id"] for e in every]
-        distinct = len(set(pci)) == len(pci)
-        ranks_ok = counts == [self.world] and all(e["transport_rank"] == e["rank"] for e in every)
-        shared_ok = self.transport == "proc"  # several PROC ranks on one GPU is what the transport is for
-        res = {"transport": self.transport, "rccl_ranks": counts[0] if len(counts) == 1 else counts,
-               "ranks": [{k: e[k] for k in ("transport_rank", "transport_device", "torch_device", "pci_bus_id")}
-                         for e in every],
-               "distinct_gpus": distinct, "ok": bool(ranks_ok and (distinct or shared_ok))}
-        if self.transport != "rccl":
-            res["rccl_ranks"] = None
-            res["transport_ranks"] = counts[0] if len(counts) == 1 else counts
-        if not distinct and shared_ok:
-            res["note"] = "PROC transport: ranks share GPUs by design (single-GPU runs of the N > 1 path)"
-        return res
+        return judge_topology(every, self.world, self.transport)
 
     def local_equivalent(self, n: int, launches: int = 10, sets: int = 2) -> dict:
         """The like-for-like single-GPU anchor of the N > 1 line: the same world-peer f32 sum-allreduce of
@@ -586,6 +572,27 @@ class CommAllreduce:
 
     def destroy(self) -> None:
         self.comm.destroy()
+
+
+def judge_topology(every: List[dict], world: int, transport: str) -> dict:
+    """The verdict of CommAllreduce.topology over every rank's report (host logic, CPU-tested): ok when the
+    transport saw exactly `world` ranks, each rank at its own index, and (RCCL) no two ranks share a GPU (PCI
+    bus id). Several PROC ranks on one GPU is what that transport is for: labelled, not an error."""
+    counts = sorted({e["transport_count"] for e in every})
+    pci = [e["pci_bus_id"] for e in every]
+    distinct = len(set(pci)) == len(pci)
+    ranks_ok = len(every) == world and counts == [world] and all(e["transport_rank"] == e["rank"] for e in every)
+    shared_ok = transport == "proc"
+    res = {"transport": transport, "rccl_ranks": counts[0] if len(counts) == 1 else counts,
+           "ranks": [{k: e[k] for k in ("transport_rank", "transport_device", "torch_device", "pci_bus_id")}
+                     for e in every],
+           "distinct_gpus": distinct, "ok": bool(ranks_ok and (distinct or shared_ok))}
+    if transport != "rccl":
+        res["rccl_ranks"] = None
+        res["transport_ranks"] = counts[0] if len(counts) == 1 else counts
+    if not distinct and shared_ok:
+        res["note"] = "PROC transport: ranks share GPUs by design (single-GPU runs of the N > 1 path)"
+    return res
 
 
 def phase_breakdown(n: int, group=None, iters: int = 5) -> dict:

@@ -143,3 +143,26 @@ def test_bench_loop_runs_multi_process(path):
     assert res[0]["step_ms"] == res[1]["step_ms"] > 0
     assert len(res[0]["kernel_ms"]) == 3
     assert res[0]["extra"]["exchange"] == path and res[0]["extra"]["kernel_algo_bytes"] == 3 * 8192 * 4
+
+
+def test_topology_verdict():
+    """bench.py's N > 1 topology check (fmi_amd.collectives.judge_topology, host logic): RCCL must see every
+    rank at its own index on its own GPU; PROC ranks may share one (labelled)."""
+    from fmi_amd.collectives import judge_topology
+
+    def rep(r, count=4, trank=None, pci=None):
+        return {"rank": r, "transport_count": count, "transport_rank": r if trank is None else trank,
+                "transport_device": r, "torch_device": r, "pci_bus_id": pci or f"0000:{0x10 + r:02x}:00.0"}
+
+    good = [rep(r) for r in range(4)]
+    v = judge_topology(good, 4, "rccl")
+    assert v["ok"] and v["rccl_ranks"] == 4 and v["distinct_gpus"]
+    shared = [rep(r, pci="0000:11:00.0") for r in range(4)]
+    assert not judge_topology(shared, 4, "rccl")["ok"]  # two ranks on one GPU over RCCL: refused
+    v = judge_topology(shared, 4, "proc")
+    assert v["ok"] and v["rccl_ranks"] is None and v["transport_ranks"] == 4 and "by design" in v["note"]
+    assert not judge_topology([rep(r, count=3) for r in range(4)], 4, "rccl")["ok"]  # RCCL saw 3 ranks
+    assert judge_topology([rep(r, count=3) for r in range(4)], 4, "rccl")["rccl_ranks"] == 3
+    swapped = [rep(0, trank=1), rep(1, trank=0), rep(2), rep(3)]
+    assert not judge_topology(swapped, 4, "rccl")["ok"]
+    assert judge_topology([rep(0, count=1)], 1, "rccl")["ok"]
