@@ -172,6 +172,26 @@ def c1_host():
         return {"error": str(e)}
 
 
+_JSON_OUT = None
+
+
+def json_out():
+    """Where the one JSON line goes: the process's original stdout, claimed by claim_stdout()."""
+    return _JSON_OUT or sys.stdout
+
+
+def claim_stdout() -> None:
+    """Keep the process's stdout for the one JSON line only: fd 1 is duplicated for the line, then pointed
+    at stderr, so whatever libraries print to stdout (RCCL prints a version banner on communicator init)
+    cannot add lines to the output the driver parses."""
+    global _JSON_OUT
+    if _JSON_OUT is not None:
+        return
+    sys.stdout.flush()
+    _JSON_OUT = os.fdopen(os.dup(1), "w", buffering=1)
+    os.dup2(2, 1)
+
+
 class _Emitter:
     """Prints the one JSON line exactly once (rank 0), from the main thread or from the deadline —
     whichever comes first."""
@@ -193,7 +213,7 @@ class _Emitter:
                     self.line = {k: v for k, v in self.line.items() if k in _HEADLINE_KEYS}
                     self.line["incomplete"] = "deadline reached while recording the after-value section"
                     text = json.dumps(self.line)
-                print(text, flush=True)
+                print(text, file=json_out(), flush=True)
 
     def deadline(self, state):
         msg = "deadline reached; the timed measurement (value, roofline, self_check) is unaffected"
@@ -260,6 +280,7 @@ def _roofline(kernel, algo_bytes, kernel_avg_ms, source, extra=None, pmc_key=Non
 # N = 1: config C2
 # ------------------------------------------------------------------------------------------------------
 def run_single(args):
+    claim_stdout()
     import numpy as np
 
     import fmi_amd
@@ -324,7 +345,7 @@ def run_single(args):
             line["c5"]["after_pause_s"] = QUIET_S
         except Exception as e:  # reported, never fails the measured line
             line["c5"] = f"failed: {type(e).__name__}: {e}"
-    print(json.dumps(line), flush=True)
+    print(json.dumps(line), file=json_out(), flush=True)
 
 
 def one_peer_allreduce(n: int, launches: int = 20) -> dict:
@@ -520,6 +541,7 @@ class _PhaseWatch:
 
 
 def run_dist(args, world, rank, local_rank):
+    claim_stdout()
     # torch first: libfmi_dev.so then binds to the HIP runtime torch already loaded (one runtime per process,
     # shared streams/pointers with RCCL) — see DESIGN.md §Runtime.
     import torch

@@ -534,7 +534,7 @@ private:
             FMI_RCCL(GroupEnd());
         }
         if (p.copy_len && recv + p.copy_dst != send + p.copy_src)
-            FMI_COMM_HIP(hipMemcpyAsync(recv + p.copy_dst, send + p.copy_src, p.copy_len, hipMemcpyDeviceToDevice, s));
+            FMI_COMM_RC(device_copy(recv + p.copy_dst, send + p.copy_src, p.copy_len, s));
         return FMI_OK;
     }
     const RcclApi* api_;
@@ -612,7 +612,7 @@ public:
     }
     int bcast(char* buf, size_t bytes, int root, hipStream_t s) override {
         return exchange(buf, s, [&](const std::vector<const char*>& all) -> int {
-            if (rank_ != root && bytes) FMI_COMM_HIP(hipMemcpyAsync(buf, all[root], bytes, hipMemcpyDeviceToDevice, s));
+            if (rank_ != root && bytes) FMI_COMM_RC(device_copy(buf, all[root], bytes, s));
             return FMI_OK;
         });
     }
@@ -653,9 +653,11 @@ public:
             rc = fail(FMI_ERR_COMM, "local transport: message of " + std::to_string(msg->bytes) + " bytes, expected " +
                                         std::to_string(bytes));
         } else if (bytes) {
-            hipError_t e = hipMemcpyAsync(buf, msg->buf, bytes, hipMemcpyDeviceToDevice, s);
-            if (e == hipSuccess) e = hipStreamSynchronize(s);
-            if (e != hipSuccess) rc = hip_err("local transport recv", e);
+            rc = device_copy(buf, msg->buf, bytes, s);
+            if (rc == FMI_OK) {
+                const hipError_t e = hipStreamSynchronize(s);
+                if (e != hipSuccess) rc = hip_err("local transport recv", e);
+            }
         }
         std::lock_guard<std::mutex> lk(hub_->mu);
         msg->done = true;
@@ -722,12 +724,11 @@ private:
                 if (k == sends.size() || sends[k].len != r.len)
                     return fail(FMI_ERR_COMM, "exchange plan: rank " + std::to_string(j) + " posts no send of " +
                                                   std::to_string(r.len) + " B to rank " + std::to_string(rank_));
-                FMI_COMM_HIP(hipMemcpyAsync(recv + r.off, all[j] + sends[k].off, r.len, hipMemcpyDeviceToDevice, s));
+                FMI_COMM_RC(device_copy(recv + r.off, all[j] + sends[k].off, r.len, s));
                 ++k;
             }
             if (mine.copy_len && recv + mine.copy_dst != send + mine.copy_src)
-                FMI_COMM_HIP(hipMemcpyAsync(recv + mine.copy_dst, send + mine.copy_src, mine.copy_len,
-                                            hipMemcpyDeviceToDevice, s));
+                FMI_COMM_RC(device_copy(recv + mine.copy_dst, send + mine.copy_src, mine.copy_len, s));
             return FMI_OK;
         });
     }
@@ -1252,7 +1253,7 @@ int padded_source(Comm* c, size_t n, size_t padded, size_t esz, const void* send
     }
     char* pad = nullptr;
     FMI_COMM_RC(c->scratch(0, padded * esz, s, &pad));
-    FMI_COMM_HIP(hipMemcpyAsync(pad, send, n * esz, hipMemcpyDeviceToDevice, s));
+    FMI_COMM_RC(device_copy(pad, send, n * esz, s));
     FMI_COMM_HIP(hipMemsetAsync(pad + n * esz, 0, (padded - n) * esz, s));
     *out = pad;
     return FMI_OK;
@@ -1368,7 +1369,7 @@ int allreduce_tree_pipelined(Comm* c, int op, int dtype, int alg, const void* se
         if (padded != cn) {  // only the last chunk can need padding
             char* pad = nullptr;
             FMI_COMM_RC(c->scratch(8 + 4 * j, padded * esz, s, &pad));
-            FMI_COMM_HIP(hipMemcpyAsync(pad, src, cn * esz, hipMemcpyDeviceToDevice, s));
+            FMI_COMM_RC(device_copy(pad, src, cn * esz, s));
             FMI_COMM_HIP(hipMemsetAsync(pad + cn * esz, 0, (padded - cn) * esz, s));
             src = pad;
         }
@@ -1391,7 +1392,7 @@ int allreduce_tree_pipelined(Comm* c, int op, int dtype, int alg, const void* se
             char* out = nullptr;
             FMI_COMM_RC(c->scratch(11 + 4 * j, padded * esz, p.gs, &out));
             FMI_COMM_RC(tg->all_gather(red, out, shard * esz, p.gs));
-            FMI_COMM_HIP(hipMemcpyAsync(dst, out, cn * esz, hipMemcpyDeviceToDevice, p.gs));
+            FMI_COMM_RC(device_copy(dst, out, cn * esz, p.gs));
         }
         FMI_COMM_HIP(hipEventRecord(p.gathered[j], p.gs));
     }
@@ -1406,7 +1407,7 @@ int allreduce_device(Comm* c, int op, int dtype, int alg, int path, const void* 
     const int N = c->t->n();
     const size_t esz = dtype_size(dtype);
     if (N == 1) {  // reference P = 1: a copy
-        if (send != recv) FMI_COMM_HIP(hipMemcpyAsync(recv, send, n * esz, hipMemcpyDeviceToDevice, s));
+        if (send != recv) FMI_COMM_RC(device_copy(recv, send, n * esz, s));
         return FMI_OK;
     }
     // Float max / min: every peer of the reference allreduce keeps its own operand order, so on ±0 ties
@@ -1478,7 +1479,7 @@ int allreduce_device(Comm* c, int op, int dtype, int alg, int path, const void* 
             char* out = nullptr;
             FMI_COMM_RC(c->scratch(3, padded * esz, s, &out));
             FMI_COMM_RC(c->t->all_to_all(red, out, shard * esz, s));
-            FMI_COMM_HIP(hipMemcpyAsync(recv, out, n * esz, hipMemcpyDeviceToDevice, s));
+            FMI_COMM_RC(device_copy(recv, out, n * esz, s));
             return FMI_OK;
         }
         FMI_COMM_RC(c->timing.begin(s));
@@ -1491,7 +1492,7 @@ int allreduce_device(Comm* c, int op, int dtype, int alg, int path, const void* 
     char* out = nullptr;
     FMI_COMM_RC(c->scratch(3, padded * esz, s, &out));
     FMI_COMM_RC(c->t->all_gather(red, out, shard * esz, s));
-    FMI_COMM_HIP(hipMemcpyAsync(recv, out, n * esz, hipMemcpyDeviceToDevice, s));
+    FMI_COMM_RC(device_copy(recv, out, n * esz, s));
     return FMI_OK;
 }
 
@@ -1797,7 +1798,7 @@ static int comm_reduce_impl(fmi_comm_t comm, int op, int dtype, int alg, const v
     hipStream_t s = resolve_stream(stream);
     const size_t esz = dtype_size(dtype);
     if (N == 1) {
-        if (send != recv) FMI_COMM_HIP(hipMemcpyAsync(recv, send, n * esz, hipMemcpyDeviceToDevice, s));
+        if (send != recv) FMI_COMM_RC(device_copy(recv, send, n * esz, s));
         return FMI_OK;
     }
     const size_t shard = shard_elems(n, N);
@@ -1823,7 +1824,7 @@ static int comm_reduce_impl(fmi_comm_t comm, int op, int dtype, int alg, const v
     char* out = nullptr;
     FMI_COMM_RC(c->scratch(3, padded * esz, s, &out));
     FMI_COMM_RC(c->t->gather(red, out, shard * esz, root, s));
-    if (is_root) FMI_COMM_HIP(hipMemcpyAsync(recv, out, n * esz, hipMemcpyDeviceToDevice, s));
+    if (is_root) FMI_COMM_RC(device_copy(recv, out, n * esz, s));
     return FMI_OK;
 }
 
@@ -1880,10 +1881,10 @@ static int comm_reduce_sendbuf_impl(fmi_comm_t comm, int op, int dtype, int alg,
             char* out = nullptr;
             FMI_COMM_RC(c->scratch(3, padded * esz, s, &out));
             FMI_COMM_RC(c->t->all_to_all(partial, out, shard * esz, s));
-            FMI_COMM_HIP(hipMemcpyAsync(send, out, n * esz, hipMemcpyDeviceToDevice, s));
+            FMI_COMM_RC(device_copy(send, out, n * esz, s));
         }
     }
-    if (is_root && recv != send) FMI_COMM_HIP(hipMemcpyAsync(recv, send, n * esz, hipMemcpyDeviceToDevice, s));
+    if (is_root && recv != send) FMI_COMM_RC(device_copy(recv, send, n * esz, s));
     return FMI_OK;
 }
 
@@ -1899,7 +1900,7 @@ static int comm_scan_impl(fmi_comm_t comm, int op, int dtype, int alg, const voi
     const int N = c->t->n();
     const size_t esz = dtype_size(dtype);
     if (N == 1) {
-        if (send != recv) FMI_COMM_HIP(hipMemcpyAsync(recv, send, n * esz, hipMemcpyDeviceToDevice, s));
+        if (send != recv) FMI_COMM_RC(device_copy(recv, send, n * esz, s));
         return FMI_OK;
     }
     const size_t shard = shard_elems(n, N);
@@ -1929,7 +1930,7 @@ static int comm_scan_impl(fmi_comm_t comm, int op, int dtype, int alg, const voi
     char* out = nullptr;
     FMI_COMM_RC(c->scratch(3, padded * esz, s, &out));
     FMI_COMM_RC(c->t->all_to_all(prefix, out, shard * esz, s));
-    FMI_COMM_HIP(hipMemcpyAsync(recv, out, n * esz, hipMemcpyDeviceToDevice, s));
+    FMI_COMM_RC(device_copy(recv, out, n * esz, s));
     return FMI_OK;
 }
 

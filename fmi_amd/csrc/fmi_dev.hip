@@ -247,8 +247,7 @@ int run_program_stepwise(int op, int dtype, const sched::HostProgram& prog, void
     for (int k = 0; k < nouts && rc == FMI_OK; ++k) {
         const void* src = addr(out_value[k]);
         if (src != outs[k] && n > 0) {
-            const hipError_t e = hipMemcpyAsync(outs[k], src, n * esz, hipMemcpyDeviceToDevice, s);
-            if (e != hipSuccess) rc = hip_fail("hipMemcpyAsync (P-way result)", e);
+            rc = device_copy(outs[k], src, n * esz, s);
         }
     }
     FMI_HIP_TRY(hipEventRecord(g_state.arena_free, s));
@@ -284,7 +283,7 @@ int tree_blocked(int op, int dtype, int alg, void* out, const void* const* ins, 
     const bool dry = t.dry;
     constexpr int B16 = sched::kMaxFusedPeers;
     if (P == 1) {
-        if (!dry && out != ins[0]) FMI_HIP_TRY(hipMemcpyAsync(out, ins[0], n * dtype_size(dtype), hipMemcpyDeviceToDevice, s));
+        if (!dry && out != ins[0]) FMI_RC_TRY(device_copy(out, ins[0], n * dtype_size(dtype), s));
         return FMI_OK;
     }
     if (P <= sched::max_fused_peers(alg)) {
@@ -401,7 +400,7 @@ int chain_superblocks(int op, int dtype, bool scan, void* const* outs, void* out
 // reduce_no_order over up to 128 values (transformed ids, root 0): fused up to 16 peers, one pass beyond.
 int reduce_level(int op, int dtype, void* out, const void* const* vals, int P, size_t n, hipStream_t s) {
     if (P == 1) {
-        if (out != vals[0]) FMI_HIP_TRY(hipMemcpyAsync(out, vals[0], n * dtype_size(dtype), hipMemcpyDeviceToDevice, s));
+        if (out != vals[0]) FMI_RC_TRY(device_copy(out, vals[0], n * dtype_size(dtype), s));
         return FMI_OK;
     }
     if (P <= sched::kMaxFusedPeers) {
@@ -559,7 +558,7 @@ int scan_blocked(int op, int dtype, int alg, void* const* outs, const void* cons
     constexpr int BL = sched::kScanBlock;
     const bool dry = t.dry;
     if (P == 1) {
-        if (!dry && outs[0] != ins[0]) FMI_HIP_TRY(hipMemcpyAsync(outs[0], ins[0], n * dtype_size(dtype), hipMemcpyDeviceToDevice, s));
+        if (!dry && outs[0] != ins[0]) FMI_RC_TRY(device_copy(outs[0], ins[0], n * dtype_size(dtype), s));
         return FMI_OK;
     }
     if (P <= sched::max_fused_peers(alg)) {
@@ -714,6 +713,35 @@ int fail(int code, const std::string& msg) {
 }
 
 hipStream_t library_stream() { return g_state.stream; }
+
+// A device allocation (this process's, or another's mapped over IPC): what copy_tile may touch. Host and
+// unknown pointers answer false, and the failed query is cleared from the runtime's last-error slot (the
+// launch checks below read it).
+static bool device_memory(const void* p) {
+    hipPointerAttribute_t a{};
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeDevice;
+}
+
+int device_copy(void* dst, const void* src, size_t bytes, hipStream_t s) {
+    if (bytes == 0 || dst == src) return FMI_OK;
+    const char* d = static_cast<const char*>(dst);
+    const char* c = static_cast<const char*>(src);
+    const bool disjoint = d + bytes <= c || c + bytes <= d;
+    if (bytes >= kDeviceCopyMin && disjoint && aligned16(dst) && aligned16(src) && device_memory(dst) &&
+        device_memory(src)) {
+        constexpr int U = 4;
+        const size_t tiles = (bytes / 16 + U * 256 - 1) / (U * 256);
+        copy_tile<U><<<static_cast<unsigned>(std::max<size_t>(1, tiles)), 256, 0, s>>>(static_cast<char*>(dst), c, bytes);
+        FMI_HIP_TRY(hipGetLastError());
+        return FMI_OK;
+    }
+    FMI_HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s));
+    return FMI_OK;
+}
 
 // The fused kernels' `pol` argument. Auto (1): buffer accesses where tools/ab_fused_policy.py measured them
 // ahead with >= 1.5 GiB of rotating buckets (tree P >= 4: +1.6..3.2 %; scan P >= 8: +0.8..0.9 %), global
@@ -881,7 +909,10 @@ int fmi_dev_d2h_async(void* dst, const void* src, size_t bytes, fmi_stream_t str
     return copy_async(dst, src, bytes, hipMemcpyDeviceToHost, stream);
 }
 int fmi_dev_d2d_async(void* dst, const void* src, size_t bytes, fmi_stream_t stream) {
-    return copy_async(dst, src, bytes, hipMemcpyDeviceToDevice, stream);
+    if (bytes == 0) return FMI_OK;
+    if (!dst || !src) return fail(FMI_ERR_INVALID, "null buffer");
+    if (int rc = require_device()) return rc;
+    return device_copy(dst, src, bytes, resolve(stream));
 }
 
 int fmi_dev_memset_async(void* dst, int value, size_t bytes, fmi_stream_t stream) {

@@ -169,6 +169,12 @@ struct PairBatch {
 };
 int launch_pair_batch(int op, int dtype, const PairBatch& pb, hipStream_t s);
 
+// dst <- src (bytes) on stream s: the copy_tile kernel (nontemporal, ≈ the chip's copy rate) when both are
+// 16-B aligned, non-overlapping device allocations of >= kDeviceCopyMin bytes; hipMemcpyAsync otherwise
+// (host or unknown pointers, small or overlapping copies).
+inline constexpr size_t kDeviceCopyMin = size_t(256) << 10;
+int device_copy(void* dst, const void* src, size_t bytes, hipStream_t s);
+
 // Workgroups to cover `items` with `block` threads each (at least 1). Callers cap it before narrowing.
 inline size_t grid_for(size_t items, unsigned block) {
     const size_t g = (items + block - 1) / block;

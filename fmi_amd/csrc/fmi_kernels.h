@@ -274,6 +274,33 @@ __device__ __forceinline__ void pair_tail(T* out, const T* a, const T* b, size_t
     }
 }
 
+// Device copy (device_copy in fmi_dev.hip: the reference's P = 1 allreduce and every staging copy of the
+// communicator): the pair tile's access pattern with one stream in and one out — U 16-B vectors per thread,
+// nontemporal loads and stores, one tile per workgroup; workgroup 0 copies the sub-16-B tail. Algorithmic
+// HBM bytes: 2 x bytes. Both pointers 16-B aligned.
+template <int U>
+__global__ void __launch_bounds__(256) copy_tile(char* out, const char* in, size_t bytes) {
+    const size_t nvec = bytes / 16;
+    const size_t base = static_cast<size_t>(blockIdx.x) * U * 256 + threadIdx.x;
+    const u32x4* src = reinterpret_cast<const u32x4*>(in);
+    u32x4* dst = reinterpret_cast<u32x4*>(out);
+    u32x4 v[U];
+    if (static_cast<size_t>(blockIdx.x + 1) * U * 256 <= nvec) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = __builtin_nontemporal_load(src + base + u * 256);
+#pragma unroll
+        for (int u = 0; u < U; ++u) __builtin_nontemporal_store(v[u], dst + base + u * 256);
+    } else {
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (base + u * 256 < nvec) v[u] = __builtin_nontemporal_load(src + base + u * 256);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (base + u * 256 < nvec) __builtin_nontemporal_store(v[u], dst + base + u * 256);
+    }
+    if (blockIdx.x == 0 && nvec * 16 + threadIdx.x < bytes) out[nvec * 16 + threadIdx.x] = in[nvec * 16 + threadIdx.x];
+}
+
 // One-shot grid: one tile per workgroup. Pointers must be 16-B aligned. Whole tiles t with t % 8 < sc1_k
 // store with sc1, the rest nontemporal (default 0: none, the round-1 kernel the exploration tools compare
 // against). Consecutive workgroups are dispatched to different XCDs, so sc1_k of the 8 XCDs store sc1

@@ -141,3 +141,19 @@ def test_gpus_n_without_launcher_starts_ranks_and_fails_loudly():
     assert r.stdout.strip() == ""
     assert "without a launcher: starting" in r.stderr and "torch.distributed.run" in r.stderr
     assert "FMI_BENCH_TEST_FAIL_RANK" in r.stderr
+
+
+def test_library_stdout_noise_cannot_reach_the_line():
+    """claim_stdout(): after it, anything written to fd 1 (RCCL's version banner, C printf) lands on stderr
+    and the JSON line alone on the original stdout."""
+    code = ("import os, sys, json\n"
+            f"sys.path.insert(0, {ROOT!r})\n"
+            "import bench\n"
+            "bench.claim_stdout()\n"
+            "os.write(1, b'RCCL version : banner\\n')\n"
+            "print('python noise')\n"
+            "print(json.dumps({'metric': 'm', 'value': 1}), file=bench.json_out(), flush=True)\n")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.strip().splitlines() == ['{"metric": "m", "value": 1}']
+    assert "RCCL version" in r.stderr and "python noise" in r.stderr

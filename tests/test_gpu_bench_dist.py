@@ -126,8 +126,8 @@ def test_bench_py_force_dist_rccl_world1():
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=240,
                        env=dict(os.environ, OMP_NUM_THREADS="1"))
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
-    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
-    assert len(lines) == 1, r.stdout
+    lines = r.stdout.strip().splitlines()
+    assert len(lines) == 1, r.stdout  # RCCL's version banner goes to stderr (bench.claim_stdout)
     line = json.loads(lines[0])
     assert line["config"]["topology"]["rccl_ranks"] == 1
     _check_topology_and_anchor(line, 1, "rccl")

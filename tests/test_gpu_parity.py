@@ -149,6 +149,47 @@ def test_reduce_pair_sc1_tiles_keep_bits(device, dtype, sc1_of_8):
             fmi_amd.tune_set(k, v)
 
 
+@pytest.mark.parametrize("nbytes", [16, 262143, 262144, 262144 + 5, (1 << 20) + 16 * 1024 + 3, 64 << 20])
+def test_device_copy_bits(device, nbytes):
+    """fmi_dev_d2d_async / the communicator's staging copies (device_copy): the copy_tile kernel for aligned
+    device buckets of >= 256 KiB (whole tiles, a partial tile, a sub-16-B tail), hipMemcpyAsync below that,
+    for unaligned views and for host (page-locked) memory: every byte, and nothing past the end."""
+    rng = np.random.default_rng(nbytes)
+    data = rng.integers(0, 256, nbytes, dtype=np.uint8)
+    src = Bucket.from_numpy(data)
+    dst = Bucket(nbytes + 64, np.uint8)
+    dst.upload(np.full(nbytes + 64, 0xA5, np.uint8))
+    dst.view(0, nbytes).copy_from(src)
+    fmi_amd.sync()
+    got = dst.numpy()
+    assert np.array_equal(got[:nbytes], data) and np.all(got[nbytes:] == 0xA5)
+    if nbytes >= 262144:  # unaligned destination: the hipMemcpyAsync path, same bytes
+        dst.upload(np.full(nbytes + 64, 0xA5, np.uint8))
+        dst.view(3, nbytes).copy_from(src)
+        fmi_amd.sync()
+        got = dst.numpy()
+        assert np.array_equal(got[3:3 + nbytes], data) and np.all(got[:3] == 0xA5) and np.all(got[3 + nbytes:] == 0xA5)
+    src.free()
+    dst.free()
+
+
+def test_one_rank_allreduce_is_a_copy(device):
+    """The reference's P = 1 allreduce (PeerToPeer.cpp:96-130 with one peer) leaves recvbuf = sendbuf: the
+    one-rank communicator's copy (device_copy kernel for 16-B aligned device buckets), bit for bit."""
+    from fmi_amd.comm import Comm, Transport, unique_id
+
+    c = Comm(unique_id(Transport.LOCAL), 1, 0)
+    for n in (1, 65536 + 7, (16 << 20) + 3):
+        x = inputs(np.float32, n, 0, seed=61)
+        s, o = Bucket.from_numpy(x), Bucket(n, np.float32)
+        c.allreduce(fmi_amd.Op.SUM, s, o)
+        fmi_amd.sync()
+        assert_bit_equal(o.numpy(), x, f"n={n}")
+        s.free()
+        o.free()
+    c.destroy()
+
+
 def test_combine_out_of_place(device):
     a, b = inputs(np.int64, 5003, 0), inputs(np.int64, 5003, 1)
     out = Bucket(5003, np.int64)
