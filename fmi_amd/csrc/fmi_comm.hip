@@ -1406,7 +1406,7 @@ int allreduce_device(Comm* c, int op, int dtype, int alg, int path, const void* 
                      hipStream_t s) {
     const int N = c->t->n();
     const size_t esz = dtype_size(dtype);
-    if (N == 1) {  // reference P = 1: a copy
+    if (N == 1 && !tune(FMI_TUNE_COMM_ONE_RANK_EXCHANGE)) {  // reference P = 1: a copy
         if (send != recv) FMI_COMM_RC(device_copy(recv, send, n * esz, s));
         return FMI_OK;
     }
@@ -1463,7 +1463,7 @@ int allreduce_device(Comm* c, int op, int dtype, int alg, int path, const void* 
         for (int j = 0; j < N; ++j) parts[j] = staging + j * shard * esz;
         if (per_rank) {
             FMI_COMM_RC(c->timing.begin(s));
-            if (N <= sched::kMaxFusedPeers) {
+            if (N >= 2 && N <= sched::kMaxFusedPeers) {
                 PeerPtrs ptrs{};
                 for (int j = 0; j < N; ++j) {
                     ptrs.in[j] = parts[j];
@@ -1797,7 +1797,7 @@ static int comm_reduce_impl(fmi_comm_t comm, int op, int dtype, int alg, const v
     std::lock_guard<std::mutex> lk(c->mu);
     hipStream_t s = resolve_stream(stream);
     const size_t esz = dtype_size(dtype);
-    if (N == 1) {
+    if (N == 1 && !tune(FMI_TUNE_COMM_ONE_RANK_EXCHANGE)) {
         if (send != recv) FMI_COMM_RC(device_copy(recv, send, n * esz, s));
         return FMI_OK;
     }
@@ -1847,7 +1847,7 @@ static int comm_reduce_sendbuf_impl(fmi_comm_t comm, int op, int dtype, int alg,
     hipStream_t s = resolve_stream(stream);
     const size_t esz = dtype_size(dtype);
     const bool is_root = c->t->rank() == root;
-    if (N > 1) {
+    if (N > 1 || tune(FMI_TUNE_COMM_ONE_RANK_EXCHANGE)) {
         const size_t shard = shard_elems(n, N);
         const size_t padded = shard * N;
         const bool ragged = padded != n && c->t->ragged();  // short last shards at their own length
@@ -1899,7 +1899,7 @@ static int comm_scan_impl(fmi_comm_t comm, int op, int dtype, int alg, const voi
     hipStream_t s = resolve_stream(stream);
     const int N = c->t->n();
     const size_t esz = dtype_size(dtype);
-    if (N == 1) {
+    if (N == 1 && !tune(FMI_TUNE_COMM_ONE_RANK_EXCHANGE)) {
         if (send != recv) FMI_COMM_RC(device_copy(recv, send, n * esz, s));
         return FMI_OK;
     }

@@ -37,12 +37,13 @@ DeviceState g_state;  // one process drives one device (one process per GPU, as 
 
 // Defaults from tools/tune_pair.py on MI355X (C2, 256 MiB f32): nontemporal one-shot tiles, 4 × 16 B per
 // operand per thread, 256-thread workgroups — 125 µs = 6.4 TB/s vs 142 µs for plain loads/stores.
-std::atomic<long long> g_tune[13] = {2 /*variant: nontemporal tiles*/, 4 /*unroll*/, 256 /*block*/,
+std::atomic<long long> g_tune[14] = {2 /*variant: nontemporal tiles*/, 4 /*unroll*/, 256 /*block*/,
                                      8 /*grid per CU*/, 64ll << 20 /*host chunk*/, 1 /*host zero-copy*/,
                                      64 /*fused in-flight KiB per CU (tools/ab_fused_cap.py)*/,
                                      1 /*one-pass blocked scan*/, 0 /*ncclAllToAll*/, 0 /*ncclAllGather*/,
                                      0 /*no allreduce pipelining*/, 1 /*fused kernels: buffer ops where measured faster*/,
-                                     1 /*pairwise: tiles t % 8 < 1 (one XCD) store sc1 (tools/ab_pair_sc1.py)*/};
+                                     1 /*pairwise: tiles t % 8 < 1 (one XCD) store sc1 (tools/ab_pair_sc1.py)*/,
+                                     0 /*one-rank communicators copy*/};
 
 int hip_fail(const char* what, hipError_t e) {
     return fail(FMI_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
@@ -1331,6 +1332,9 @@ int fmi_tune_set(int key, long long value) {
         case FMI_TUNE_PAIR_SC1_OF_8:
             if (value < 0 || value > 8) return fail(FMI_ERR_INVALID, "pair sc1 tiles per 8 must be in [0, 8]");
             break;
+        case FMI_TUNE_COMM_ONE_RANK_EXCHANGE:
+            if (value != 0 && value != 1) return fail(FMI_ERR_INVALID, "one-rank exchange must be 0 or 1");
+            break;
         default: return fail(FMI_ERR_INVALID, "unknown tuning key");
     }
     g_tune[key].store(value);
@@ -1338,7 +1342,7 @@ int fmi_tune_set(int key, long long value) {
 }
 
 int fmi_tune_get(int key, long long* value) {
-    if (!value || key < 0 || key > FMI_TUNE_PAIR_SC1_OF_8) return fail(FMI_ERR_INVALID, "bad tuning query");
+    if (!value || key < 0 || key > FMI_TUNE_COMM_ONE_RANK_EXCHANGE) return fail(FMI_ERR_INVALID, "bad tuning query");
     *value = g_tune[key].load();
     return FMI_OK;
 }

@@ -367,11 +367,16 @@ typedef enum {
                                     loads nt with sc1 (tree) / nt sc1 (scan) stores; 0 = global_load /
                                     global_store nt; 1 = auto (default): 2 for trees of >= 4 and scans of
                                     >= 8 peers, 0 otherwise (tools/ab_fused_policy.py). Same bits always */
-    FMI_TUNE_PAIR_SC1_OF_8 = 12   /* pairwise kernel (16-B aligned buckets, one-shot tiles): tiles t with
+    FMI_TUNE_PAIR_SC1_OF_8 = 12,  /* pairwise kernel (16-B aligned buckets, one-shot tiles): tiles t with
                                     t % 8 < k store with sc1 instead of nontemporal (k = 0..8). Consecutive
                                     workgroups are dispatched to different XCDs, so k of the 8 XCDs store sc1.
                                     Default 1 (tools/ab_pair_sc1.py, measured with no MALL re-use). Same bits
                                     always */
+    FMI_TUNE_COMM_ONE_RANK_EXCHANGE = 13 /* 1: a ONE-rank communicator runs the full sharded schedule —
+                                    all-to-all, shard kernel, all-gather / gather / all-to-all back, RCCL
+                                    reduce-scatter, window mapping, the pipelined split — exchanging with
+                                    itself, instead of the reference's P = 1 copy. Same bits; exists so that
+                                    a 1-GPU box runs the RCCL transport's real collectives (tests). Default 0 */
 } fmi_tune_key_t;
 int fmi_tune_set(int key, long long value);
 int fmi_tune_get(int key, long long* value);

@@ -154,7 +154,7 @@ def test_tuning_knobs_validate():
     for bad in (-1, 9):
         with pytest.raises(fmi_amd.FmiError):
             fmi_amd.tune_set(fmi_amd.Tune.PAIR_SC1_OF_8, bad)
-    for key in (fmi_amd.Tune.COMM_A2A, fmi_amd.Tune.COMM_GATHER):  # RCCL exchange realisations
+    for key in (fmi_amd.Tune.COMM_A2A, fmi_amd.Tune.COMM_GATHER, fmi_amd.Tune.COMM_ONE_RANK_EXCHANGE):
         assert fmi_amd.tune_get(key) == 0
         fmi_amd.tune_set(key, 1)
         assert fmi_amd.tune_get(key) == 1
