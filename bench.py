@@ -90,7 +90,8 @@ def parse():
                     help="N>1: seconds the measurement up to `value` (setup, warm-up, timed steps, self-check) may "
                          "take; past it the rank names the phase it is stuck in on stderr and exits with status 3")
     ap.add_argument("--force-dist", action="store_true",
-                    help="run the N>1 code path (fmi_comm over RCCL) even at world size 1 — plumbing check")
+                    help="run the N>1 code path (fmi_comm over RCCL) even at world size 1 — plumbing check; the one "
+                         "rank then runs the full exchange with itself (FMI_TUNE_COMM_ONE_RANK_EXCHANGE)")
     ap.add_argument("--cpu-reps", type=int, default=30, help="adapter combines timed (≈10 s of CPU work)")
     return ap.parse_args()
 
@@ -563,6 +564,9 @@ def run_dist(args, world, rank, local_rank):
     from fmi_amd.collectives import CommAllreduce
 
     fmi_amd.init(dev)
+    one_rank_exchange = args.force_dist and world == 1
+    if one_rank_exchange:  # the plumbing check runs the real exchange (RCCL calls with itself), not the P = 1 copy
+        fmi_amd.tune_set(fmi_amd.Tune.COMM_ONE_RANK_EXCHANGE, 1)
     watch.enter("fmi_comm init (communicator id broadcast, RCCL init)")
     ar = CommAllreduce(dist.group.WORLD, path=args.path, transport=args.transport)
     watch.enter("topology check")
@@ -601,6 +605,9 @@ def run_dist(args, world, rank, local_rank):
                      f"{world} GPUs, one peer per GPU, buckets sharded {world} ways; path {args.path}: "
                      f"{path_desc[args.path]}; transport {args.transport}", n, roof)
     line["config"]["topology"] = topo
+    if one_rank_exchange:
+        line["config"]["one_rank_exchange"] = ("FMI_TUNE_COMM_ONE_RANK_EXCHANGE = 1: the one rank runs the full "
+                                               "sharded exchange with itself (RCCL calls), not the P = 1 copy")
     line["config"].update({"rotating_sets": args.dist_sets, "numa_binding_rank0": numa, "peers": world,
                            "path": args.path, "transport": args.transport,
                            "algbw_GiB_s": extra["algbw_GiB_s"], "busbw_GiB_s": extra["busbw_GiB_s"],

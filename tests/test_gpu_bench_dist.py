@@ -130,4 +130,6 @@ def test_bench_py_force_dist_rccl_world1():
     assert len(lines) == 1, r.stdout  # RCCL's version banner goes to stderr (bench.claim_stdout)
     line = json.loads(lines[0])
     assert line["config"]["topology"]["rccl_ranks"] == 1
+    assert "one_rank_exchange" in line["config"] and line["self_check"]["ok"] and line["c4"]["tree"]["self_check"]["ok"]
+    assert line["c4"]["rccl"]["self_check"]["ok"]  # ncclReduceScatter + ncclAllGather with one rank
     _check_topology_and_anchor(line, 1, "rccl")

@@ -23,7 +23,8 @@ def algorithmic_bytes(kernel: str, write_bytes: float):
     """Algorithmic HBM bytes of one launch, from the launch's output bytes, which every
     kernel here writes exactly once: pair a = a (+) b reads 2 and writes 1 bucket (3 x out); the fused P-way
     tree reads P buckets and writes one (P + 1 x out); the peer-axis scan reads P and writes P (2 x out); the
-    synthetic-input generator only writes (1 x out); a buffer copy reads and writes (2 x out). The output is
+    synthetic-input generator only writes (1 x out); a buffer copy (the runtime's, or the library's copy_tile)
+    reads and writes (2 x out). The output is
     rounded to whole 4 KiB pages first (a WRITE_SIZE median carries a few hundred stray bytes). None for a
     kernel of another shape."""
     out = round(write_bytes / 4096) * 4096
@@ -36,7 +37,7 @@ def algorithmic_bytes(kernel: str, write_bytes: float):
         return 2 * out
     if "synth_kernel<" in kernel:
         return out
-    if "copyBuffer" in kernel:
+    if "copyBuffer" in kernel or "copy_tile<" in kernel:
         return 2 * out
     return None
 
