@@ -78,33 +78,50 @@ def main():
     stats = glob.glob(os.path.join(args.trace, "*_kernel_stats.csv"))
     if stats:
         shutil.copy(stats[0], os.path.join(args.out, f"{args.tag}_kernel_stats.csv"))
-    fetch = {}
+    # Launches are grouped by (kernel, grid size): one instantiation launched at several shapes in one run
+    # (copy_tile at 256 MiB and at the 64 MiB host-pipeline chunks) gives one entry per shape, never a median
+    # across shapes.
+    def grid_of(r):
+        if "Grid_Size" in r:
+            return int(float(r["Grid_Size"]))
+        return int(float(r["Grid_Size_X"])) * int(float(r["Grid_Size_Y"])) * int(float(r["Grid_Size_Z"]))
+
+    fetch, write = {}, {}
     for r in _rows(os.path.join(args.fetch, "*_counter_collection.csv")):
         if r["Counter_Name"] == "FETCH_SIZE":
-            fetch.setdefault(r["Kernel_Name"], []).append(float(r["Counter_Value"]))
-    write = {}
+            fetch.setdefault((r["Kernel_Name"], grid_of(r)), []).append(float(r["Counter_Value"]))
     for r in _rows(os.path.join(args.write, "*_counter_collection.csv")):
         if r["Counter_Name"] == "WRITE_SIZE":
-            write.setdefault(r["Kernel_Name"], []).append(float(r["Counter_Value"]))
+            write.setdefault((r["Kernel_Name"], grid_of(r)), []).append(float(r["Counter_Value"]))
     durations = {}
-    if stats:
+    traces = glob.glob(os.path.join(args.trace, "*_kernel_trace.csv"))
+    if traces:
+        per = {}
+        for r in _rows(traces[0]):
+            per.setdefault((r["Kernel_Name"], grid_of(r)), []).append(float(r["End_Timestamp"]) - float(r["Start_Timestamp"]))
+        for key, ns in per.items():
+            durations[key] = dict(calls=len(ns), avg_ns=statistics.fmean(ns), median_ns=statistics.median(ns),
+                                  min_ns=min(ns), max_ns=max(ns), source="kernel_trace.csv, this shape")
+    elif stats:
         for r in _rows(stats[0]):
-            durations[r["Name"]] = dict(calls=int(r["Calls"]), avg_ns=float(r["AverageNs"]),
-                                        min_ns=float(r["MinNs"]), max_ns=float(r["MaxNs"]))
+            durations[(r["Name"], None)] = dict(calls=int(r["Calls"]), avg_ns=float(r["AverageNs"]),
+                                                min_ns=float(r["MinNs"]), max_ns=float(r["MaxNs"]),
+                                                source="kernel_stats.csv, every shape of this kernel")
     kernels = []
-    for name in sorted(set(fetch) | set(write)):
-        f_kib = statistics.median(fetch.get(name, [0.0]))
-        w_kib = statistics.median(write.get(name, [0.0]))
+    for name, grid in sorted(set(fetch) | set(write)):
+        f_kib = statistics.median(fetch.get((name, grid), [0.0]))
+        w_kib = statistics.median(write.get((name, grid), [0.0]))
         kernels.append({
             "kernel": name,
-            "launches_profiled": max(len(fetch.get(name, [])), len(write.get(name, []))),
+            "grid_size": grid,
+            "launches_profiled": max(len(fetch.get((name, grid), [])), len(write.get((name, grid), []))),
             "fetch_size_kib_median": f_kib,
             "write_size_kib_median": w_kib,
             "hbm_read_bytes_per_launch": int(round(2 * f_kib * 1024)),
             "hbm_write_bytes_per_launch": int(round(w_kib * 1024)),
             "hbm_bytes_per_launch": int(round(2 * f_kib * 1024 + w_kib * 1024)),
             "algorithmic_bytes_per_launch": algorithmic_bytes(name, w_kib * 1024),
-            "trace": durations.get(name),
+            "trace": durations.get((name, grid)) or durations.get((name, None)),
         })
     summary = {
         "source": f"profiles/{args.tag}: rocprofv3 separate --pmc FETCH_SIZE / --pmc WRITE_SIZE passes, "
