@@ -302,3 +302,21 @@ def test_python_enums_match_the_header():
         declared = {k for k in consts if k.startswith(prefix)}
         if prefix not in ("FMI_",):  # every header enumerator of the group is bound in Python
             assert declared == {prefix + m.name for m in enum_cls}, (prefix, declared ^ {prefix + m.name for m in enum_cls})
+
+
+def test_host_out_of_memory_is_a_status_not_a_crash():
+    """No C++ exception crosses the C-ABI (include/fmi_dev.h entry points run under a guard): building a
+    16,777,216-peer allreduce program under a 3 GiB address-space limit throws std::bad_alloc inside the
+    library, which must come back as FMI_ERR_ALLOC with a message instead of std::terminate killing the caller."""
+    import subprocess
+    import sys
+
+    code = (f"import resource, ctypes, sys\nsys.path.insert(0, {ROOT!r})\n"
+            "from fmi_amd import _lib\nlib = _lib.load()\n"
+            "resource.setrlimit(resource.RLIMIT_AS, (3 << 30, 3 << 30))\n"
+            "buf = ctypes.create_string_buffer(64)\n"
+            "rc = lib.fmi_schedule_expr(0, 1 << 24, 0, buf, 64)\n"
+            "print(rc, _lib.last_error())\n")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.split()[0] == str(_lib.FMI_ERR_ALLOC) and "out of host memory" in r.stdout
