@@ -10,6 +10,10 @@
 //   copy8_2ph  copy8 storing outputs 0..3 of the tile first, then 4..7, the loads of 4..7 after the first
 //              stores (4 + 4 write streams per phase)
 //   scan8      the library's own peer scan (fmi_dev_scan_peers, scan_no_order, f32 sum) on the same buckets
+//   copy8_xcd  copy8 with an XCD-contiguous tile order: workgroup b (dispatched to XCD b % 8) copies tile
+//              (b % 8) * T/8 + b / 8, so each XCD streams its own eighth of every bucket instead of all XCDs
+//              sharing one moving window (does DRAM locality improve on the slow placements?)
+//   pair3 / pair3_xcd   C2's shape (2 reads + 1 write, f32 sum) on buckets 0..2 of the set, both tile orders
 // Draws: each draw allocates a fresh set of 2 x 16 x 64 MiB buckets (two rotating sets, 2 GiB, beyond the
 // 256 MB MALL), so placement varies draw to draw as it does between callers; per draw, the kernels run
 // interleaved over R rounds of K back-to-back launches (events), median per kernel.
@@ -62,6 +66,40 @@ __global__ void __launch_bounds__(256) copy8(Ptrs16 b) {
     for (int p = 0; p < kP; ++p)
 #pragma unroll
         for (int u = 0; u < kU; ++u) st(b.out[p] + base + u * 256, v[p][u]);
+}
+
+__device__ __forceinline__ size_t xcd_tile(unsigned b, unsigned tiles) {
+    const unsigned per = tiles / 8;  // tiles % 8 == 0 (64 MiB buckets)
+    return static_cast<size_t>(b % 8) * per + b / 8;
+}
+
+__global__ void __launch_bounds__(256) copy8_xcd(Ptrs16 b) {
+    const size_t base = xcd_tile(blockIdx.x, gridDim.x) * kU * 256 + threadIdx.x;
+    V v[kP][kU];
+#pragma unroll
+    for (int p = 0; p < kP; ++p)
+#pragma unroll
+        for (int u = 0; u < kU; ++u) v[p][u] = ld(b.in[p] + base + u * 256);
+#pragma unroll
+    for (int p = 0; p < kP; ++p)
+#pragma unroll
+        for (int u = 0; u < kU; ++u) st(b.out[p] + base + u * 256, v[p][u]);
+}
+
+template <bool XCD>
+__global__ void __launch_bounds__(256) pair3(Ptrs16 b) {
+    const size_t t = XCD ? xcd_tile(blockIdx.x, gridDim.x) : blockIdx.x;
+    const size_t base = t * kU * 256 + threadIdx.x;
+    using F4 = float __attribute__((ext_vector_type(4)));
+    V x[kU], y[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+        x[u] = ld(b.in[0] + base + u * 256);
+        y[u] = ld(b.in[1] + base + u * 256);
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u)
+        st(b.out[0] + base + u * 256, __builtin_bit_cast(V, __builtin_bit_cast(F4, x[u]) + __builtin_bit_cast(F4, y[u])));
 }
 
 __global__ void __launch_bounds__(256) copy8_2ph(Ptrs16 b) {
@@ -149,6 +187,9 @@ int main(int argc, char** argv) {
         std::vector<Kernel> ks = {
             {"copy8", rw, [&](int k) { copy8<<<grid, 256, 0, s>>>(sets[k & 1]); }, {}},
             {"copy8_2ph", rw, [&](int k) { copy8_2ph<<<grid, 256, 0, s>>>(sets[k & 1]); }, {}},
+            {"copy8_xcd", rw, [&](int k) { copy8_xcd<<<grid, 256, 0, s>>>(sets[k & 1]); }, {}},
+            {"pair3", 3.0 * kBytes, [&](int k) { pair3<false><<<grid, 256, 0, s>>>(sets[k & 1]); }, {}},
+            {"pair3_xcd", 3.0 * kBytes, [&](int k) { pair3<true><<<grid, 256, 0, s>>>(sets[k & 1]); }, {}},
             {"read16", rw, [&](int k) { read16<<<grid, 256, 0, s>>>(sets[k & 1], sink); }, {}},
             {"write16", rw, [&](int k) { write16<<<grid, 256, 0, s>>>(sets[k & 1]); }, {}},
             {"scan8", rw, [&](int k) {
