@@ -349,37 +349,46 @@ def run_single(args):
     print(json.dumps(line), file=json_out(), flush=True)
 
 
-def one_peer_allreduce(n: int, launches: int = 20) -> dict:
+def one_peer_allreduce(n: int, launches: int = 20, sets: int = 4) -> dict:
     """The N = 1 point of the N > 1 curve's own workload: fmi_comm_allreduce of one 256 MiB bucket on a
     one-rank communicator — the reference's P = 1 allreduce (PeerToPeer.cpp:96-130 with P = 1) is a copy
-    of the bucket into recvbuf (2·S HBM bytes). Events around back-to-back calls on the library stream."""
+    of the bucket into recvbuf (2·S HBM bytes). Events around back-to-back calls on the library stream,
+    rotating over `sets` (send, recv) pairs: the copy stores with sc1, so a recv bucket is rewritten only
+    after (sets - 1) x 256 MiB of other writes have passed through the 256 MB MALL."""
     import numpy as np
 
     from fmi_amd import Bucket, Event, Op
     from fmi_amd.comm import Comm, Transport, unique_id
 
     comm = Comm(unique_id(Transport.LOCAL), 1, 0)
-    src, dst = Bucket(n, np.float32).fill_synthetic(11, 0), Bucket(n, np.float32)
+    pairs = [(Bucket(n, np.float32).fill_synthetic(11 + s, 0), Bucket(n, np.float32)) for s in range(sets)]
     try:
-        comm.allreduce(Op.SUM, src, dst)
+        for src, dst in pairs:
+            comm.allreduce(Op.SUM, src, dst)
         e0, e1 = Event(), Event()
         e0.record()
-        for _ in range(launches):
+        for k in range(launches):
+            src, dst = pairs[k % sets]
             comm.allreduce(Op.SUM, src, dst)
         e1.record()
         e1.sync()
         ms = e0.elapsed_ms(e1) / launches
         e0.destroy()
         e1.destroy()
-        ok = bool(np.array_equal(src.view(0, 4096).numpy().view(np.uint32), dst.view(0, 4096).numpy().view(np.uint32)))
+        ok = all(bool(np.array_equal(s.view(0, 4096).numpy().view(np.uint32), d.view(0, 4096).numpy().view(np.uint32)))
+                 and bool(np.array_equal(s.view(n - 4096, 4096).numpy().view(np.uint32),
+                                         d.view(n - 4096, 4096).numpy().view(np.uint32)))
+                 for s, d in pairs)
     finally:
-        src.free()
-        dst.free()
+        for src, dst in pairs:
+            src.free()
+            dst.free()
         comm.destroy()
     S = n * 4
     return {"workload": f"fmi_comm_allreduce, 1 rank, {S >> 20} MiB f32 (the reference's P = 1 allreduce: a copy)",
             "ms": round(ms, 4), "GiB_s_reduced_buckets": round(S / GIB / (ms * 1e-3), 2),
-            "hbm_frac": round(2 * S / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "result_ok": ok, "launches": launches}
+            "hbm_frac": round(2 * S / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "result_ok": ok, "launches": launches,
+            "rotating_sets": sets}
 
 
 C3_PAIR_SETS = 64  # 63 x 8 MiB of sc1 tile writes between two uses of a set (see --sets)

@@ -213,6 +213,40 @@ __device__ __forceinline__ void store_tile(void* bucket, size_t tile_byte, unsig
                                            lane_byte, 0, AUX);
 }
 
+// Device copy (device_copy in fmi_dev.hip: the reference's P = 1 allreduce and every staging copy of the
+// communicator): the pair tile's shape with one stream in and one out — U 16-B vectors per thread, one tile
+// per workgroup. Whole tiles load nontemporal and store with sc1 through a buffer descriptor (the tree kernel's
+// policy, above): 4.6 % faster than global nontemporal stores at 256 MiB, 3 % at 64 MiB, with no set
+// re-read from the MALL (tools/microbench_copypol.hip, profiles/r03_copypol.jsonl). The partial last tile
+// goes through bounds-checked global accesses; workgroup 0 copies the sub-16-B tail. Algorithmic HBM bytes:
+// 2 x bytes. Both pointers 16-B aligned.
+template <int U>
+__global__ void __launch_bounds__(256) copy_tile(char* out, const char* in, size_t bytes) {
+    const size_t nvec = bytes / 16;
+    const size_t base = static_cast<size_t>(blockIdx.x) * U * 256 + threadIdx.x;
+    if (static_cast<size_t>(blockIdx.x + 1) * U * 256 <= nvec) {
+        const size_t tile_byte = static_cast<size_t>(blockIdx.x) * U * 256 * 16;
+        Lanes<unsigned, 4> v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            v[u] = load_tile<kAuxNT, unsigned, 4>(in, tile_byte, static_cast<unsigned>((u * 256 + threadIdx.x) * 16));
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            store_tile<kAuxSC1, unsigned, 4>(out, tile_byte, static_cast<unsigned>((u * 256 + threadIdx.x) * 16), v[u]);
+    } else {
+        const u32x4* src = reinterpret_cast<const u32x4*>(in);
+        u32x4* dst = reinterpret_cast<u32x4*>(out);
+        u32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (base + u * 256 < nvec) v[u] = __builtin_nontemporal_load(src + base + u * 256);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (base + u * 256 < nvec) __builtin_nontemporal_store(v[u], dst + base + u * 256);
+    }
+    if (blockIdx.x == 0 && nvec * 16 + threadIdx.x < bytes) out[nvec * 16 + threadIdx.x] = in[nvec * 16 + threadIdx.x];
+}
+
 // ---------------------------------------------------------------------------------------------------
 // Pairwise combine. A "tile" is U vectors per thread: thread t of block b owns vectors
 // b*U*B + u*B + t (u < U), so each of the U wave-instructions is one contiguous 1-KiB access and each
@@ -272,33 +306,6 @@ __device__ __forceinline__ void pair_tail(T* out, const T* a, const T* b, size_t
         const size_t i = first + threadIdx.x;
         out[i] = Op::template apply<T>(a[i], b[i]);
     }
-}
-
-// Device copy (device_copy in fmi_dev.hip: the reference's P = 1 allreduce and every staging copy of the
-// communicator): the pair tile's access pattern with one stream in and one out — U 16-B vectors per thread,
-// nontemporal loads and stores, one tile per workgroup; workgroup 0 copies the sub-16-B tail. Algorithmic
-// HBM bytes: 2 x bytes. Both pointers 16-B aligned.
-template <int U>
-__global__ void __launch_bounds__(256) copy_tile(char* out, const char* in, size_t bytes) {
-    const size_t nvec = bytes / 16;
-    const size_t base = static_cast<size_t>(blockIdx.x) * U * 256 + threadIdx.x;
-    const u32x4* src = reinterpret_cast<const u32x4*>(in);
-    u32x4* dst = reinterpret_cast<u32x4*>(out);
-    u32x4 v[U];
-    if (static_cast<size_t>(blockIdx.x + 1) * U * 256 <= nvec) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) v[u] = __builtin_nontemporal_load(src + base + u * 256);
-#pragma unroll
-        for (int u = 0; u < U; ++u) __builtin_nontemporal_store(v[u], dst + base + u * 256);
-    } else {
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-            if (base + u * 256 < nvec) v[u] = __builtin_nontemporal_load(src + base + u * 256);
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-            if (base + u * 256 < nvec) __builtin_nontemporal_store(v[u], dst + base + u * 256);
-    }
-    if (blockIdx.x == 0 && nvec * 16 + threadIdx.x < bytes) out[nvec * 16 + threadIdx.x] = in[nvec * 16 + threadIdx.x];
 }
 
 // One-shot grid: one tile per workgroup. Pointers must be 16-B aligned. Whole tiles t with t % 8 < sc1_k

@@ -114,3 +114,40 @@ def test_python_api_custom_op_follows_reference_order(device, P):
     for p in range(P):
         assert r[p][0] == ar[p] and r[p][1] == ltr[p] and r[p][2] == sc[p]
     assert r[P - 1][3] == red
+
+
+def test_absent_peer_raises_fmi_timeout(device):
+    """The reference's Python API raises fmi.Timeout when a peer stays away (reference channels:
+    include/utils/Common.h:11-15, src/comm/Direct.cpp:28-30), bounded by the config's max_timeout: peer 1 joins
+    and never calls the allreduce; peer 0's allreduce raises fmi.Timeout after ≈ 1 s, not a hang."""
+    import time
+
+    import fmi_amd.fmi as fmi
+
+    with tempfile.TemporaryDirectory() as d:
+        cfg = os.path.join(d, "fmi.json")
+        json.dump({"backends": {"Local": {"enabled": True, "rendezvous_dir": d, "max_timeout": 1000}}}, open(cfg, "w"))
+        out, errors = {}, []
+        joined = threading.Event()
+
+        def absent():
+            try:
+                comm = fmi.Communicator(1, 2, cfg, "timeout", 512)
+                joined.set()
+                time.sleep(4.0)
+                comm.finalize()
+            except BaseException as e:  # noqa: BLE001
+                errors.append(e)
+
+        t = threading.Thread(target=absent)
+        t.start()
+        comm = fmi.Communicator(0, 2, cfg, "timeout", 512)
+        assert joined.wait(60)
+        t0 = time.monotonic()
+        with pytest.raises(fmi.Timeout):
+            comm.allreduce([1.5, 2.5], fmi.func(fmi.op.sum), fmi.types(fmi.datatypes.double_list, 2))
+        out["waited"] = time.monotonic() - t0
+        comm.finalize()
+        t.join(timeout=60)
+        assert not errors, errors
+        assert 0.9 <= out["waited"] < 20, out
