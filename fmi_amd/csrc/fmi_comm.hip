@@ -82,8 +82,6 @@ struct RcclApi {
     ncclResult_t (*AllReduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t);
     // RCCL's native all-to-all (optional symbol; grouped send/recv otherwise)
     ncclResult_t (*AllToAll)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t);
-    // optional: a second communicator for the pipelined allreduce (FMI_TUNE_COMM_PIPELINE)
-    ncclResult_t (*CommSplit)(ncclComm_t, int, int, ncclComm_t*, ncclConfig_t*);
     // optional: bounded waits (non-blocking init, asynchronous errors, abort on timeout) and introspection
     ncclResult_t (*CommInitRankConfig)(ncclComm_t*, int, ncclUniqueId, int, ncclConfig_t*);
     ncclResult_t (*CommGetAsyncError)(ncclComm_t, ncclResult_t*);
@@ -127,7 +125,6 @@ const RcclApi* rccl_api() {
         FMI_RCCL_SYM(AllReduce)
 #undef FMI_RCCL_SYM
         api.AllToAll = reinterpret_cast<decltype(api.AllToAll)>(dlsym(h, "ncclAllToAll"));
-        api.CommSplit = reinterpret_cast<decltype(api.CommSplit)>(dlsym(h, "ncclCommSplit"));
 #define FMI_RCCL_OPT(name) api.name = reinterpret_cast<decltype(api.name)>(dlsym(h, "nccl" #name));
         FMI_RCCL_OPT(CommInitRankConfig)
         FMI_RCCL_OPT(CommGetAsyncError)
@@ -281,7 +278,7 @@ public:
     static size_t span(int j, size_t shard, size_t total) { return plan::span(j, shard, total); }
     // A second communicator over the same ranks (collective), so two exchanges can be in flight at once on
     // two streams. nullptr: this transport's exchanges are host-synchronous, use it as is.
-    virtual int split(std::unique_ptr<Transport>* out) {
+    virtual int split(std::unique_ptr<Transport>* out, hipStream_t) {
         out->reset();
         return FMI_OK;
     }
@@ -492,15 +489,36 @@ public:
         for (int j = 0; j < static_cast<int>(peers.size()); ++j)
             if (j != rank_ && peers[j]) (void)hipIpcCloseMemHandle(peers[j]);
     }
-    int split(std::unique_ptr<Transport>* out) override {
-        if (!api_->CommSplit) return fail(FMI_ERR_UNSUPPORTED, "librccl lacks ncclCommSplit");
+    // The second communicator is made like the first: rank 0 draws a fresh id, this communicator broadcasts
+    // it on s, every rank joins it (non-blocking init bounded by the timeout when this one is non-blocking).
+    // Not ncclCommSplit: with a non-blocking parent the child's handle is published asynchronously, and the
+    // librccl torch ships (2.26) handed back a handle that was not valid yet (ncclCommGetAsyncError: invalid
+    // argument), with the library's pointer to it written later by RCCL's own thread.
+    int split(std::unique_ptr<Transport>* out, hipStream_t s) override {
+        ncclUniqueId id{};
+        if (rank_ == 0) FMI_RCCL(GetUniqueId(&id));
+        char* d = nullptr;
+        FMI_COMM_HIP(hipMalloc(&d, sizeof(id)));
+        const int rc = [&]() -> int {
+            FMI_COMM_HIP(hipMemcpyAsync(d, &id, sizeof(id), hipMemcpyHostToDevice, s));
+            FMI_RCCL(Broadcast(d, d, sizeof(id), ncclUint8, 0, comm_, s));
+            FMI_COMM_HIP(hipMemcpyAsync(&id, d, sizeof(id), hipMemcpyDeviceToHost, s));
+            return wait_stream(s, "second communicator (id broadcast)");
+        }();
+        if (!aborted_) (void)hipFree(d);
+        FMI_COMM_RC(rc);
         ncclComm_t nc = nullptr;
-        // a non-blocking parent makes a non-blocking child (config inherited): wait on the child
-        const ncclResult_t r = api_->CommSplit(comm_, 0, rank_, &nc, nullptr);
-        if (r != ncclSuccess && r != ncclInProgress) return nccl_fail(api_, "ncclCommSplit", r);
+        if (nonblocking_) {
+            ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+            cfg.blocking = 0;
+            const ncclResult_t r = api_->CommInitRankConfig(&nc, n_, id, rank_, &cfg);
+            if (r != ncclSuccess && r != ncclInProgress) return nccl_fail(api_, "ncclCommInitRankConfig (second)", r);
+        } else {
+            FMI_NCCL(api_, CommInitRank(&nc, n_, id, rank_));
+        }
         auto child = std::make_unique<RcclTransport>(api_, nc, n_, rank_, nonblocking_);
         child->set_timeout(timeout_s_);
-        FMI_COMM_RC(child->wait_ready("ncclCommSplit"));
+        FMI_COMM_RC(child->wait_ready("ncclCommInitRankConfig (second communicator)"));
         *out = std::move(child);
         return FMI_OK;
     }
@@ -1078,14 +1096,14 @@ struct Window {
 struct ChunkPipe {
     std::unique_ptr<Transport> t2;  // nullptr with LOCAL / PROC: their exchanges are host-synchronous
     bool split_done = false;
-    bool no_split = false;  // the transport cannot split (librccl without ncclCommSplit): never pipeline
+    bool no_split = false;  // the transport could not make a second communicator: never pipeline
     hipStream_t gs = nullptr;  // all-gathers
     hipEvent_t reduced[2] = {}, gathered[2] = {}, start = nullptr;
     bool ready = false;
 
-    int init(Transport* t) {
+    int init(Transport* t, hipStream_t s) {
         if (!split_done) {
-            const int rc = t->split(&t2);
+            const int rc = t->split(&t2, s);
             if (rc == FMI_ERR_UNSUPPORTED) no_split = true;  // every rank loads the same librccl: all fall back
             if (rc != FMI_OK) return rc;
             split_done = true;
@@ -1351,7 +1369,7 @@ int allreduce_tree_pipelined(Comm* c, int op, int dtype, int alg, const void* se
     const int N = c->t->n();
     const size_t esz = dtype_size(dtype);
     ChunkPipe& p = c->chunks;
-    FMI_COMM_RC(p.init(c->t.get()));
+    FMI_COMM_RC(p.init(c->t.get(), s));
     Transport* tg = p.t2 ? p.t2.get() : c->t.get();
     const size_t step = kShardAlign * static_cast<size_t>(N);
     const size_t ce = ((n + K - 1) / K + step - 1) / step * step;  // chunk elements, whole shards
@@ -1427,7 +1445,7 @@ int allreduce_device(Comm* c, int op, int dtype, int alg, int path, const void* 
         // path below runs (same bits)
         if (K >= 2 && n * esz / static_cast<size_t>(K) >= (size_t(1) << 20) * static_cast<size_t>(N) &&
             !c->chunks.no_split) {
-            const int rc = c->chunks.init(c->t.get());
+            const int rc = c->chunks.init(c->t.get(), s);
             if (rc == FMI_OK) return allreduce_tree_pipelined(c, op, dtype, alg, send, recv, n, s, static_cast<size_t>(K));
             if (rc != FMI_ERR_UNSUPPORTED) return rc;
         }

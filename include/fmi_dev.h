@@ -359,9 +359,10 @@ typedef enum {
                                     same value (as FMI_TUNE_COMM_A2A) */
     FMI_TUNE_COMM_PIPELINE = 10,  /* EXPERIMENTAL (not yet run over RCCL with more than one rank). Path TREE
                                     allreduce in K chunks (0 or 1 = off, default; 2..64): chunk k's
-                                    all-gather runs on a second stream and communicator (ncclCommSplit)
+                                    all-gather runs on a second stream and a second communicator (made
+                                    once: a fresh id broadcast over the first, then a bounded init)
                                     while chunk k + 1's all-to-all and kernel run; chunks of >= 1 MiB per
-                                    rank only. A librccl without ncclCommSplit runs the unpipelined path.
+                                    rank only. If the second communicator cannot be made, the unpipelined path runs.
                                     Same bits (element-wise); EVERY rank must set the same K */
     FMI_TUNE_FUSED_POLICY = 11,   /* fused P-way kernels (tree, scan; <= 16 peers), 16-B accesses: 2 = buffer
                                     loads nt with sc1 (tree) / nt sc1 (scan) stores; 0 = global_load /

@@ -4,6 +4,7 @@ The schedules (shard layout, padding, all-to-all, fused kernel in the reference'
 gather / all-to-all back) are exactly those the RCCL transport runs across GPUs; the result of every rank
 is compared bit-exactly with the oracle's simulation of the reference collective over the same buckets.
 """
+import os
 import threading
 
 import numpy as np
@@ -457,77 +458,25 @@ def test_comm_rccl_transport_single_rank(device):
     c.destroy()
 
 
-def test_comm_rccl_one_rank_runs_the_full_exchange(device):
+@pytest.mark.parametrize("torch_first", [False, True], ids=["system_librccl", "torch_librccl"])
+def test_comm_rccl_one_rank_runs_the_full_exchange(device, torch_first):
     """FMI_TUNE_COMM_ONE_RANK_EXCHANGE: a one-rank RCCL communicator (non-blocking init) runs the full sharded
     schedule against itself — ncclAllToAll / grouped send-recv, the shard kernel, ncclAllGather / grouped
     send-recv, ncclReduceScatter (path RCCL), the IPC window exchange (path DIRECT), the second communicator
-    of the pipelined allreduce (ncclCommSplit), reduce / reduce_sendbuf / scan, the host pipeline — so a
-    1-GPU box executes the RCCL calls the 8-GPU run makes. Every result is the reference's P = 1 result (a
-    copy of the rank's own bucket, PeerToPeer.cpp:96-184 with one peer), bit for bit."""
-    Tn = fmi_amd.Tune
-    uid = unique_id(Transport.RCCL)
-    c = Comm(uid, 1, 0, timeout_s=120)
-    q = c.query()
-    assert q["count"] == 1 and q["rank"] == 0
-    fmi_amd.tune_set(Tn.COMM_ONE_RANK_EXCHANGE, 1)
-    try:
-        for dtype, op in ((np.float32, Op.SUM), (np.float64, Op.MAX), (np.int64, Op.MIN)):
-            for n in (4099, 64 * 1024, (1 << 20) + 64):
-                x = inputs(dtype, n, 0, seed=71)
-                s, out = Bucket.from_numpy(x), Bucket(n, dtype)
-                variants = [(a2a, gather, 0) for a2a in (0, 1) for gather in (0, 1)]
-                if n >= (1 << 20):
-                    variants.append((0, 0, 4))  # pipelined: a second, split communicator on a second stream
-                for a2a, gather, pipe in variants:
-                    fmi_amd.tune_set(Tn.COMM_A2A, a2a)
-                    fmi_amd.tune_set(Tn.COMM_GATHER, gather)
-                    fmi_amd.tune_set(Tn.COMM_PIPELINE, pipe)
-                    for path in (Path.TREE, Path.RCCL):
-                        out.upload(np.zeros(n, dtype))
-                        c.allreduce(op, s, out, path=path)
-                        c.sync()
-                        assert_bit_equal(out.numpy(), x, f"allreduce {np.dtype(dtype).name} n={n} {path.name} "
-                                                         f"a2a={a2a} gather={gather} pipe={pipe}")
-                fmi_amd.tune_set(Tn.COMM_A2A, 0)
-                fmi_amd.tune_set(Tn.COMM_GATHER, 0)
-                fmi_amd.tune_set(Tn.COMM_PIPELINE, 0)
-                for ordered in (False, True):
-                    out.upload(np.zeros(n, dtype))
-                    c.reduce(op, s, out, 0, ordered=ordered)
-                    c.sync()
-                    assert_bit_equal(out.numpy(), x, f"reduce ordered={ordered}")
-                    out.upload(np.zeros(n, dtype))
-                    c.scan(op, s, out, ordered=ordered)
-                    c.sync()
-                    assert_bit_equal(out.numpy(), x, f"scan ordered={ordered}")
-                sb = Bucket.from_numpy(x)
-                out.upload(np.zeros(n, dtype))
-                c.reduce(op, sb, out, 0, sendbuf_partials=True)
-                c.sync()
-                assert_bit_equal(out.numpy(), x, "reduce_sendbuf result")
-                assert_bit_equal(sb.numpy(), x, "reduce_sendbuf partial of the root")
-                for b in (s, out, sb):
-                    b.free()
-        # path DIRECT: the window's IPC handle exchanged by ncclAllGather and agreed by ncclAllReduce(min)
-        w = c.window(4099, np.float32)
-        x = inputs(np.float32, 4099, 0, seed=72)
-        w.upload(x)
-        out = Bucket(4099, np.float32)
-        c.allreduce(Op.SUM, w, out, path=Path.DIRECT)
-        c.sync()
-        assert_bit_equal(out.numpy(), x, "DIRECT")
-        c.window_free(w)
-        out.free()
-        # host pipeline (C5 shape, small): H2D / sharded allreduce / D2H
-        h = np.ascontiguousarray(inputs(np.float32, 3 * 65536 + 5, 0, seed=73))
-        r = np.empty_like(h)
-        c.allreduce_host(Op.SUM, h, r, chunk=65536)
-        assert_bit_equal(r, h, "host allreduce")
-        c.barrier()
-    finally:
-        for key in (Tn.COMM_A2A, Tn.COMM_GATHER, Tn.COMM_PIPELINE, Tn.COMM_ONE_RANK_EXCHANGE):
-            fmi_amd.tune_set(key, 0)
-    c.destroy()
+    of the pipelined allreduce, reduce / reduce_sendbuf / scan, the host pipeline — so a 1-GPU box executes
+    the RCCL calls the 8-GPU run makes. Every result is the reference's P = 1 result (a copy of the rank's own
+    bucket, PeerToPeer.cpp:96-184 with one peer), bit for bit (tests/_one_rank_worker.py). Run in a child
+    process twice: with the system librccl (fmi_amd loaded first) and with torch's (torch imported first, as
+    bench.py's N > 1 path does) — the two differ in version (2.27 / 2.26)."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-u", "-m", "tests._one_rank_worker"] + (["--torch-first"] if torch_first else []),
+                       cwd=root, capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0 and "one-rank exchange ok" in r.stdout, (r.stdout[-3000:], r.stderr[-3000:])
+    mapped = [l for l in r.stdout.splitlines() if l.startswith("librccl mapped:")][0]
+    assert ("torch/lib" in mapped) == torch_first, mapped  # which librccl ran: torch's or the system's
 
 
 def test_c4_8peer_1gib_allreduce_full_size(device):
