@@ -547,9 +547,19 @@ private:
     int run_plan(const plan::Plan& p, const char* send, char* recv, hipStream_t s) {
         if (!p.sends.empty() || !p.recvs.empty()) {
             FMI_RCCL(GroupStart());
-            for (const plan::Xfer& x : p.sends) FMI_RCCL(Send(send + x.off, x.len, ncclUint8, x.peer, comm_, s));
-            for (const plan::Xfer& x : p.recvs) FMI_RCCL(Recv(recv + x.off, x.len, ncclUint8, x.peer, comm_, s));
-            FMI_RCCL(GroupEnd());
+            int rc = FMI_OK;
+            for (size_t i = 0; i < p.sends.size() && rc == FMI_OK; ++i) {
+                const plan::Xfer& x = p.sends[i];
+                rc = ck(api_->Send(send + x.off, x.len, ncclUint8, x.peer, comm_, s), "Send");
+            }
+            for (size_t i = 0; i < p.recvs.size() && rc == FMI_OK; ++i) {
+                const plan::Xfer& x = p.recvs[i];
+                rc = ck(api_->Recv(recv + x.off, x.len, ncclUint8, x.peer, comm_, s), "Recv");
+            }
+            // the group is closed even after a failed post, so this thread's later RCCL calls are not grouped
+            const int end = ck(api_->GroupEnd(), "GroupEnd");
+            FMI_COMM_RC(rc);
+            FMI_COMM_RC(end);
         }
         if (p.copy_len && recv + p.copy_dst != send + p.copy_src)
             FMI_COMM_RC(device_copy(recv + p.copy_dst, send + p.copy_src, p.copy_len, s));
