@@ -14,6 +14,9 @@
 //              (b % 8) * T/8 + b / 8, so each XCD streams its own eighth of every bucket instead of all XCDs
 //              sharing one moving window (does DRAM locality improve on the slow placements?)
 //   pair3 / pair3_xcd   C2's shape (2 reads + 1 write, f32 sum) on buckets 0..2 of the set, both tile orders
+//   sum8       8 reads + 1 write, plain f32 sum in index order (no reference bracketing): the traffic of the
+//              N = 8 shard kernel / C3's 8-peer tree
+//   tree8      the library's fused 8-peer allreduce (fmi_dev_reduce_tree, allreduce_no_order order)
 // Draws: each draw allocates a fresh set of 2 x 16 x 64 MiB buckets (two rotating sets, 2 GiB, beyond the
 // 256 MB MALL), so placement varies draw to draw as it does between callers; per draw, the kernels run
 // interleaved over R rounds of K back-to-back launches (events), median per kernel.
@@ -100,6 +103,20 @@ __global__ void __launch_bounds__(256) pair3(Ptrs16 b) {
 #pragma unroll
     for (int u = 0; u < kU; ++u)
         st(b.out[0] + base + u * 256, __builtin_bit_cast(V, __builtin_bit_cast(F4, x[u]) + __builtin_bit_cast(F4, y[u])));
+}
+
+__global__ void __launch_bounds__(256) sum8(Ptrs16 b) {
+    const size_t base = static_cast<size_t>(blockIdx.x) * kU * 256 + threadIdx.x;
+    using F4 = float __attribute__((ext_vector_type(4)));
+    F4 acc[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) acc[u] = __builtin_bit_cast(F4, ld(b.in[0] + base + u * 256));
+#pragma unroll
+    for (int p = 1; p < kP; ++p)
+#pragma unroll
+        for (int u = 0; u < kU; ++u) acc[u] += __builtin_bit_cast(F4, ld(b.in[p] + base + u * 256));
+#pragma unroll
+    for (int u = 0; u < kU; ++u) st(b.out[0] + base + u * 256, __builtin_bit_cast(V, acc[u]));
 }
 
 __global__ void __launch_bounds__(256) copy8_2ph(Ptrs16 b) {
@@ -190,6 +207,16 @@ int main(int argc, char** argv) {
             {"copy8_xcd", rw, [&](int k) { copy8_xcd<<<grid, 256, 0, s>>>(sets[k & 1]); }, {}},
             {"pair3", 3.0 * kBytes, [&](int k) { pair3<false><<<grid, 256, 0, s>>>(sets[k & 1]); }, {}},
             {"pair3_xcd", 3.0 * kBytes, [&](int k) { pair3<true><<<grid, 256, 0, s>>>(sets[k & 1]); }, {}},
+            {"sum8", 9.0 * kBytes, [&](int k) { sum8<<<grid, 256, 0, s>>>(sets[k & 1]); }, {}},
+            {"tree8", 9.0 * kBytes, [&](int k) {
+                 const Ptrs16& b = sets[k & 1];
+                 const void* ins[kP];
+                 for (int p = 0; p < kP; ++p) ins[p] = b.in[p];
+                 if (fmi_dev_reduce_tree(FMI_OP_SUM, FMI_F32, FMI_ALG_ALLREDUCE, b.out[0], ins, kP, 0, kBytes / 4, s) != FMI_OK) {
+                     std::fprintf(stderr, "tree: %s\n", fmi_last_error());
+                     std::exit(1);
+                 }
+             }, {}},
             {"read16", rw, [&](int k) { read16<<<grid, 256, 0, s>>>(sets[k & 1], sink); }, {}},
             {"write16", rw, [&](int k) { write16<<<grid, 256, 0, s>>>(sets[k & 1]); }, {}},
             {"scan8", rw, [&](int k) {
