@@ -80,6 +80,32 @@ def test_graph_capture_of_a_synchronising_call_fails_loudly(device):
     s.destroy()
 
 
+def test_graph_replays_device_copies(device):
+    """fmi_dev_d2d_async inside a graph: the copy kernel (aligned device buckets of >= 256 KiB, whose pointer
+    check runs at capture time) and the runtime copy (small or unaligned) are both recorded and replayed."""
+    s = Stream()
+    big = 1 << 20  # floats: 4 MiB, the copy_tile kernel
+    a, b = Bucket.from_numpy(np.arange(big, dtype=np.float32)), Bucket(big, np.float32)
+    c, d = Bucket.from_numpy(np.arange(100, dtype=np.float32)), Bucket(100, np.float32)
+
+    def record():
+        b.copy_from(a, stream=s)
+        d.copy_from(c, stream=s)
+
+    g = Graph.capture(s, record)
+    for k in (1, 2):
+        a.upload(np.arange(big, dtype=np.float32) * k)
+        c.upload(np.arange(100, dtype=np.float32) * k)
+        g.launch(s)
+        s.sync()
+        assert np.array_equal(b.numpy(), np.arange(big, dtype=np.float32) * k)
+        assert np.array_equal(d.numpy(), np.arange(100, dtype=np.float32) * k)
+    g.destroy()
+    s.destroy()
+    for x in (a, b, c, d):
+        x.free()
+
+
 def test_graph_capture_of_an_arena_call_is_refused(device):
     """A call that needs the library's scratch arena (here an unaligned 4-peer reduce_tree, which runs the
     program as pairwise passes through arena temps) is refused while its stream is capturing: the arena's
