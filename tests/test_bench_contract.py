@@ -157,3 +157,42 @@ def test_library_stdout_noise_cannot_reach_the_line():
     assert r.returncode == 0, r.stderr
     assert r.stdout.strip().splitlines() == ['{"metric": "m", "value": 1}']
     assert "RCCL version" in r.stderr and "python noise" in r.stderr
+
+
+def test_pmc_summary_splits_one_kernel_by_launch_shape(tmp_path):
+    """tools/pmc_summarize.py groups launches by (kernel, grid size): copy_tile launched at 256 MiB and at
+    64 MiB in one run gives two entries with their own PMC bytes and trace durations, never a median across
+    shapes (what round 3's first C2 profile would otherwise have reported for the copy kernel)."""
+    import csv
+
+    name = "void fmi::dev::copy_tile<4>(char*, char const*, unsigned long)"
+    big, small = 16384, 4096  # workgroups: 256 MiB and 64 MiB in 16-KiB tiles (grid size = threads)
+    for sub, counter, per in (("f", "FETCH_SIZE", lambda g: g * 8.0), ("w", "WRITE_SIZE", lambda g: g * 16.0)):
+        d = tmp_path / sub
+        d.mkdir()
+        with open(d / "run_counter_collection.csv", "w", newline="") as f:
+            w = csv.writer(f)
+            w.writerow(["Grid_Size", "Kernel_Name", "Counter_Name", "Counter_Value"])
+            for g, k in ((big, 3), (small, 5)):
+                for _ in range(k):  # KiB: fetch is half the bytes on gfx950 (x2 correction), write exact
+                    w.writerow([g * 256, name, counter, per(g)])
+    t = tmp_path / "t"
+    t.mkdir()
+    with open(t / "run_kernel_trace.csv", "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["Kernel_Name", "Start_Timestamp", "End_Timestamp", "Grid_Size_X", "Grid_Size_Y", "Grid_Size_Z"])
+        for g, ns, k in ((big, 84000, 3), (small, 24000, 5)):
+            for i in range(k):
+                w.writerow([name, 1000 * i, 1000 * i + ns, g * 256, 1, 1])
+    out = tmp_path / "out"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_summarize.py"), "--trace", str(t),
+                        "--fetch", str(tmp_path / "f"), "--write", str(tmp_path / "w"), "--tag", "t", "--command", "x",
+                        "--no-default", "--out", str(out)], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    entries = {e["grid_size"]: e for e in json.load(open(out / "t_pmc_summary.json"))["kernels"]}
+    assert set(entries) == {big * 256, small * 256}
+    for g, mib, ns in ((big, 256, 84000), (small, 64, 24000)):
+        e = entries[g * 256]
+        assert e["algorithmic_bytes_per_launch"] == 2 * mib << 20
+        assert e["hbm_bytes_per_launch"] == 2 * mib << 20  # 2 x fetch KiB + write KiB = 2 x bucket
+        assert e["trace"]["avg_ns"] == ns and e["trace"]["calls"] == (3 if g == big else 5)
