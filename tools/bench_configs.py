@@ -223,12 +223,13 @@ def main():
             row(f"pair {op.name.lower()} {np.dtype(dt).name} 256MiB", 3 * 256 * MIB, med, mn)
         del sets
 
-    # calibration: the runtime's device-to-device copy (1 read + 1 write stream) at 256 MiB
-    src = Bucket(64 * MIB, np.float32)
-    dst = Bucket(64 * MIB, np.float32)
-    med, mn = timed(lambda k: dst.copy_from(src), it, 1)
-    row("calibration hipMemcpy D2D 256MiB", 2 * 256 * MIB, med, mn, note="runtime copy kernel, read:write 1:1")
-    del src, dst
+    # calibration: the library's device-to-device copy (fmi_dev_d2d_async -> copy_tile, 1 read + 1 write stream)
+    # at 256 MiB, 4 rotating pairs: its sc1 stores would otherwise leave the destination in the MALL
+    pairs = [(Bucket(64 * MIB, np.float32), Bucket(64 * MIB, np.float32)) for _ in range(4)]
+    med, mn = timed(lambda k: pairs[k][1].copy_from(pairs[k][0]), it, 4)
+    row("calibration device copy 256MiB (copy_tile, 4 rotating pairs)", 2 * 256 * MIB, med, mn,
+        note="fmi_dev_d2d_async, read:write 1:1")
+    del pairs
 
     # C3a: int64 max, 64 MiB buckets; 8 rotating sets = 1.5 GiB working set (defeats the MALL)
     n = 64 * MIB // 8
@@ -262,7 +263,10 @@ def main():
     del ins, outs, out
     wide_tree_rows(it)
 
-    # host-inclusive (C5-shaped, one GPU): pinned and pageable 256 MiB f32 pairs through the device
+    # host-inclusive (C5-shaped, one GPU): pinned and pageable 256 MiB f32 pairs through the device, on a
+    # quiet device (see host_allreduce_rows)
+    fmi_amd.sync()
+    time.sleep(1.0)
     n = 256 * MIB // 4
     ha, pa = pinned(n, np.float32)
     hb, pb = pinned(n, np.float32)
@@ -331,6 +335,10 @@ def host_allreduce_rows():
         for r, (s, _) in enumerate(bufs):
             s.array[:] = np.float32(r + 1)
         for chunk in chunks:
+            # a quiet device first: VRAM freed by the rows before is cleared asynchronously on the copy
+            # engines these H2D / D2H copies use (profiles/r02_c5_after_free_probe.jsonl)
+            fmi_amd.sync()
+            time.sleep(1.0)
             uid = unique_id(Transport.LOCAL)
             times = [None] * N
 
