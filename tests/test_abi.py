@@ -320,3 +320,29 @@ def test_host_out_of_memory_is_a_status_not_a_crash():
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr[-2000:]
     assert r.stdout.split()[0] == str(_lib.FMI_ERR_ALLOC) and "out of host memory" in r.stdout
+
+
+def test_pci_bus_id_and_comm_query_host_side():
+    """fmi_dev_pci_bus_id refuses a device that is not there (FMI_ERR_NO_DEVICE, no crash); fmi_comm_query on a
+    LOCAL communicator reports its own size and rank (host logic); both refuse null arguments."""
+    from fmi_amd.comm import Comm, Transport, unique_id
+
+    lib = _lib.load()
+    buf = ctypes.create_string_buffer(64)
+    assert lib.fmi_dev_pci_bus_id(4096, buf, 64) == _lib.FMI_ERR_NO_DEVICE
+    assert lib.fmi_dev_pci_bus_id(0, None, 64) == _lib.FMI_ERR_INVALID
+    uid = unique_id(Transport.LOCAL)
+    c0, c1 = Comm(uid, 2, 0), Comm(uid, 2, 1)
+    cnt, rk, dev = ctypes.c_int(-1), ctypes.c_int(-1), ctypes.c_int(-1)
+    assert lib.fmi_comm_query(ctypes.c_void_p(c1.handle), None, ctypes.byref(rk), ctypes.byref(dev)) == _lib.FMI_ERR_INVALID
+    rc = lib.fmi_comm_query(ctypes.c_void_p(c1.handle), ctypes.byref(cnt), ctypes.byref(rk), ctypes.byref(dev))
+    c = ctypes.c_int(0)
+    lib.fmi_dev_count(ctypes.byref(c))
+    if c.value == 0:  # no device: hipGetDevice fails after the size and rank are known
+        assert rc in (_lib.FMI_OK, _lib.FMI_ERR_HIP)
+    else:
+        assert rc == _lib.FMI_OK
+    assert (cnt.value, rk.value) == (2, 1)
+    assert lib.fmi_comm_sync(ctypes.c_void_p(c0.handle), None) in (_lib.FMI_OK, _lib.FMI_ERR_NO_DEVICE)
+    c0.destroy()
+    c1.destroy()
