@@ -5,7 +5,8 @@ Python, Utils::Timeout in C++ (tests/test_cpp_communicator.py runs rccl_channel_
 instead of a hang, and the communicator is aborted (later calls fail) but destroys cleanly.
 
 - LOCAL: two ranks as threads, one never calls the collective.
-- PROC: three processes, one exits after the first allreduce; the other two must time out in the second.
+- PROC: three processes, one exits after the first allreduce (or in the middle of its next exchange); the other
+  two must time out in their second allreduce.
 - RCCL: rank 0 alone initialising a 2-rank communicator (non-blocking init + ncclCommAbort)."""
 import json
 import os
@@ -62,11 +63,12 @@ def _run(cmd, timeout):
     return r, (json.loads(lines[-1]) if lines else None)
 
 
-def test_proc_rank_exit_makes_the_others_time_out(device):
+@pytest.mark.parametrize("when", ["before", "during"])
+def test_proc_rank_exit_makes_the_others_time_out(device, when):
     N, die, limit = 3, 2, 4.0
     uid = unique_id(Transport.PROC).hex()
     procs = [subprocess.Popen([sys.executable, "-u", "-m", "tests._timeout_worker", "proc", uid, str(N), str(r),
-                               str(limit), str(die)], cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                               str(limit), str(die), when], cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
                               text=True, env=dict(os.environ, OMP_NUM_THREADS="1"))
              for r in range(N)]
     outs = []
