@@ -12,21 +12,18 @@ A CPU restatement of the reference's bucket-reduction path (spcl/fmi @ v1):
   * the side effects: commutative reduce/allreduce/scan overwrite the caller's sendbuf
     (reference src/comm/PeerToPeer.cpp:72,103,119,160,179); the simulation returns both buffers.
 
-Pinning: the reference library cannot be built here without writing stand-ins for
-headers it needs (src/comm/Channel.cpp → S3.h / Redis.h / Direct.h → aws-sdk-cpp, hiredis, TCPunch;
-src/Communicator.cpp → boost::property_tree), which this task forbids, so there is no oracle/_ref.
-This restatement is pinned instead by
+Pinning. Since round 3 this restatement is pinned by the REFERENCE ITSELF, floats included:
+oracle/_ref/libfmi_ref.so (oracle/Makefile) is the reference's own src/comm/PeerToPeer.cpp, compiled unmodified
+from /root/reference, run over an in-memory PeerToPeer transport (oracle/ref_harness.cpp; oracle/fmi_ref.py).
+Only src/comm/Channel.cpp (the S3 / Redis / Direct factory: aws-sdk-cpp, hiredis, TCPunch) and
+include/Communicator.h (boost::property_tree) stay unbuilt; neither is on the evaluation-order path. Checked by
   (1) the reference's own known-answer tests (reference tests/communicator.cpp:94-254,
-      tests/channels.cpp:419-690), including the non-commutative LTR subtraction cases that fix the
-      left-to-right order — tests/golden/reference_kats.json;
-  (2) the evaluation-order table of SURVEY.md Appendix B — tests/golden/bracketing.json. The survey traced it
-      from a reference build that needed stand-ins, which by this task's rules pins nothing: it is a third
-      restatement that agrees, not a reference output.
-Both are checked by tests/test_oracle.py. Every reference-held vector is integer, and the commutative
-collectives' integer results do not depend on the order, so the FLOAT EVALUATION ORDER of the commutative
-allreduce / reduce / scan is PARITY UNPINNED: it rests on this restatement's line-by-line reading of
-src/comm/PeerToPeer.cpp:59-184, checked against two independent in-repo restatements (the kernels' programs
-and the C++ channel algorithms). Integer results and the left-to-right (LTR) order are pinned.
+      tests/channels.cpp:419-690) — tests/golden/reference_kats.json, tests/test_oracle.py;
+  (2) the reference's float outputs and exact bracketing — tests/golden/ref_vectors.npz / ref_expr.json
+      (tests/golden/make_ref_vectors.py) and live runs of oracle/_ref — tests/test_ref_pinning.py: every
+      collective, commutative and left-to-right, every rank / root, sendbuf side effects, bit-exact.
+(SURVEY.md Appendix B's table, tests/golden/bracketing.json, came from a survey build with stand-ins and is
+kept only as a cross-check.)
 
 Floating point: numpy float32/float64 arithmetic is IEEE round-to-nearest-even with denormals kept,
 the same as the reference's libstdc++ loop compiled without fast-math. Integer arrays wrap modulo 2^bits

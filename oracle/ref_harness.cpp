@@ -1,0 +1,292 @@
+// ORACLE — TEST INFRASTRUCTURE ONLY (built into oracle/_ref/libfmi_ref.so by oracle/Makefile; loaded only by
+// tests/ and tests/golden/make_ref_vectors.py, never by the product, smoke() or bench.py's timed regions).
+//
+// Runs the REFERENCE's own collective algorithms — /root/reference/src/comm/PeerToPeer.cpp, compiled unmodified
+// from where it lies and linked beside this file — over an in-memory transport, so that the float evaluation
+// order of FMI's reduce / allreduce / scan comes from the reference itself rather than from a restatement.
+//
+// What is the reference and what is this harness:
+//   * reference (compiled from /root/reference, never copied): PeerToPeer::{reduce, reduce_ltr, reduce_no_order,
+//     allreduce, allreduce_no_order, scan, scan_ltr, scan_no_order, bcast, gather, scatter, barrier}
+//     (src/comm/PeerToPeer.cpp:6-293) and the headers it includes (include/comm/{PeerToPeer,Channel,Data}.h,
+//     include/utils/{Function,Common}.h).
+//   * this harness: `Loopback`, a PeerToPeer channel — the plug-in point the reference defines for transports
+//     (include/comm/PeerToPeer.h:47-50, send_object / recv_object; the reference's own Direct channel fills it
+//     with TCP sockets, src/comm/Direct.cpp:25-45) — whose per-peer-pair FIFO mailboxes live in memory; the
+//     peers run as threads; and the element-wise combine f.f(a, b): a[i] = op(a[i], b[i]) with the reference's
+//     built-in functors (std::plus / std::multiplies / std::max / std::min, python/PythonCommunicator.h:131-149),
+//     i.e. what Communicator::convert_to_raw_function (include/Communicator.h:180-189) hands the channel. That
+//     adapter itself is not compiled: include/Communicator.h needs include/utils/Configuration.h and so
+//     boost::property_tree, which the image lacks. Its copies do not change any value.
+//   * not built: src/comm/Channel.cpp (the S3 / Redis / Direct factory and Channel's default gather / scatter /
+//     allreduce, all overridden by PeerToPeer; it needs aws-sdk-cpp, hiredis and TCPunch). Both files are built
+//     with -fno-rtti because Channel's type_info would be emitted there (key function Channel::gather); no code
+//     of Channel.cpp runs on any path used here. No stand-in for any missing header or library is written.
+//
+// C-ABI (oracle/fmi_ref.py wraps it with ctypes):
+//   fmi_ref_run   numeric collective over P peers' buckets: every peer's recvbuf and sendbuf after the call.
+//   fmi_ref_expr  symbolic run: each element is a handle to an expression; f.f(a, b) makes "(a+b)" (left operand
+//                 = arg 0 of f.f), so the result is the exact bracketing the reference evaluates.
+#include "comm/PeerToPeer.h"
+
+#include <algorithm>
+#include <chrono>
+#include <condition_variable>
+#include <cstdint>
+#include <cstring>
+#include <deque>
+#include <functional>
+#include <mutex>
+#include <new>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <vector>
+
+#define FMI_REF_API extern "C" __attribute__((visibility("default")))
+
+namespace {
+
+using FMI::Utils::peer_num;
+
+// Per-peer-pair FIFO mailboxes: send never blocks (the reference's Direct channel writes into a socket
+// buffer), recv blocks until the message from that peer is there and must read exactly buf.len bytes.
+struct Mailbox {
+    explicit Mailbox(int p) : P(p), q(static_cast<size_t>(p) * p) {}
+    int P;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::vector<std::deque<std::vector<char>>> q;  // q[src * P + dst]
+    std::string error;                              // first failure; every waiting peer gives up on it
+    size_t dropped = 0;                             // sends to a peer id >= P (reference scan_ltr at P = 1)
+};
+
+constexpr double kRecvTimeoutS = 60.0;
+
+class Loopback final : public FMI::Comm::PeerToPeer {
+public:
+    Loopback(Mailbox* mb, peer_num id, peer_num P) : mb_(mb) {
+        set_peer_id(id);
+        set_num_peers(P);  // (comm_name stays empty: PeerToPeer never reads it)
+    }
+    void send_object(channel_data buf, peer_num dst) override {
+        std::lock_guard<std::mutex> lk(mb_->mu);
+        if (dst >= static_cast<peer_num>(mb_->P)) {  // no such peer: nothing would ever read it
+            ++mb_->dropped;
+            return;
+        }
+        mb_->q[static_cast<size_t>(peer_id) * mb_->P + dst].emplace_back(buf.buf, buf.buf + buf.len);
+        mb_->cv.notify_all();
+    }
+    void recv_object(channel_data buf, peer_num src) override {
+        std::unique_lock<std::mutex> lk(mb_->mu);
+        if (src >= static_cast<peer_num>(mb_->P)) throw std::runtime_error("recv from a peer id >= P");
+        auto& box = mb_->q[static_cast<size_t>(src) * mb_->P + peer_id];
+        const auto deadline = std::chrono::steady_clock::now() + std::chrono::duration<double>(kRecvTimeoutS);
+        while (box.empty() && mb_->error.empty()) {
+            if (mb_->cv.wait_until(lk, deadline) == std::cv_status::timeout && box.empty())
+                throw FMI::Utils::Timeout();
+        }
+        if (!mb_->error.empty()) throw std::runtime_error("another peer failed");
+        std::vector<char> msg = std::move(box.front());
+        box.pop_front();
+        if (msg.size() != buf.len)
+            throw std::runtime_error("message of " + std::to_string(msg.size()) + " B received into a " +
+                                     std::to_string(buf.len) + " B buffer");
+        std::memcpy(buf.buf, msg.data(), msg.size());
+    }
+    double get_latency(peer_num, peer_num, std::size_t) override { return 0.0; }
+    double get_price(peer_num, peer_num, std::size_t) override { return 0.0; }
+
+private:
+    Mailbox* mb_;
+};
+
+enum Coll { kAllreduce = 0, kReduce = 1, kScan = 2, kBcast = 3, kGather = 4, kScatter = 5, kBarrier = 6 };
+enum Op { kSum = 0, kProd = 1, kMax = 2, kMin = 3, kSub = 4 };
+enum Dtype { kF32 = 0, kF64 = 1, kI32 = 2, kI64 = 3, kU32 = 4, kU64 = 5 };
+
+size_t dtype_size(int d) {
+    switch (d) {
+        case kF32: case kI32: case kU32: return 4;
+        case kF64: case kI64: case kU64: return 8;
+        default: return 0;
+    }
+}
+
+// a[i] = op(a[i], b[i]) for i < n — the channel-level combine f.f(a, b) (a overwritten, b read-only).
+template <typename T>
+raw_func elementwise(int op, size_t n) {
+    std::function<T(T, T)> g;
+    switch (op) {
+        case kSum: g = std::plus<T>(); break;
+        case kProd: g = std::multiplies<T>(); break;
+        case kMax: g = [](T a, T b) { return std::max(a, b); }; break;
+        case kMin: g = [](T a, T b) { return std::min(a, b); }; break;
+        default: g = std::minus<T>(); break;  // the reference KATs' non-commutative op
+    }
+    return [g, n](char* a, char* b) {
+        T* x = reinterpret_cast<T*>(a);
+        const T* y = reinterpret_cast<const T*>(b);
+        std::transform(x, x + n, y, x, g);
+    };
+}
+
+raw_func make_combine(int op, int dtype, size_t n) {
+    switch (dtype) {
+        case kF32: return elementwise<float>(op, n);
+        case kF64: return elementwise<double>(op, n);
+        case kI32: return elementwise<int32_t>(op, n);
+        case kI64: return elementwise<int64_t>(op, n);
+        case kU32: return elementwise<uint32_t>(op, n);
+        default: return elementwise<uint64_t>(op, n);
+    }
+}
+
+void set_err(char* err, size_t len, const std::string& msg) {
+    if (!err || !len) return;
+    const size_t k = std::min(len - 1, msg.size());
+    std::memcpy(err, msg.data(), k);
+    err[k] = '\0';
+}
+
+// Runs `body(channel, peer)` on P threads, one Loopback per peer. Returns "" or the first failure.
+std::string run_peers(int P, const std::function<void(Loopback&, int)>& body, size_t* dropped) {
+    Mailbox mb(P);
+    std::vector<std::thread> th;
+    th.reserve(P);
+    for (int p = 0; p < P; ++p) {
+        th.emplace_back([&, p] {
+            try {
+                // Built in place and never destroyed: Channel has no virtual destructor and its implicit one
+                // would name Channel's vtable, which only the unbuilt Channel.cpp emits. Nothing is leaked:
+                // the object holds a non-owning mailbox pointer and an empty in-place string.
+                alignas(Loopback) unsigned char storage[sizeof(Loopback)];
+                Loopback& ch = *new (storage) Loopback(&mb, static_cast<peer_num>(p), static_cast<peer_num>(P));
+                body(ch, p);
+            } catch (const std::exception& e) {
+                std::lock_guard<std::mutex> lk(mb.mu);
+                if (mb.error.empty()) mb.error = "peer " + std::to_string(p) + ": " + e.what();
+                mb.cv.notify_all();
+            }
+        });
+    }
+    for (auto& t : th) t.join();
+    if (mb.error.empty()) {
+        for (const auto& box : mb.q)
+            if (!box.empty()) return "unconsumed messages after the collective";
+    }
+    if (dropped) *dropped = mb.dropped;
+    return mb.error;
+}
+
+}  // namespace
+
+// Numeric collective. ins: P buckets of n elements (peer-major). recv_out / send_out: P buckets each, the
+// recvbuf (pre-filled from recv_init when not null, else zero) and the sendbuf of every peer after the call.
+// ordered = 1: the raw_function is flagged non-commutative (the reference then takes its LTR algorithms).
+// root: reduce / bcast / gather / scatter root. gather's recvbuf at the root is P buckets (recv_out holds
+// P * P buckets for gather: peer p's slot is recv_out + p * P * n). Returns 0, or -1 with a message in err.
+FMI_REF_API int fmi_ref_run(int coll, int op, int dtype, int ordered, int P, int root, size_t n, const void* ins,
+                            const void* recv_init, void* recv_out, void* send_out, size_t* dropped, char* err,
+                            size_t errlen) {
+    const size_t es = dtype_size(dtype);
+    if (P < 1 || es == 0 || root < 0 || root >= P || (!ins && coll != kBarrier)) {
+        set_err(err, errlen, "invalid argument");
+        return -1;
+    }
+    const size_t S = n * es;
+    const size_t recv_buckets = coll == kGather ? static_cast<size_t>(P) : 1;
+    const size_t send_buckets = coll == kScatter ? static_cast<size_t>(P) : 1;
+    std::vector<std::vector<char>> send(P), recv(P);
+    for (int p = 0; p < P; ++p) {
+        if (ins)
+            send[p].assign(static_cast<const char*>(ins) + p * send_buckets * S,
+                           static_cast<const char*>(ins) + (p + 1) * send_buckets * S);
+        else
+            send[p].assign(send_buckets * S, 0);
+        recv[p].assign(recv_buckets * S, 0);
+        if (recv_init)
+            std::memcpy(recv[p].data(), static_cast<const char*>(recv_init) + p * recv_buckets * S, recv_buckets * S);
+    }
+    const raw_function f{make_combine(op, dtype, n), /*associative=*/true, /*commutative=*/ordered == 0};
+    const std::string e = run_peers(
+        P,
+        [&](Loopback& ch, int p) {
+            channel_data sd{send[p].data(), send[p].size()};
+            channel_data rd{recv[p].data(), recv[p].size()};
+            switch (coll) {
+                case kAllreduce: ch.allreduce(sd, rd, f); break;
+                case kReduce: ch.reduce(sd, rd, static_cast<peer_num>(root), f); break;
+                case kScan: ch.scan(sd, rd, f); break;
+                case kBcast: ch.bcast(sd, static_cast<peer_num>(root)); break;
+                case kGather: ch.gather(sd, rd, static_cast<peer_num>(root)); break;
+                case kScatter: ch.scatter(sd, rd, static_cast<peer_num>(root)); break;
+                default: ch.barrier(); break;
+            }
+        },
+        dropped);
+    if (!e.empty()) {
+        set_err(err, errlen, e);
+        return -1;
+    }
+    for (int p = 0; p < P; ++p) {
+        if (recv_out) std::memcpy(static_cast<char*>(recv_out) + p * recv_buckets * S, recv[p].data(), recv[p].size());
+        if (send_out) std::memcpy(static_cast<char*>(send_out) + p * send_buckets * S, send[p].data(), send[p].size());
+    }
+    return 0;
+}
+
+// Symbolic collective (one element per bucket): the expression peer `rank` ends with in its recvbuf (reduce:
+// the root's), written to buf as "x0", "(x0+x1)", ... ; `which` = 1 returns the sendbuf after the call instead.
+// Returns the expression length (buf may be too small: call again with a larger one), or -1 with err.
+FMI_REF_API long fmi_ref_expr(int coll, int ordered, int P, int rank, int root, int which, char* buf, size_t len,
+                              char* err, size_t errlen) {
+    if (P < 1 || rank < 0 || rank >= P || root < 0 || root >= P || coll < kAllreduce || coll > kScan) {
+        set_err(err, errlen, "invalid argument");
+        return -1;
+    }
+    std::mutex mu;  // the expression table is shared by the peer threads
+    std::vector<std::string> table;
+    for (int p = 0; p < P; ++p) table.push_back("x" + std::to_string(p));
+    auto combine = [&](char* a, char* b) {
+        std::lock_guard<std::mutex> lk(mu);
+        int32_t ia, ib;
+        std::memcpy(&ia, a, 4);
+        std::memcpy(&ib, b, 4);
+        const std::string e = "(" + table.at(ia) + "+" + table.at(ib) + ")";
+        table.push_back(e);
+        const int32_t h = static_cast<int32_t>(table.size() - 1);
+        std::memcpy(a, &h, 4);
+    };
+    const raw_function f{combine, true, ordered == 0};
+    std::vector<int32_t> send(P), recv(P, -1);
+    for (int p = 0; p < P; ++p) send[p] = p;
+    const std::string e = run_peers(
+        P,
+        [&](Loopback& ch, int p) {
+            channel_data sd{reinterpret_cast<char*>(&send[p]), 4};
+            channel_data rd{reinterpret_cast<char*>(&recv[p]), 4};
+            if (coll == kAllreduce) ch.allreduce(sd, rd, f);
+            else if (coll == kReduce) ch.reduce(sd, rd, static_cast<peer_num>(root), f);
+            else ch.scan(sd, rd, f);
+        },
+        nullptr);
+    if (!e.empty()) {
+        set_err(err, errlen, e);
+        return -1;
+    }
+    const int who = coll == kReduce && which == 0 ? root : rank;
+    const int32_t h = which ? send[who] : recv[who];
+    if (h < 0 || h >= static_cast<int32_t>(table.size())) {
+        set_err(err, errlen, "no value in that buffer");
+        return -1;
+    }
+    const std::string& s = table[h];
+    if (buf && len) {
+        const size_t k = std::min(len - 1, s.size());
+        std::memcpy(buf, s.data(), k);
+        buf[k] = '\0';
+    }
+    return static_cast<long>(s.size());
+}

@@ -1,6 +1,7 @@
 """Pins the CPU oracle (oracle/fmi_oracle.py) before anything is checked against it:
   * the reference's own known-answer tests (tests/golden/reference_kats.json),
-  * the evaluation order traced from the compiled reference (tests/golden/bracketing.json),
+  * SURVEY.md Appendix B's evaluation-order table (tests/golden/bracketing.json; a cross-check only: the float
+    order is pinned by the reference itself in tests/test_ref_pinning.py),
   * the reference's side effects (sendbuf clobbering).
 CPU only."""
 import json
