@@ -7,7 +7,8 @@ tests/golden/{ref_vectors.npz, ref_expr.json} hold its outputs (tests/golden/mak
   * the committed bracketing == the oracle's == the kernels' programs (fmi_schedule_expr, host-only C-ABI);
   * where the library is built (the build container): a live run still gives the fixtures, the reference's
     own integer known answers (tests/golden/reference_kats.json) come out of the harness, and the live
-    bracketing equals the oracle and the programs for every rank / root up to 64 peers and at 100, 128, 129, 257.
+    bracketing equals the oracle and the programs for every rank / root up to 33 peers, and for sampled ranks /
+    roots at 37, 48, 63, 64, 65, 100, 128, 129 and 257.
 CPU only.
 """
 import json
@@ -145,9 +146,9 @@ def test_live_reference_reproduces_the_fixtures(case):
 
 
 @live
-@pytest.mark.parametrize("P", list(range(1, 65)) + [100, 128, 129, 257])
+@pytest.mark.parametrize("P", list(range(1, 34)) + [37, 48, 63, 64, 65, 100, 128, 129, 257])
 def test_live_reference_bracketing_equals_oracle_and_programs(P):
-    ranks = range(P) if P <= 64 else sorted({0, 1, P // 2, P - 2, P - 1})
+    ranks = range(P) if P <= 33 else sorted({0, 1, 5, P // 2, P - 2, P - 1})
     for (kind, ordered), alg in SCHEDULE.items():
         for r in ranks:
             kw = dict(root=r) if kind == "reduce" else dict(rank=r)
