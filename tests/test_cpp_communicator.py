@@ -10,6 +10,7 @@ import numpy as np
 import pytest
 
 from oracle import fmi_oracle as orc
+from oracle import fmi_ref as ref
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 EXE = os.path.join(ROOT, "build", "cpp", "test_communicator")
@@ -58,6 +59,38 @@ def _check(kind, P, n, recv, send):
         assert np.array_equal(send[p].view(np.uint32), sends[p].view(np.uint32)), f"{kind} P={P} sendbuf {p}"
 
 
+def _reference(kind, P, n):
+    """The reference itself (oracle/_ref: its src/comm/PeerToPeer.cpp) on the dump's inputs: (recv, send) per
+    peer, recv None where the reference leaves it undefined (reduce: non-roots)."""
+    xs = [orc.synthetic(np.float32, n, 42, p) for p in range(P)]
+    ordered = kind.endswith("_ltr")
+    base = kind[:-4] if ordered else kind
+    recv, send, _ = ref.run(base, "sum", xs, root=0, ordered=ordered)
+    res = list(recv) if base != "reduce" else [recv[0]] + [None] * (P - 1)
+    return res, list(send)
+
+
+def _check_against_reference(kind, P, recv, send):
+    res, sends = _reference(kind, P, recv.shape[1])
+    for p in range(P):
+        if res[p] is not None:
+            assert np.array_equal(recv[p].view(np.uint32), res[p].view(np.uint32)), f"{kind} P={P} peer {p}"
+        assert np.array_equal(send[p].view(np.uint32), sends[p].view(np.uint32)), f"{kind} P={P} sendbuf {p}"
+
+
+live = pytest.mark.skipif(not ref.available(), reason="oracle/_ref not built (needs /root/reference)")
+
+
+@live
+@pytest.mark.parametrize("kind", ["allreduce", "reduce", "scan", "allreduce_ltr", "reduce_ltr", "scan_ltr"])
+@pytest.mark.parametrize("P", [1, 2, 3, 5, 6, 8, 13, 16])
+def test_cpp_host_path_matches_the_reference(exe, kind, P):
+    """The C++ surface's channel algorithms (fmi_amd/cpp/include/fmi/comm/PeerToPeer.h) against the
+    reference's own PeerToPeer.cpp on the same float buckets: every peer's recvbuf and sendbuf."""
+    recv, send = _dump(exe, kind, P, 515)
+    _check_against_reference(kind, P, recv, send)
+
+
 def test_cpp_suite_host(exe):
     out = subprocess.run([exe], capture_output=True, text=True, timeout=600)
     assert out.returncode == 0, out.stderr[-4000:]
@@ -95,6 +128,8 @@ def test_cpp_device_path_matches_oracle(exe, mode, kind):
     P, n = 8, (1 << 16) + 5
     recv, send = _dump(exe, kind, P, n, mode)
     _check(kind, P, n, recv, send)
+    if ref.available():  # the prebuilt checker travels with the tree
+        _check_against_reference(kind, P, recv, send)
 
 
 def test_c1_host_bench_runs(exe):
