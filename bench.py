@@ -392,12 +392,16 @@ def one_peer_allreduce(n: int, launches: int = 20, sets: int = 4) -> dict:
 
 
 C3_PAIR_SETS = 64  # 63 x 8 MiB of sc1 tile writes between two uses of a set (see --sets)
+# The scan's rate depends on where its 16 buckets land in HBM (0.70-0.80 by allocation draw, the
+# write side bimodal); 8 sets of 16 separately allocated buckets (8 GiB) average over 8 draws instead of
+# letting two decide the line.
+C3_SCAN_SETS = 8
 
 
 def c3_single(reps: int = 60) -> dict:
     """Config C3 on this GPU, in the driver's run: the int64 max pairwise combine of 64 MiB buckets (64
     rotating sets, 8 GiB: no set is re-read from the 256 MiB MALL) and the f32 peer-axis scan (scan_no_order)
-    of 8 peers x 64 MiB (2 rotating sets: each launch writes 512 MiB); mean launch time from two HIP events
+    of 8 peers x 64 MiB (C3_SCAN_SETS rotating sets, 3 passes over them); mean launch time from two HIP events
     around back-to-back launches on the library stream, against the algorithmic bytes (3 x 64 MiB and
     2 x 8 x 64 MiB)."""
     import numpy as np
@@ -427,9 +431,20 @@ def c3_single(reps: int = 60) -> dict:
         a.free()
         b.free()
     P, n32 = 8, 64 * MIB // 4
-    ins = [[Bucket(n32, np.float32).fill_synthetic(7 + s, p) for p in range(P)] for s in range(2)]
-    outs = [[Bucket(n32, np.float32) for _ in range(P)] for _ in range(2)]
-    ms_scan = timed(lambda i: fmi_amd.scan_peers(Op.SUM, Alg.SCAN, outs[i % 2], ins[i % 2]), max(10, reps // 3))
+    S = C3_SCAN_SETS
+    ins = [[Bucket(n32, np.float32).fill_synthetic(7 + s, p) for p in range(P)] for s in range(S)]
+    outs = [[Bucket(n32, np.float32) for _ in range(P)] for _ in range(S)]
+    ms_scan = timed(lambda i: fmi_amd.scan_peers(Op.SUM, Alg.SCAN, outs[i % S], ins[i % S]), 3 * S)
+    per_set = [(Event(), Event()) for _ in range(S)]  # diagnostic, untimed: one launch per set, its own events
+    for i, (a, b) in enumerate(per_set):
+        a.record()
+        fmi_amd.scan_peers(Op.SUM, Alg.SCAN, outs[i], ins[i])
+        b.record()
+    fmi_amd.sync()
+    per_set_us = [round(a.elapsed_ms(b) * 1e3, 1) for a, b in per_set]
+    for a, b in per_set:
+        a.destroy()
+        b.destroy()
     for b in [x for s in ins + outs for x in s]:
         b.free()
 
@@ -442,7 +457,7 @@ def c3_single(reps: int = 60) -> dict:
     return {"i64_max_pair_64MiB": dict(row(ms_max, 3 * 64 * MIB, "pair_tile<fmi::dev::OpMax, long, 4, 3>"),
                                        rotating_sets=C3_PAIR_SETS),
             "f32_scan_P8_64MiB": dict(row(ms_scan, 2 * P * 64 * MIB, "scan_kernel<fmi::dev::OpSum, float, 3, 8>"),
-                                      rotating_sets=2),
+                                      rotating_sets=C3_SCAN_SETS, per_set_launch_us=per_set_us),
             "timing": "two HIP events around back-to-back launches on the library stream (gaps included)"}
 
 
