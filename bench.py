@@ -155,6 +155,7 @@ def cpu_baseline(args):
         "all_threads_loop": {"gib_s": round(omp["bucket_gib_s"], 4), "threads": omp["threads"],
                              "median_ms": round(omp["median_ms"], 3)},
         "c1": c1_host(),
+        "c1_reference": c1_reference(),
     }
 
 
@@ -171,6 +172,28 @@ def c1_host():
         return json.loads(out.stdout.strip().splitlines()[-1])
     except Exception as e:  # reported, never required
         return {"error": str(e)}
+
+
+def c1_reference(reps: int = 41) -> dict:
+    """Config C1 through the REFERENCE's own collective code: oracle/_ref (src/comm/PeerToPeer.cpp compiled
+    unmodified; prebuilt, it travels with the tree) runs the 2-peer f32 sum-allreduce of 1 MiB buckets, peers as
+    threads over in-memory FIFOs (a memcpy per message, no TCP), combining through the reference's vector
+    adapter (restated: include/Communicator.h needs boost) and through std::transform in place."""
+    try:
+        from oracle import fmi_ref
+
+        if not fmi_ref.available():
+            return {"error": "oracle/_ref not built"}
+        n = MIB // 4
+        ad = fmi_ref.time_allreduce(2, n, reps, adapter=True)
+        bi = fmi_ref.time_allreduce(2, n, reps, adapter=False)
+    except Exception as e:  # reported, never required
+        return {"error": f"{type(e).__name__}: {e}"}
+    return {"config": "C1", "kind": "reference", "peers": 2, "bucket_mib": 1, "reps": reps,
+            "code": "reference src/comm/PeerToPeer.cpp (allreduce_no_order), compiled unmodified (oracle/_ref)",
+            "transport": "peer threads, in-memory FIFOs (oracle/ref_harness.cpp)",
+            "adapter_ms": round(ad, 4), "builtin_inplace_ms": round(bi, 4),
+            "adapter_gib_s": round(1 / 1024 / (ad * 1e-3), 4), "builtin_inplace_gib_s": round(1 / 1024 / (bi * 1e-3), 4)}
 
 
 _JSON_OUT = None

@@ -1,6 +1,7 @@
 """ORACLE — TEST INFRASTRUCTURE ONLY. ctypes access to oracle/_ref/libfmi_ref.so: the REFERENCE's own
 src/comm/PeerToPeer.cpp (compiled unmodified from /root/reference by oracle/Makefile) running over an in-memory
-PeerToPeer transport (oracle/ref_harness.cpp). Imported only by tests/ and tests/golden/make_ref_vectors.py.
+PeerToPeer transport (oracle/ref_harness.cpp). Imported only by tests/, tests/golden/make_ref_vectors.py and
+bench.py's cpu_baseline leg (config C1 through the reference's code, `time_allreduce`).
 
 The library exists where oracle/Makefile could build it: in the build container (the reference is there) and
 on a GPU box that received the prebuilt file with the tree. `available()` says whether it is loadable; the
@@ -118,3 +119,19 @@ def exprs(kind: str, P: int, ordered: bool = False) -> List[str]:
     if kind == "reduce":
         return [expr(kind, P, root=r, ordered=ordered) for r in range(P)]
     return [expr(kind, P, rank=r, ordered=ordered) for r in range(P)]
+
+
+def time_allreduce(P: int, n: int, reps: int, adapter: bool) -> float:
+    """Median ms of the reference's own f32 sum-allreduce (PeerToPeer::allreduce) over P peer threads and the
+    in-memory transport; adapter=True combines through the reference's vector adapter (include/Communicator.h
+    :180-189, restated in oracle/ref_harness.cpp), False through std::transform in place."""
+    lib = _load()
+    f = lib.fmi_ref_time_allreduce
+    f.restype = ctypes.c_int
+    f.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
+                  ctypes.c_char_p, ctypes.c_size_t]
+    ms = ctypes.c_double(0.0)
+    err = ctypes.create_string_buffer(512)
+    if f(P, n, reps, int(adapter), ctypes.byref(ms), err, len(err)) != 0:
+        raise RefError(err.value.decode())
+    return ms.value

@@ -1,5 +1,6 @@
 // ORACLE — TEST INFRASTRUCTURE ONLY (built into oracle/_ref/libfmi_ref.so by oracle/Makefile; loaded only by
-// tests/ and tests/golden/make_ref_vectors.py, never by the product, smoke() or bench.py's timed regions).
+// tests/, tests/golden/make_ref_vectors.py and bench.py's cpu_baseline leg — never by the product, smoke() or
+// bench.py's timed regions).
 //
 // Runs the REFERENCE's own collective algorithms — /root/reference/src/comm/PeerToPeer.cpp, compiled unmodified
 // from where it lies and linked beside this file — over an in-memory transport, so that the float evaluation
@@ -27,6 +28,7 @@
 //   fmi_ref_run   numeric collective over P peers' buckets: every peer's recvbuf and sendbuf after the call.
 //   fmi_ref_expr  symbolic run: each element is a handle to an expression; f.f(a, b) makes "(a+b)" (left operand
 //                 = arg 0 of f.f), so the result is the exact bracketing the reference evaluates.
+//   fmi_ref_time_allreduce  CPU time of the reference's allreduce (bench.py's C1 row of the CPU baseline).
 #include "comm/PeerToPeer.h"
 
 #include <algorithm>
@@ -59,6 +61,7 @@ struct Mailbox {
     std::vector<std::deque<std::vector<char>>> q;  // q[src * P + dst]
     std::string error;                              // first failure; every waiting peer gives up on it
     size_t dropped = 0;                             // sends to a peer id >= P (reference scan_ltr at P = 1)
+    std::vector<std::vector<char>> pool;            // consumed message buffers, reused (no mmap / munmap per message)
 };
 
 constexpr double kRecvTimeoutS = 60.0;
@@ -75,7 +78,13 @@ public:
             ++mb_->dropped;
             return;
         }
-        mb_->q[static_cast<size_t>(peer_id) * mb_->P + dst].emplace_back(buf.buf, buf.buf + buf.len);
+        std::vector<char> msg;
+        if (!mb_->pool.empty()) {
+            msg = std::move(mb_->pool.back());
+            mb_->pool.pop_back();
+        }
+        msg.assign(buf.buf, buf.buf + buf.len);
+        mb_->q[static_cast<size_t>(peer_id) * mb_->P + dst].push_back(std::move(msg));
         mb_->cv.notify_all();
     }
     void recv_object(channel_data buf, peer_num src) override {
@@ -94,6 +103,7 @@ public:
             throw std::runtime_error("message of " + std::to_string(msg.size()) + " B received into a " +
                                      std::to_string(buf.len) + " B buffer");
         std::memcpy(buf.buf, msg.data(), msg.size());
+        mb_->pool.push_back(std::move(msg));
     }
     double get_latency(peer_num, peer_num, std::size_t) override { return 0.0; }
     double get_price(peer_num, peer_num, std::size_t) override { return 0.0; }
@@ -289,4 +299,93 @@ FMI_REF_API long fmi_ref_expr(int coll, int ordered, int P, int rank, int root, 
         buf[k] = '\0';
     }
     return static_cast<long>(s.size());
+}
+
+namespace {
+
+// Reusable barrier for the peer threads of fmi_ref_time.
+class Barrier {
+public:
+    explicit Barrier(int n) : n_(n) {}
+    void wait() {
+        std::unique_lock<std::mutex> lk(mu_);
+        const long gen = gen_;
+        if (++count_ == n_) {
+            count_ = 0;
+            ++gen_;
+            cv_.notify_all();
+            return;
+        }
+        cv_.wait(lk, [&] { return gen_ != gen; });
+    }
+
+private:
+    int n_;
+    int count_ = 0;
+    long gen_ = 0;
+    std::mutex mu_;
+    std::condition_variable cv_;
+};
+
+}  // namespace
+
+// CPU timing of the reference's own allreduce (PeerToPeer::allreduce -> allreduce_no_order, f32 sum) over P
+// peer threads and the in-memory transport: bench.py's cpu_baseline leg reports it for config C1 (2 peers,
+// 1 MiB) beside the C++ port. adapter = 1: the combine is the reference's vector adapter as Communicator
+// builds it for Data<std::vector<float>> (include/Communicator.h:180-189: both buckets copied into vectors,
+// the user's Function called by value, the result memcpy'd back) around the Python layer's
+// std::transform(std::plus) (python/PythonCommunicator.h:131-149) — restated here, since Communicator.h
+// cannot be compiled (boost::property_tree); adapter = 0: std::transform in place. Every repetition starts
+// from the same buckets (restored outside the timed span); the time of one repetition is peer 0's, from a
+// barrier that releases every peer to a barrier every peer reaches after its allreduce. Writes the median.
+FMI_REF_API int fmi_ref_time_allreduce(int P, size_t n, int reps, int adapter, double* median_ms, char* err,
+                                       size_t errlen) {
+    if (P < 1 || reps < 1 || !median_ms) {
+        set_err(err, errlen, "invalid argument");
+        return -1;
+    }
+    const size_t S = n * sizeof(float);
+    std::vector<std::vector<float>> init(P, std::vector<float>(n)), send(P), recv(P, std::vector<float>(n));
+    for (int p = 0; p < P; ++p)
+        for (size_t i = 0; i < n; ++i) init[p][i] = static_cast<float>((i * 2654435761u + p * 40503u) % 2048) / 1024.0f - 1.0f;
+    raw_func f;
+    if (adapter) {
+        const std::function<std::vector<float>(std::vector<float>, std::vector<float>)> user =
+            [](std::vector<float> a, std::vector<float> b) {
+                std::vector<float> res(a.size());
+                std::transform(a.begin(), a.end(), b.begin(), res.begin(), std::plus<float>());
+                return res;
+            };
+        f = [user, S](char* a, char* b) {
+            std::vector<float> va(reinterpret_cast<float*>(a), reinterpret_cast<float*>(a + S));
+            std::vector<float> vb(reinterpret_cast<float*>(b), reinterpret_cast<float*>(b + S));
+            std::vector<float> res = user(va, vb);
+            std::memcpy(a, res.data(), S);
+        };
+    } else {
+        f = make_combine(kSum, kF32, n);
+    }
+    const raw_function rf{f, true, true};
+    Barrier bar(P);
+    std::vector<double> ms(reps);
+    const std::string e = run_peers(
+        P,
+        [&](Loopback& ch, int p) {
+            for (int r = 0; r < reps; ++r) {
+                send[p] = init[p];
+                bar.wait();
+                const auto t0 = std::chrono::steady_clock::now();
+                ch.allreduce({reinterpret_cast<char*>(send[p].data()), S}, {reinterpret_cast<char*>(recv[p].data()), S}, rf);
+                bar.wait();
+                if (p == 0) ms[r] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+            }
+        },
+        nullptr);
+    if (!e.empty()) {
+        set_err(err, errlen, e);
+        return -1;
+    }
+    std::sort(ms.begin(), ms.end());
+    *median_ms = ms[ms.size() / 2];
+    return 0;
 }

@@ -244,3 +244,12 @@ def test_reference_scan_ltr_at_one_peer_sends_to_a_missing_peer():
     recv, send, dropped = ref.run("scan", "sum", [x], ordered=True)
     assert dropped == 1
     assert_bits(recv[0], x, "P = 1 scan_ltr result")
+
+
+@live
+def test_reference_allreduce_timing_runs():
+    """bench.py's cpu_baseline C1 row: the reference's allreduce timed over 2 peer threads, through the vector
+    adapter and in place; the adapter (6 bucket copies per combine) is the slower of the two."""
+    ad = ref.time_allreduce(2, 1 << 16, 5, adapter=True)
+    bi = ref.time_allreduce(2, 1 << 16, 5, adapter=False)
+    assert ad > 0 and bi > 0
