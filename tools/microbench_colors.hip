@@ -1,0 +1,157 @@
+// microbench_colors.hip — exploration harness (not part of the library): does a per-bucket address skew
+// ("colouring") remove the placement spread of the multi-stream kernels? C3's peer scan reads 8 and writes 8
+// separately allocated 64 MiB buckets at the same element offset at the same time; its time varies 170-220 us
+// with the allocation draw, the write side bimodal. Hypothesis: the DRAM channel / bank of an
+// address is a function of its low bits XOR a function of the bucket's base, so buckets whose bases hash alike
+// collide at every offset; skewing bucket k by k x `skew` bytes changes the low bits that meet at one offset.
+// Per draw: 16 buckets of 64 MiB + 1 MiB slack, each its own hipMalloc (a random spacer allocation before each
+// draw varies placement); the same physical buckets are then timed through every skew scheme (views base_k +
+// (k * skew) mod 1 MiB), interleaved over R rounds of K back-to-back launches (events), median per scheme:
+//   write8   out_k = const for the 8 output buckets           (the write side alone)
+//   copy8    out_k = in_k                                      (the scan's traffic, no arithmetic)
+//   scan8    the library's peer scan (fmi_dev_scan_peers, scan_no_order, f32 sum)
+// Build: hipcc -std=c++20 -O3 --offload-arch=gfx950 -ffp-contract=off tools/microbench_colors.hip
+//          -Lfmi_amd/lib -lfmi_dev -Wl,-rpath,$PWD/fmi_amd/lib -o build/mbcol
+// Run:   build/mbcol [draws, default 6] [rounds, default 4]
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <vector>
+
+#include "../fmi_amd/csrc/fmi_internal.h"
+
+using namespace fmi::dev;
+
+#define CHECK(x)                                                                                   \
+    do {                                                                                           \
+        hipError_t e = (x);                                                                        \
+        if (e != hipSuccess) {                                                                     \
+            std::fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e)); \
+            std::exit(1);                                                                          \
+        }                                                                                          \
+    } while (0)
+
+constexpr int kP = 8;
+constexpr int kU = 4;
+using V = u32x4;
+
+struct Ptrs {
+    const V* in[kP];
+    V* out[kP];
+};
+
+__device__ __forceinline__ V ld(const V* p) { return __builtin_nontemporal_load(p); }
+__device__ __forceinline__ void st(V* p, V v) { __builtin_nontemporal_store(v, p); }
+
+__global__ void __launch_bounds__(256) copy8(Ptrs b) {
+    const size_t base = static_cast<size_t>(blockIdx.x) * kU * 256 + threadIdx.x;
+    V v[kP][kU];
+#pragma unroll
+    for (int p = 0; p < kP; ++p)
+#pragma unroll
+        for (int u = 0; u < kU; ++u) v[p][u] = ld(b.in[p] + base + u * 256);
+#pragma unroll
+    for (int p = 0; p < kP; ++p)
+#pragma unroll
+        for (int u = 0; u < kU; ++u) st(b.out[p] + base + u * 256, v[p][u]);
+}
+
+__global__ void __launch_bounds__(256) write8(Ptrs b) {
+    const size_t base = static_cast<size_t>(blockIdx.x) * kU * 256 + threadIdx.x;
+    const V c = {blockIdx.x, threadIdx.x, 7u, 9u};
+#pragma unroll
+    for (int p = 0; p < kP; ++p)
+#pragma unroll
+        for (int u = 0; u < kU; ++u) st(b.out[p] + base + u * 256, c);
+}
+
+int main(int argc, char** argv) {
+    const int draws = argc > 1 ? std::atoi(argv[1]) : 6;
+    const int rounds = argc > 2 ? std::atoi(argv[2]) : 4;
+    constexpr int K = 10;
+    constexpr size_t kBytes = size_t(64) << 20;
+    constexpr size_t kSlack = size_t(1) << 20;
+    const size_t nvec = kBytes / 16;
+    const unsigned grid = static_cast<unsigned>(nvec / (kU * 256));
+    const size_t skews[] = {0, 4096, 8192, 65536, 4352, 256 * 1024 + 4096};
+    CHECK(hipSetDevice(0));
+    if (fmi_dev_init(0) != FMI_OK) {
+        std::fprintf(stderr, "fmi_dev_init: %s\n", fmi_last_error());
+        return 1;
+    }
+    hipEvent_t e0, e1;
+    CHECK(hipEventCreate(&e0));
+    CHECK(hipEventCreate(&e1));
+    hipStream_t s = nullptr;
+    CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    std::mt19937 rng(12345);
+    std::vector<void*> spacers;
+    for (int d = 0; d < draws; ++d) {
+        void* sp = nullptr;
+        CHECK(hipMalloc(&sp, (size_t(2) << 20) * (1 + rng() % 48)));  // kept: later draws land elsewhere
+        spacers.push_back(sp);
+        char* buf[2 * kP];
+        for (auto& b : buf) {
+            CHECK(hipMalloc(reinterpret_cast<void**>(&b), kBytes + kSlack));
+            CHECK(hipMemset(b, 0x3c, kBytes + kSlack));  // finite f32 values for the scan
+        }
+        CHECK(hipDeviceSynchronize());
+        struct Row {
+            const char* kernel;
+            size_t skew;
+            double bytes;
+            std::vector<double> us;
+        };
+        std::vector<Row> rows;
+        for (size_t sk : skews)
+            for (const char* k : {"write8", "copy8", "scan8"})
+                rows.push_back({k, sk, (k[0] == 'w' ? 1.0 : 2.0) * kP * kBytes, {}});
+        for (int r = 0; r < rounds; ++r)
+            for (auto& row : rows) {
+                Ptrs p{};
+                for (int k = 0; k < kP; ++k) {
+                    p.in[k] = reinterpret_cast<const V*>(buf[k] + (k * row.skew) % kSlack);
+                    p.out[k] = reinterpret_cast<V*>(buf[kP + k] + ((kP + k) * row.skew) % kSlack);
+                }
+                auto launch = [&] {
+                    if (row.kernel[0] == 'w') {
+                        write8<<<grid, 256, 0, s>>>(p);
+                    } else if (row.kernel[0] == 'c') {
+                        copy8<<<grid, 256, 0, s>>>(p);
+                    } else {
+                        void* outs[kP];
+                        const void* ins[kP];
+                        for (int k = 0; k < kP; ++k) {
+                            outs[k] = p.out[k];
+                            ins[k] = p.in[k];
+                        }
+                        if (fmi_dev_scan_peers(FMI_OP_SUM, FMI_F32, FMI_ALG_SCAN, outs, ins, kP, kBytes / 4, s) != FMI_OK) {
+                            std::fprintf(stderr, "scan: %s\n", fmi_last_error());
+                            std::exit(1);
+                        }
+                    }
+                };
+                launch();
+                CHECK(hipEventRecord(e0, s));
+                for (int k = 0; k < K; ++k) launch();
+                CHECK(hipEventRecord(e1, s));
+                CHECK(hipEventSynchronize(e1));
+                float ms = 0;
+                CHECK(hipEventElapsedTime(&ms, e0, e1));
+                row.us.push_back(ms * 1e3 / K);
+            }
+        for (auto& row : rows) {
+            std::sort(row.us.begin(), row.us.end());
+            const double us = row.us[row.us.size() / 2];
+            std::printf("{\"draw\": %d, \"kernel\": \"%s\", \"skew\": %zu, \"median_us\": %.2f, \"frac\": %.4f}\n", d,
+                        row.kernel, row.skew, us, row.bytes / (us * 1e-6) / 8e12);
+        }
+        std::fflush(stdout);
+        for (char* b : buf) CHECK(hipFree(b));
+    }
+    for (void* sp : spacers) CHECK(hipFree(sp));
+    return 0;
+}
