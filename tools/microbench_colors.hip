@@ -12,13 +12,14 @@
 //   scan8    the library's peer scan (fmi_dev_scan_peers, scan_no_order, f32 sum)
 // Build: hipcc -std=c++20 -O3 --offload-arch=gfx950 -ffp-contract=off tools/microbench_colors.hip
 //          -Lfmi_amd/lib -lfmi_dev -Wl,-rpath,$PWD/fmi_amd/lib -o build/mbcol
-// Run:   build/mbcol [draws, default 6] [rounds, default 4]
+// Run:   build/mbcol [draws, default 6] [rounds, default 4]    |    build/mbcol rot|rotwarm|streams [draws] [rounds]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <random>
+#include <string>
 #include <vector>
 
 #include "../fmi_amd/csrc/fmi_internal.h"
@@ -41,6 +42,11 @@ using V = u32x4;
 struct Ptrs {
     const V* in[kP];
     V* out[kP];
+};
+
+template <int N>
+struct Ptrs16N {
+    V* p[N];
 };
 
 __device__ __forceinline__ V ld(const V* p) { return __builtin_nontemporal_load(p); }
@@ -68,7 +74,195 @@ __global__ void __launch_bounds__(256) write8(Ptrs b) {
         for (int u = 0; u < kU; ++u) st(b.out[p] + base + u * 256, c);
 }
 
+// Touches one 16-B word per 64 KiB of every bucket of a set (address translations only, a few us): run
+// before a launch, outside its events, it tells translation misses apart from placement ("rotwarm").
+__global__ void __launch_bounds__(256) touch16(Ptrs b, V* sink) {
+    const size_t i = static_cast<size_t>(blockIdx.x) * 256 + threadIdx.x;  // page index within a bucket
+    const int k = blockIdx.y;
+    const V* base = k < kP ? b.in[k] : b.out[k - kP];
+    const V v = __builtin_nontemporal_load(base + i * (65536 / 16));
+    if (v[0] == 0x12345678u && v[1] == 0x9abcdef0u) sink[threadIdx.x] = v;  // never true: keeps the load
+}
+
+// Mode "rot": the bench's protocol — S sets of 16 buckets rotating (no set re-used within 3 GiB of traffic), an
+// event pair around every launch, median per set; allocation size exactly 64 MiB ("exact") or 64 MiB + 16 MiB
+// ("slack", the bucket at the allocation's base), or bucket k at (k x skew) mod 16 MiB into it ("skew*").
+int rotating(int draws, int rounds, bool warm) {
+    constexpr size_t kBytes = size_t(64) << 20;
+    constexpr size_t kSlack = size_t(16) << 20;
+    constexpr int S = 4;
+    const size_t nvec = kBytes / 16;
+    const unsigned grid = static_cast<unsigned>(nvec / (kU * 256));
+    hipStream_t s = nullptr;
+    CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    std::vector<hipEvent_t> ev(2 * S * rounds);
+    V* sink = nullptr;
+    CHECK(hipMalloc(&sink, 4096));
+    for (auto& evt : ev) CHECK(hipEventCreate(&evt));
+    struct Mode {
+        const char* name;
+        size_t alloc;
+        size_t skew;
+    };
+    const Mode modes[] = {{"exact", kBytes, 0},           {"slack", kBytes + kSlack, 0},
+                          {"skew4k", kBytes + kSlack, 4096}, {"skew64k", kBytes + kSlack, 65536},
+                          {"skew256k", kBytes + kSlack, 262144}, {"skew1m", kBytes + kSlack, 1 << 20},
+                          {"skew2m64k", kBytes + kSlack, (2 << 20) + 65536}};
+    for (int d = 0; d < draws; ++d)
+        for (const Mode& m : modes) {
+            std::vector<char*> bufs;
+            Ptrs sets[S];
+            for (int j = 0; j < S; ++j)
+                for (int k = 0; k < 2 * kP; ++k) {
+                    char* b = nullptr;
+                    CHECK(hipMalloc(reinterpret_cast<void**>(&b), m.alloc));
+                    CHECK(hipMemset(b, 0x3c, m.alloc));
+                    bufs.push_back(b);
+                    char* v = b + (k * m.skew) % kSlack;
+                    if (k < kP) sets[j].in[k] = reinterpret_cast<const V*>(v);
+                    else sets[j].out[k - kP] = reinterpret_cast<V*>(v);
+                }
+            CHECK(hipDeviceSynchronize());
+            for (const char* kern : {"write8", "scan8"}) {
+                auto launch = [&](int j) {
+                    const Ptrs& p = sets[j];
+                    if (kern[0] == 'w') {
+                        write8<<<grid, 256, 0, s>>>(p);
+                        return;
+                    }
+                    void* outs[kP];
+                    const void* ins[kP];
+                    for (int k = 0; k < kP; ++k) {
+                        outs[k] = p.out[k];
+                        ins[k] = p.in[k];
+                    }
+                    if (fmi_dev_scan_peers(FMI_OP_SUM, FMI_F32, FMI_ALG_SCAN, outs, ins, kP, kBytes / 4, s) != FMI_OK) {
+                        std::fprintf(stderr, "scan: %s\n", fmi_last_error());
+                        std::exit(1);
+                    }
+                };
+                for (int j = 0; j < S; ++j) launch(j);
+                for (int r = 0; r < rounds; ++r)
+                    for (int j = 0; j < S; ++j) {
+                        if (warm) touch16<<<dim3(kBytes / 65536 / 256, 2 * kP), 256, 0, s>>>(sets[j], sink);
+                        CHECK(hipEventRecord(ev[2 * (r * S + j)], s));
+                        launch(j);
+                        CHECK(hipEventRecord(ev[2 * (r * S + j) + 1], s));
+                    }
+                CHECK(hipStreamSynchronize(s));
+                const double bytes = (kern[0] == 'w' ? 1.0 : 2.0) * kP * kBytes;
+                for (int j = 0; j < S; ++j) {
+                    std::vector<double> us;
+                    for (int r = 0; r < rounds; ++r) {
+                        float ms = 0;
+                        CHECK(hipEventElapsedTime(&ms, ev[2 * (r * S + j)], ev[2 * (r * S + j) + 1]));
+                        us.push_back(ms * 1e3);
+                    }
+                    std::sort(us.begin(), us.end());
+                    const double u = us[us.size() / 2];
+                    std::printf("{\"warm\": %d, \"mode\": \"%s\", \"draw\": %d, \"set\": %d, \"kernel\": \"%s\", \"median_us\": %.2f, "
+                                "\"frac\": %.4f}\n", int(warm), m.name, d, j, kern, u, bytes / (u * 1e-6) / 8e12);
+                }
+            }
+            std::fflush(stdout);
+            for (char* b : bufs) CHECK(hipFree(b));
+        }
+    return 0;
+}
+
+// Mode "streams": the same 512 MiB written (or read) as N concurrent streams of 512/N MiB each (N = 1, 2, 4, 8,
+// 16), S = 4 rotating sets of separate allocations, an event pair per launch, median per set: does the write
+// rate depend on how many streams are open at once?
+template <int N, bool WRITE>
+__global__ void __launch_bounds__(256) streamsN(Ptrs16N<N> b, V* sink) {
+    const size_t base = static_cast<size_t>(blockIdx.x) * kU * 256 + threadIdx.x;
+    if constexpr (WRITE) {
+        const V c = {blockIdx.x, threadIdx.x, 7u, 9u};
+#pragma unroll
+        for (int p = 0; p < N; ++p)
+#pragma unroll
+            for (int u = 0; u < kU; ++u) st(b.p[p] + base + u * 256, c);
+    } else {
+        V acc = {0, 0, 0, 0};
+#pragma unroll
+        for (int p = 0; p < N; ++p)
+#pragma unroll
+            for (int u = 0; u < kU; ++u) acc ^= ld(b.p[p] + base + u * 256);
+        if (acc[0] == 0x12345678u && acc[1] == 0x9abcdef0u) sink[threadIdx.x] = acc;
+    }
+}
+
+template <int N, bool WRITE>
+void run_streams(int draws, int rounds, hipStream_t s, std::vector<hipEvent_t>& ev, V* sink) {
+    constexpr size_t kTotal = size_t(512) << 20;
+    constexpr size_t kEach = kTotal / N;
+    constexpr int S = 4;
+    const unsigned grid = static_cast<unsigned>(kEach / 16 / (kU * 256));
+    for (int d = 0; d < draws; ++d) {
+        std::vector<void*> bufs;
+        Ptrs16N<N> sets[S];
+        for (int j = 0; j < S; ++j)
+            for (int k = 0; k < N; ++k) {
+                void* b = nullptr;
+                CHECK(hipMalloc(&b, kEach));
+                CHECK(hipMemset(b, 0x3c, kEach));
+                bufs.push_back(b);
+                sets[j].p[k] = static_cast<V*>(b);
+            }
+        CHECK(hipDeviceSynchronize());
+        for (int j = 0; j < S; ++j) streamsN<N, WRITE><<<grid, 256, 0, s>>>(sets[j], sink);
+        for (int r = 0; r < rounds; ++r)
+            for (int j = 0; j < S; ++j) {
+                CHECK(hipEventRecord(ev[2 * (r * S + j)], s));
+                streamsN<N, WRITE><<<grid, 256, 0, s>>>(sets[j], sink);
+                CHECK(hipEventRecord(ev[2 * (r * S + j) + 1], s));
+            }
+        CHECK(hipStreamSynchronize(s));
+        for (int j = 0; j < S; ++j) {
+            std::vector<double> us;
+            for (int r = 0; r < rounds; ++r) {
+                float ms = 0;
+                CHECK(hipEventElapsedTime(&ms, ev[2 * (r * S + j)], ev[2 * (r * S + j) + 1]));
+                us.push_back(ms * 1e3);
+            }
+            std::sort(us.begin(), us.end());
+            const double u = us[us.size() / 2];
+            std::printf("{\"streams\": %d, \"op\": \"%s\", \"draw\": %d, \"set\": %d, \"median_us\": %.2f, \"frac\": %.4f}\n",
+                        N, WRITE ? "write" : "read", d, j, u, kTotal / (u * 1e-6) / 8e12);
+        }
+        std::fflush(stdout);
+        for (void* b : bufs) CHECK(hipFree(b));
+    }
+}
+
+int streams(int draws, int rounds) {
+    hipStream_t s = nullptr;
+    CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    std::vector<hipEvent_t> ev(2 * 4 * rounds);
+    for (auto& evt : ev) CHECK(hipEventCreate(&evt));
+    V* sink = nullptr;
+    CHECK(hipMalloc(&sink, 4096));
+    run_streams<1, true>(draws, rounds, s, ev, sink);
+    run_streams<2, true>(draws, rounds, s, ev, sink);
+    run_streams<4, true>(draws, rounds, s, ev, sink);
+    run_streams<8, true>(draws, rounds, s, ev, sink);
+    run_streams<16, true>(draws, rounds, s, ev, sink);
+    run_streams<1, false>(draws, rounds, s, ev, sink);
+    run_streams<8, false>(draws, rounds, s, ev, sink);
+    return 0;
+}
+
 int main(int argc, char** argv) {
+    if (argc > 1 && std::string(argv[1]) == "streams") {
+        CHECK(hipSetDevice(0));
+        return streams(argc > 2 ? std::atoi(argv[2]) : 2, argc > 3 ? std::atoi(argv[3]) : 6);
+    }
+    if (argc > 1 && (std::string(argv[1]) == "rot" || std::string(argv[1]) == "rotwarm")) {
+        CHECK(hipSetDevice(0));
+        if (fmi_dev_init(0) != FMI_OK) return 1;
+        return rotating(argc > 2 ? std::atoi(argv[2]) : 3, argc > 3 ? std::atoi(argv[3]) : 5,
+                        std::string(argv[1]) == "rotwarm");
+    }
     const int draws = argc > 1 ? std::atoi(argv[1]) : 6;
     const int rounds = argc > 2 ? std::atoi(argv[2]) : 4;
     constexpr int K = 10;
