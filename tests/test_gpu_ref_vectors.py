@@ -120,3 +120,54 @@ def test_communicator_equals_reference_outputs(device, case):
                          f"{key} comm reduce root {root}")
         assert_bit_equal(res[root][f"reduce_ltr/root{root}/recv"], VEC[f"{key}/reduce_ltr/root{root}/recv"],
                          f"{key} comm reduce_ltr root {root}")
+
+
+def test_empty_buckets_are_no_ops(device):
+    """Zero-element buckets, which the reference accepts (Data<std::vector<A>> of size 0: size_in_bytes 0,
+    PeerToPeer exchanges empty messages and combines nothing): every P-way entry point and every communicator
+    collective returns success and leaves every buffer as it was. Checked against the reference itself where
+    oracle/_ref travels with the tree (its allreduce / reduce / scan of empty buckets complete)."""
+    from fmi_amd.comm import Comm, Transport, unique_id
+    from oracle import fmi_ref as ref
+
+    guard = Bucket(16, np.float32)
+    guard.upload(np.arange(16, dtype=np.float32))
+    empty = guard.view(0, 0)
+    for P in (1, 2, 5, 17, 40):
+        ins = [empty] * P
+        for alg in (Alg.ALLREDUCE, Alg.REDUCE, Alg.REDUCE_LTR):
+            fmi_amd.reduce_tree(Op.SUM, alg, empty, ins, rank=P - 1)
+        for alg in (Alg.SCAN, Alg.SCAN_LTR):
+            fmi_amd.scan_peers(Op.MAX, alg, [empty] * P, ins)
+    fmi_amd.sync()
+    assert_bit_equal(guard.numpy(), np.arange(16, dtype=np.float32), "nothing written")
+    if ref.available():
+        for coll in ("allreduce", "reduce", "scan"):
+            recv, send, _ = ref.run(coll, "sum", [np.zeros(0, np.float32)] * 3)
+            assert recv.shape == (3, 0) and send.shape == (3, 0)
+
+    N = 3
+    uid = unique_id(Transport.LOCAL)
+    errors = []
+
+    def rank(r):
+        try:
+            c = Comm(uid, N, r)
+            s, o = Bucket(0, np.float32), Bucket(0, np.float32)
+            for ordered in (False, True):
+                c.allreduce(Op.SUM, s, o, ordered=ordered)
+                c.scan(Op.SUM, s, o, ordered=ordered)
+                c.reduce(Op.SUM, s, o if r == 1 else None, 1, ordered=ordered)
+            c.reduce(Op.SUM, s, o if r == 1 else None, 1, sendbuf_partials=True)
+            fmi_amd.sync()
+            c.destroy()
+        except BaseException as e:  # noqa: BLE001 - re-raised below
+            errors.append(e)
+
+    threads = [threading.Thread(target=rank, args=(r,)) for r in range(N)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=60)
+    if errors:
+        raise errors[0]
