@@ -211,6 +211,32 @@ def test_schedule_expr_rejects_bad_args():
         fmi_amd.schedule_expr(Alg.ALLREDUCE, 4, 4)
 
 
+def _offload_bundles(data: bytes):
+    """The offload bundles of a .hip_fatbin section, one per translation unit: compressed ("CCOB" header,
+    version 2/3: the bundle's total size at byte 8, 32- or 64-bit; the library is built with
+    --offload-compress) or plain ("__CLANG_OFFLOAD_BUNDLE__", running to the next magic)."""
+    import struct
+
+    plain = b"__CLANG_OFFLOAD_BUNDLE__"
+    pos, out = 0, []
+    while True:
+        c, p = data.find(b"CCOB", pos), data.find(plain, pos)
+        starts = [x for x in (c, p) if x >= 0]
+        if not starts:
+            return out
+        pos = min(starts)
+        if pos == c:
+            version = struct.unpack_from("<H", data, pos + 4)[0]
+            total = struct.unpack_from("<Q" if version >= 3 else "<I", data, pos + 8)[0]
+            out.append(data[pos:pos + total])
+            pos += total
+        else:
+            nxt = [x for x in (data.find(b"CCOB", pos + 1), data.find(plain, pos + 1)) if x >= 0]
+            end = min(nxt) if nxt else len(data)
+            out.append(data[pos:end])
+            pos = end
+
+
 def test_no_kernel_spills_to_scratch(tmp_path):
     """Every gfx950 kernel in libfmi_dev.so keeps its values in registers: .private_segment_fixed_size is 0
     for all of them (fused programs index their value arrays with constants only; a select chain over
@@ -224,12 +250,10 @@ def test_no_kernel_spills_to_scratch(tmp_path):
     subprocess.run([os.path.join(llvm, "llvm-objcopy"), f"--dump-section=.hip_fatbin={fat}", _lib.LIB_PATH,
                     str(tmp_path / "lib.so")], check=True)
     data = fat.read_bytes()
-    magic = b"__CLANG_OFFLOAD_BUNDLE__"
-    starts = [m.start() for m in re.finditer(re.escape(magic), data)] + [len(data)]
     kernels = spilled = 0
-    for k in range(len(starts) - 1):
+    for k, bundle in enumerate(_offload_bundles(data)):
         b, elf = tmp_path / f"b{k}", tmp_path / f"b{k}.elf"
-        b.write_bytes(data[starts[k]:starts[k + 1]])
+        b.write_bytes(bundle)
         subprocess.run([os.path.join(llvm, "clang-offload-bundler"), "--unbundle", "--type=o", f"--input={b}",
                         f"--output={elf}", "--targets=hipv4-amdgcn-amd-amdhsa--gfx950"], check=True)
         notes = subprocess.run([os.path.join(llvm, "llvm-readelf"), "--notes", str(elf)], check=True,
