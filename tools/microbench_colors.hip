@@ -12,7 +12,7 @@
 //   scan8    the library's peer scan (fmi_dev_scan_peers, scan_no_order, f32 sum)
 // Build: hipcc -std=c++20 -O3 --offload-arch=gfx950 -ffp-contract=off tools/microbench_colors.hip
 //          -Lfmi_amd/lib -lfmi_dev -Wl,-rpath,$PWD/fmi_amd/lib -o build/mbcol
-// Run:   build/mbcol [draws, default 6] [rounds, default 4]    |    build/mbcol rot|rotwarm|streams [draws] [rounds]
+// Run:   build/mbcol [draws, default 6] [rounds, default 4]    |    build/mbcol rot|rotwarm|streams|contig|libcontig [draws] [rounds]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -193,7 +193,7 @@ __global__ void __launch_bounds__(256) streamsN(Ptrs16N<N> b, V* sink) {
 }
 
 template <int N, bool WRITE>
-void run_streams(int draws, int rounds, hipStream_t s, std::vector<hipEvent_t>& ev, V* sink) {
+void run_streams(int draws, int rounds, hipStream_t s, std::vector<hipEvent_t>& ev, V* sink, unsigned flags = 0) {
     constexpr size_t kTotal = size_t(512) << 20;
     constexpr size_t kEach = kTotal / N;
     constexpr int S = 4;
@@ -204,7 +204,8 @@ void run_streams(int draws, int rounds, hipStream_t s, std::vector<hipEvent_t>& 
         for (int j = 0; j < S; ++j)
             for (int k = 0; k < N; ++k) {
                 void* b = nullptr;
-                CHECK(hipMalloc(&b, kEach));
+                if (flags) CHECK(hipExtMallocWithFlags(&b, kEach, flags));
+                else CHECK(hipMalloc(&b, kEach));
                 CHECK(hipMemset(b, 0x3c, kEach));
                 bufs.push_back(b);
                 sets[j].p[k] = static_cast<V*>(b);
@@ -227,8 +228,8 @@ void run_streams(int draws, int rounds, hipStream_t s, std::vector<hipEvent_t>& 
             }
             std::sort(us.begin(), us.end());
             const double u = us[us.size() / 2];
-            std::printf("{\"streams\": %d, \"op\": \"%s\", \"draw\": %d, \"set\": %d, \"median_us\": %.2f, \"frac\": %.4f}\n",
-                        N, WRITE ? "write" : "read", d, j, u, kTotal / (u * 1e-6) / 8e12);
+            std::printf("{\"streams\": %d, \"op\": \"%s\", \"alloc_flags\": %u, \"draw\": %d, \"set\": %d, \"median_us\": %.2f, "
+                        "\"frac\": %.4f}\n", N, WRITE ? "write" : "read", flags, d, j, u, kTotal / (u * 1e-6) / 8e12);
         }
         std::fflush(stdout);
         for (void* b : bufs) CHECK(hipFree(b));
@@ -252,7 +253,99 @@ int streams(int draws, int rounds) {
     return 0;
 }
 
+// Mode "contig": 8 write streams from hipMalloc against hipExtMallocWithFlags(hipDeviceMallocContiguous)
+// (physically contiguous buckets), interleaved draw by draw.
+int contig(int draws, int rounds) {
+    hipStream_t s = nullptr;
+    CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    std::vector<hipEvent_t> ev(2 * 4 * rounds);
+    for (auto& evt : ev) CHECK(hipEventCreate(&evt));
+    V* sink = nullptr;
+    CHECK(hipMalloc(&sink, 4096));
+    for (int d = 0; d < draws; ++d) {
+        run_streams<8, true>(1, rounds, s, ev, sink, 0);
+        run_streams<8, true>(1, rounds, s, ev, sink, hipDeviceMallocContiguous);
+        run_streams<1, true>(1, rounds, s, ev, sink, 0);
+        run_streams<1, true>(1, rounds, s, ev, sink, hipDeviceMallocContiguous);
+    }
+    return 0;
+}
+
+// Mode "libcontig": the library's own C2 pair kernel (fmi_dev_reduce_pair, f32 sum, 256 MiB, 16 rotating pairs)
+// and C3 scan (fmi_dev_scan_peers, 8 x 64 MiB, 4 rotating sets) on buckets from hipMalloc against
+// hipExtMallocWithFlags(hipDeviceMallocContiguous); two HIP events around each pass of back-to-back launches.
+double lib_pass(bool scan, unsigned flags, int passes, hipStream_t s) {
+    const int S = scan ? 4 : 16;
+    const size_t bytes = scan ? size_t(64) << 20 : size_t(256) << 20;
+    const int per = scan ? 16 : 2;
+    std::vector<void*> b(static_cast<size_t>(S) * per);
+    for (auto& p : b) {
+        if (flags) CHECK(hipExtMallocWithFlags(&p, bytes, flags));
+        else CHECK(hipMalloc(&p, bytes));
+        CHECK(hipMemset(p, 0x3c, bytes));
+    }
+    CHECK(hipDeviceSynchronize());
+    auto launch = [&](int j) {
+        void** q = &b[static_cast<size_t>(j) * per];
+        int rc;
+        if (scan) {
+            const void* ins[kP];
+            void* outs[kP];
+            for (int k = 0; k < kP; ++k) {
+                ins[k] = q[k];
+                outs[k] = q[kP + k];
+            }
+            rc = fmi_dev_scan_peers(FMI_OP_SUM, FMI_F32, FMI_ALG_SCAN, outs, ins, kP, bytes / 4, s);
+        } else {
+            rc = fmi_dev_reduce_pair(FMI_OP_SUM, FMI_F32, q[0], q[1], bytes / 4, s);
+        }
+        if (rc != FMI_OK) {
+            std::fprintf(stderr, "launch: %s\n", fmi_last_error());
+            std::exit(1);
+        }
+    };
+    for (int j = 0; j < S; ++j) launch(j);
+    hipEvent_t e0, e1;
+    CHECK(hipEventCreate(&e0));
+    CHECK(hipEventCreate(&e1));
+    CHECK(hipEventRecord(e0, s));
+    for (int r = 0; r < passes; ++r)
+        for (int j = 0; j < S; ++j) launch(j);
+    CHECK(hipEventRecord(e1, s));
+    CHECK(hipEventSynchronize(e1));
+    float ms = 0;
+    CHECK(hipEventElapsedTime(&ms, e0, e1));
+    CHECK(hipEventDestroy(e0));
+    CHECK(hipEventDestroy(e1));
+    for (void* p : b) CHECK(hipFree(p));
+    return ms * 1e3 / (passes * S);
+}
+
+int libcontig(int draws) {
+    hipStream_t s = nullptr;
+    CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    for (int d = 0; d < draws; ++d)
+        for (bool scan : {false, true})
+            for (unsigned flags : {0u, unsigned(hipDeviceMallocContiguous)}) {
+                const double us = lib_pass(scan, flags, scan ? 6 : 4, s);
+                const double bytes = scan ? 2.0 * kP * (64 << 20) : 3.0 * (256 << 20);
+                std::printf("{\"kernel\": \"%s\", \"alloc_flags\": %u, \"draw\": %d, \"mean_us\": %.2f, \"frac\": %.4f}\n",
+                            scan ? "scan8" : "pair_c2", flags, d, us, bytes / (us * 1e-6) / 8e12);
+                std::fflush(stdout);
+            }
+    return 0;
+}
+
 int main(int argc, char** argv) {
+    if (argc > 1 && std::string(argv[1]) == "libcontig") {
+        CHECK(hipSetDevice(0));
+        if (fmi_dev_init(0) != FMI_OK) return 1;
+        return libcontig(argc > 2 ? std::atoi(argv[2]) : 4);
+    }
+    if (argc > 1 && std::string(argv[1]) == "contig") {
+        CHECK(hipSetDevice(0));
+        return contig(argc > 2 ? std::atoi(argv[2]) : 3, argc > 3 ? std::atoi(argv[3]) : 6);
+    }
     if (argc > 1 && std::string(argv[1]) == "streams") {
         CHECK(hipSetDevice(0));
         return streams(argc > 2 ? std::atoi(argv[2]) : 2, argc > 3 ? std::atoi(argv[3]) : 6);
