@@ -253,3 +253,22 @@ def test_reference_allreduce_timing_runs():
     ad = ref.time_allreduce(2, 1 << 16, 5, adapter=True)
     bi = ref.time_allreduce(2, 1 << 16, 5, adapter=False)
     assert ad > 0 and bi > 0
+
+
+@live
+@pytest.mark.parametrize("P", [1, 2, 3, 5, 8, 13, 17])
+def test_live_reference_bcast_and_gather_equal_oracle(P):
+    """The binomial bcast and gather the oracle restates (PeerToPeer.cpp:14-27, :186-239; gather carries
+    reduce_ltr), against the reference's own, every root: the root's gathered buckets in real-id order (the
+    wraparound copy of :213-222 included) and every peer's bucket after the bcast."""
+    rng = np.random.default_rng(P)
+    xs = [rng.standard_normal(7).astype(np.float32) for _ in range(P)]
+    for root in range(P):
+        recv, _, _ = ref.run("gather", "sum", xs, root=root)
+        want = orc.gather(xs, root)
+        assert_bits(recv[root], np.concatenate(want), f"gather P={P} root {root}")
+        _, send, _ = ref.run("bcast", "sum", xs, root=root)
+        got = orc.bcast(xs, root)
+        for p in range(P):
+            assert_bits(send[p], got[p], f"bcast P={P} root {root} peer {p}")
+            assert_bits(send[p], xs[root], f"bcast P={P} root {root} peer {p} holds the root's bucket")
