@@ -5,7 +5,9 @@
 N = 1 (config C2). One *step* = one pairwise combine a = a + b of two 256 MiB float32 peer buckets
 resident in HBM — the reference's `f.f(a, b)` (include/Communicator.h:180-189) on the device, rotating over
 16 buffer sets (8 GiB; the rotation runs on from the warm-up, so no step re-reads a bucket the 256 MB
-Infinity Cache still holds, see --sets). value = 256 MiB / (wall time per step).
+Infinity Cache still holds, see --sets). value = 256 MiB / (wall time per step). After the timed region every
+set's bucket is checked bit for bit against numpy's float32 a + b repeated once per launch of that set, on three
+windows (`self_check`); a mismatch prints the line and exits 1.
 
 N > 1 (config C4's shape at the metric's bucket size). One *step* = the N-peer float32 sum-allreduce of
 256 MiB buckets, ONE FMI peer per GPU (one process per GPU), through the product C-ABI communicator
@@ -315,10 +317,16 @@ def run_single(args):
     nbytes = n * 4
     sets = [tuple(Bucket(n, np.float32).fill_synthetic(42 + s, j) for j in range(2)) for s in range(args.sets)]
     fmi_amd.sync()
+    # self-check windows (head, middle, tail of every set's buckets), read before the first launch
+    win = 4096
+    offs = [0, (n // 2) // 64 * 64, n - win]
+    before = [[(a.view(o, win).numpy(), b.view(o, win).numpy()) for o in offs] for a, b in sets]
+    launches = [0] * len(sets)
 
     def step(k):  # k runs on from the warm-up, so every set is re-used exactly len(sets) steps later
         a, b = sets[k % len(sets)]
         fmi_amd.reduce_pair(Op.SUM, a, b)
+        launches[k % len(sets)] += 1
 
     for k in range(args.warmup):
         step(k)
@@ -344,6 +352,7 @@ def run_single(args):
         pairs[k][1].record()
     fmi_amd.sync()
     isolated_us = 1e3 * sum(a.elapsed_ms(b) for a, b in pairs) / probe
+    check = c2_self_check(sets, offs, win, before, launches)
     for a, b in sets:
         a.free()
         b.free()
@@ -354,6 +363,7 @@ def run_single(args):
                      "C2: 1-GPU pairwise float32 sum-reduce of two 256 MiB device-resident peer buckets",
                      "single GPU (2 peers resident)", n, roof)
     line["config"]["peers"] = 2
+    line["self_check"] = check
     line["allreduce_1peer"] = one_peer_allreduce(n)
     if not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args)
@@ -370,6 +380,29 @@ def run_single(args):
         except Exception as e:  # reported, never fails the measured line
             line["c5"] = f"failed: {type(e).__name__}: {e}"
     print(json.dumps(line), file=json_out(), flush=True)
+    if not check["ok"]:
+        print("bench: C2 self-check FAILED", file=sys.stderr, flush=True)
+        sys.exit(1)
+
+
+def c2_self_check(sets, offs, win, before, launches) -> dict:
+    """The timed C2 combines checked in the run: every set's a was combined in place with its b `launches[s]`
+    times (warm-up, timed and probe launches), so on each window a must equal numpy's float32 a + b repeated
+    that many times (IEEE round-to-nearest, the reference's std::plus<float>) — bit for bit."""
+    import numpy as np
+
+    bad = checked = 0
+    for s, (a, b) in enumerate(sets):
+        for o, (a0, b0) in zip(offs, before[s]):
+            want = a0.copy()
+            for _ in range(launches[s]):
+                want = want + b0
+            got = a.view(o, win).numpy()
+            bad += int(np.count_nonzero(got.view(np.uint32) != want.view(np.uint32)))
+            checked += win
+    return {"ok": bad == 0, "mismatches": bad, "elements_checked": checked,
+            "against": "numpy float32 a + b repeated once per launch of each set (warm-up, timed, probe), "
+                       "on the head, middle and tail window of every set, bit-exact"}
 
 
 def one_peer_allreduce(n: int, launches: int = 20, sets: int = 4) -> dict:

@@ -133,3 +133,22 @@ def test_bench_py_force_dist_rccl_world1():
     assert "one_rank_exchange" in line["config"] and line["self_check"]["ok"] and line["c4"]["tree"]["self_check"]["ok"]
     assert line["c4"]["rccl"]["self_check"]["ok"]  # ncclReduceScatter + ncclAllGather with one rank
     _check_topology_and_anchor(line, 1, "rccl")
+
+
+def test_bench_py_n1_line_self_checks_the_timed_combines():
+    """N = 1 (config C2): the line carries a passing self_check — every set's bucket after its warm-up, timed and
+    probe launches equals numpy's float32 a + b repeated that many times, bit for bit, on three windows per set —
+    and is the only stdout line."""
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "FMI_BENCH_LAUNCHED"):
+        env.pop(k, None)
+    cmd = [sys.executable, "bench.py", "--steps", "10", "--warmup", "3", "--sets", "4", "--no-cpu-baseline",
+           "--no-c3", "--no-c5"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = r.stdout.strip().splitlines()
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    chk = line["self_check"]
+    assert line["n_gpus"] == 1 and line["value"] > 0 and chk["ok"] and chk["mismatches"] == 0
+    assert chk["elements_checked"] == 4 * 3 * 4096
