@@ -272,3 +272,24 @@ def test_live_reference_bcast_and_gather_equal_oracle(P):
         for p in range(P):
             assert_bits(send[p], got[p], f"bcast P={P} root {root} peer {p}")
             assert_bits(send[p], xs[root], f"bcast P={P} root {root} peer {p} holds the root's bucket")
+
+
+@live
+def test_reference_library_is_built_from_the_reference_alone():
+    """oracle/_ref/libfmi_ref.so holds the reference's PeerToPeer code (its symbols are defined in the library)
+    and needs nothing of FMI from elsewhere: no undefined FMI symbol (the link ran with -Wl,-z,defs), so no
+    stand-in for a missing reference part exists; its only C entry points are the harness's."""
+    import subprocess
+
+    nm = ["nm", "-C", "--defined-only", ref.LIB_PATH]
+    defined = subprocess.run(nm, check=True, capture_output=True, text=True).stdout
+    for fn in ("PeerToPeer::allreduce_no_order", "PeerToPeer::scan_no_order", "PeerToPeer::reduce_no_order",
+               "PeerToPeer::reduce_ltr", "PeerToPeer::scan_ltr", "PeerToPeer::gather", "PeerToPeer::bcast"):
+        assert fn in defined, fn
+    undefined = subprocess.run(["nm", "-C", "-D", "--undefined-only", ref.LIB_PATH], check=True,
+                               capture_output=True, text=True).stdout
+    assert "FMI" not in undefined, undefined
+    dyn = subprocess.run(["nm", "-D", "--defined-only", ref.LIB_PATH], check=True, capture_output=True,
+                         text=True).stdout
+    exported = sorted(line.split()[-1] for line in dyn.splitlines() if " T " in line)
+    assert exported == ["fmi_ref_expr", "fmi_ref_run", "fmi_ref_time_allreduce"], exported
