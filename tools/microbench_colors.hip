@@ -12,7 +12,7 @@
 //   scan8    the library's peer scan (fmi_dev_scan_peers, scan_no_order, f32 sum)
 // Build: hipcc -std=c++20 -O3 --offload-arch=gfx950 -ffp-contract=off tools/microbench_colors.hip
 //          -Lfmi_amd/lib -lfmi_dev -Wl,-rpath,$PWD/fmi_amd/lib -o build/mbcol
-// Run:   build/mbcol [draws, default 6] [rounds, default 4]    |    build/mbcol rot|rotwarm|streams|contig|libcontig [draws] [rounds]
+// Run:   build/mbcol [draws, default 6] [rounds, default 4]    |    build/mbcol rot|rotwarm|streams|contig|libcontig|vmm [draws] [rounds]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -336,7 +336,108 @@ int libcontig(int draws) {
     return 0;
 }
 
+// Mode "vmm": 8 write streams into buckets placed with the HIP virtual-memory API — physical memory from
+// hipMemCreate mapped at virtual addresses aligned to 1 GiB (one reservation per bucket), or all 8 buckets
+// back to back in one 1 GiB-aligned reservation — against hipMalloc, rotating sets as in "streams". Does the
+// virtual placement (translation fragments, alignment) decide the write rate?
+struct VmmBuf {
+    void* va = nullptr;
+    size_t reserved = 0;
+    hipMemGenericAllocationHandle_t h{};
+};
+
+void run_vmm_mode(int mode, int rounds, hipStream_t s, std::vector<hipEvent_t>& ev, V* sink, int d) {
+    constexpr size_t kEach = size_t(64) << 20;
+    constexpr int N = 8, S = 4;
+    const unsigned grid = static_cast<unsigned>(kEach / 16 / (kU * 256));
+    hipMemAllocationProp prop{};
+    prop.type = hipMemAllocationTypePinned;
+    prop.location.type = hipMemLocationTypeDevice;
+    prop.location.id = 0;
+    hipMemAccessDesc acc{};
+    acc.location = prop.location;
+    acc.flags = hipMemAccessFlagsProtReadWrite;
+    std::vector<void*> plain;
+    std::vector<VmmBuf> vm;
+    std::vector<void*> ranges;
+    Ptrs16N<N> sets[S];
+    for (int j = 0; j < S; ++j) {
+        char* block = nullptr;
+        if (mode == 2) {
+            CHECK(hipMemAddressReserve(reinterpret_cast<void**>(&block), N * kEach, size_t(1) << 30, nullptr, 0));
+            ranges.push_back(block);
+        }
+        for (int k = 0; k < N; ++k) {
+            void* p = nullptr;
+            if (mode == 0) {
+                CHECK(hipMalloc(&p, kEach));
+                plain.push_back(p);
+            } else {
+                VmmBuf b;
+                if (mode == 1) {
+                    CHECK(hipMemAddressReserve(&b.va, kEach, size_t(1) << 30, nullptr, 0));
+                    b.reserved = kEach;
+                } else {
+                    b.va = block + k * kEach;
+                }
+                CHECK(hipMemCreate(&b.h, kEach, &prop, 0));
+                CHECK(hipMemMap(b.va, kEach, 0, b.h, 0));
+                CHECK(hipMemSetAccess(b.va, kEach, &acc, 1));
+                p = b.va;
+                vm.push_back(b);
+            }
+            CHECK(hipMemset(p, 0x3c, kEach));
+            sets[j].p[k] = static_cast<V*>(p);
+        }
+    }
+    CHECK(hipDeviceSynchronize());
+    for (int j = 0; j < S; ++j) streamsN<N, true><<<grid, 256, 0, s>>>(sets[j], sink);
+    for (int r = 0; r < rounds; ++r)
+        for (int j = 0; j < S; ++j) {
+            CHECK(hipEventRecord(ev[2 * (r * S + j)], s));
+            streamsN<N, true><<<grid, 256, 0, s>>>(sets[j], sink);
+            CHECK(hipEventRecord(ev[2 * (r * S + j) + 1], s));
+        }
+    CHECK(hipStreamSynchronize(s));
+    for (int j = 0; j < S; ++j) {
+        std::vector<double> us;
+        for (int r = 0; r < rounds; ++r) {
+            float ms = 0;
+            CHECK(hipEventElapsedTime(&ms, ev[2 * (r * S + j)], ev[2 * (r * S + j) + 1]));
+            us.push_back(ms * 1e3);
+        }
+        std::sort(us.begin(), us.end());
+        const double u = us[us.size() / 2];
+        std::printf("{\"vmm_mode\": %d, \"draw\": %d, \"set\": %d, \"median_us\": %.2f, \"frac\": %.4f}\n", mode, d, j, u,
+                    N * kEach / (u * 1e-6) / 8e12);
+    }
+    std::fflush(stdout);
+    for (void* p : plain) CHECK(hipFree(p));
+    for (auto& b : vm) {
+        CHECK(hipMemUnmap(b.va, kEach));
+        CHECK(hipMemRelease(b.h));
+        if (b.reserved) CHECK(hipMemAddressFree(b.va, b.reserved));
+    }
+    for (void* r : ranges) CHECK(hipMemAddressFree(r, N * kEach));
+}
+
+int vmm(int draws, int rounds) {
+    hipStream_t s = nullptr;
+    CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    std::vector<hipEvent_t> ev(2 * 4 * rounds);
+    for (auto& evt : ev) CHECK(hipEventCreate(&evt));
+    V* sink = nullptr;
+    CHECK(hipMalloc(&sink, 4096));
+    for (int d = 0; d < draws; ++d)
+        for (int mode : {0, 1, 2}) run_vmm_mode(mode, rounds, s, ev, sink, d);
+    return 0;
+}
+
 int main(int argc, char** argv) {
+    if (argc > 1 && std::string(argv[1]) == "vmm") {
+        CHECK(hipSetDevice(0));
+        return vmm(argc > 2 ? std::atoi(argv[2]) : 3, argc > 3 ? std::atoi(argv[3]) : 6);
+    }
     if (argc > 1 && std::string(argv[1]) == "libcontig") {
         CHECK(hipSetDevice(0));
         if (fmi_dev_init(0) != FMI_OK) return 1;
