@@ -196,3 +196,38 @@ def test_pmc_summary_splits_one_kernel_by_launch_shape(tmp_path):
         assert e["algorithmic_bytes_per_launch"] == 2 * mib << 20
         assert e["hbm_bytes_per_launch"] == 2 * mib << 20  # 2 x fetch KiB + write KiB = 2 x bucket
         assert e["trace"]["avg_ns"] == ns and e["trace"]["calls"] == (3 if g == big else 5)
+
+
+def test_c2_self_check_counts_every_launch_and_catches_one_flipped_bit():
+    """bench.py's N = 1 self_check (c2_self_check) on host stand-ins for the buckets: after each set's a was
+    combined in place with b as many times as `launches` says, the check passes bit for bit; one wrong element
+    in one window (or a miscounted launch) fails it."""
+    import numpy as np
+
+    import bench
+
+    class Host:
+        def __init__(self, arr):
+            self.arr = arr
+
+        def view(self, o, n):
+            return Host(self.arr[o:o + n])
+
+        def numpy(self):
+            return self.arr.copy()
+
+    rng = np.random.default_rng(3)
+    n, win = 1 << 14, 4096
+    offs = [0, (n // 2) // 64 * 64, n - win]
+    sets = [(Host(rng.random(n, dtype=np.float32)), Host(rng.random(n, dtype=np.float32))) for _ in range(3)]
+    before = [[(a.view(o, win).numpy(), b.view(o, win).numpy()) for o in offs] for a, b in sets]
+    launches = [5, 4, 4]
+    for (a, b), k in zip(sets, launches):
+        for _ in range(k):
+            a.arr[:] = a.arr + b.arr
+    ok = bench.c2_self_check(sets, offs, win, before, launches)
+    assert ok["ok"] and ok["mismatches"] == 0 and ok["elements_checked"] == 3 * 3 * win
+    assert not bench.c2_self_check(sets, offs, win, before, [4, 4, 4])["ok"]  # a miscounted launch
+    sets[1][0].arr[n // 2 + 7] = np.nextafter(sets[1][0].arr[n // 2 + 7], np.float32(2))
+    bad = bench.c2_self_check(sets, offs, win, before, launches)
+    assert not bad["ok"] and bad["mismatches"] == 1
