@@ -199,6 +199,8 @@ def c1_reference(reps: int = 41) -> dict:
 
 
 _JSON_OUT = None
+_LINE_PRINTED = False  # the one JSON line is out (N > 1: by the emitter, on every rank's view)
+_WATCH = None  # N > 1: the phase watch of this rank (names the phase an error line reports)
 
 
 def json_out():
@@ -228,10 +230,12 @@ class _Emitter:
         self.done = False
 
     def emit(self):
+        global _LINE_PRINTED
         with self.lock:
             if self.done:
                 return
             self.done = True
+            _LINE_PRINTED = True
             if self.rank == 0:
                 try:
                     text = json.dumps(self.line)
@@ -628,7 +632,8 @@ def run_dist(args, world, rank, local_rank):
     import torch
     import torch.distributed as dist
 
-    watch = _PhaseWatch(args.measure_deadline, rank)
+    global _WATCH
+    watch = _WATCH = _PhaseWatch(args.measure_deadline, rank)
 
     proc = args.transport == "proc"
     dev = local_rank % max(1, torch.cuda.device_count()) if proc else local_rank
@@ -890,7 +895,14 @@ def main():
     if os.environ.get("FMI_BENCH_TEST_FAIL_RANK") == str(rank) and world > 1:  # CPU test of the launcher's status
         raise SystemExit(f"bench: rank {rank} failing on purpose (FMI_BENCH_TEST_FAIL_RANK)")
     if world > 1 or args.force_dist:
-        run_dist(args, world, rank, local_rank)
+        try:
+            run_dist(args, world, rank, local_rank)
+        except Exception as e:  # a failed N > 1 run still leaves one line saying where and why, then fails
+            if rank == 0 and not _LINE_PRINTED:
+                print(json.dumps({"metric": METRIC, "value": None, "unit": "GiB/s", "n_gpus": world,
+                                  "higher_is_better": True, "error": f"{type(e).__name__}: {e}",
+                                  "phase": _WATCH.phase if _WATCH else "start"}), file=json_out(), flush=True)
+            raise
     else:
         run_single(args)
 

@@ -7,6 +7,8 @@ import subprocess
 import sys
 import textwrap
 
+import pytest
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
@@ -231,3 +233,34 @@ def test_c2_self_check_counts_every_launch_and_catches_one_flipped_bit():
     sets[1][0].arr[n // 2 + 7] = np.nextafter(sets[1][0].arr[n // 2 + 7], np.float32(2))
     bad = bench.c2_self_check(sets, offs, win, before, launches)
     assert not bad["ok"] and bad["mismatches"] == 1
+
+
+def test_failed_n_gt_1_run_leaves_one_error_line(monkeypatch, capsys):
+    """A rank-0 failure inside the N > 1 path (here: the communicator bootstrap raising) prints one JSON line
+    naming the error and the phase, then fails; with the line already out, nothing more is printed."""
+    import json
+
+    import bench
+
+    def boom(args, world, rank, local_rank):
+        bench._WATCH = type("W", (), {"phase": "fmi_comm init (communicator id broadcast, RCCL init)"})()
+        raise RuntimeError("ncclCommInitRankConfig: unhandled system error")
+
+    monkeypatch.setattr(bench, "run_dist", boom)
+    monkeypatch.setattr(bench, "_LINE_PRINTED", False)
+    monkeypatch.setattr(bench, "_JSON_OUT", None)
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    monkeypatch.setenv("RANK", "0")
+    monkeypatch.setenv("LOCAL_RANK", "0")
+    monkeypatch.setattr("sys.argv", ["bench.py", "--gpus", "2"])
+    with pytest.raises(RuntimeError):
+        bench.main()
+    out = capsys.readouterr().out.strip().splitlines()
+    assert len(out) == 1
+    line = json.loads(out[0])
+    assert line["value"] is None and line["n_gpus"] == 2 and "unhandled system error" in line["error"]
+    assert line["phase"].startswith("fmi_comm init")
+    monkeypatch.setattr(bench, "_LINE_PRINTED", True)  # the measured line was already printed: no second line
+    with pytest.raises(RuntimeError):
+        bench.main()
+    assert capsys.readouterr().out.strip() == ""
