@@ -658,6 +658,10 @@ def run_dist(args, world, rank, local_rank):
     topo = ar.topology()
     if not topo["ok"]:  # RCCL did not see `world` ranks, or two ranks share a GPU: the line would be wrong
         print("bench: topology check FAILED: " + json.dumps(topo), file=sys.stderr, flush=True)
+        if rank == 0:
+            print(json.dumps({"metric": METRIC, "value": None, "unit": "GiB/s", "n_gpus": world,
+                              "higher_is_better": True, "error": "topology check failed", "phase": "topology check",
+                              "topology": topo}), file=json_out(), flush=True)
         os._exit(1)
     n = args.bucket_mib * MIB // 4
     S = n * 4
