@@ -619,6 +619,10 @@ class _PhaseWatch:
     def _expire(self):
         print(f"bench: rank {self.rank} still in phase '{self.phase}' after {time.time() - self.t0:.0f} s "
               f"(--measure-deadline); exiting", file=sys.stderr, flush=True)
+        if self.rank == 0 and not _LINE_PRINTED:  # the one line says where the run hung
+            print(json.dumps({"metric": METRIC, "value": None, "unit": "GiB/s", "error": "measure deadline reached",
+                              "phase": self.phase, "seconds": round(time.time() - self.t0)}),
+                  file=json_out(), flush=True)
         os._exit(3)
 
     def done(self):

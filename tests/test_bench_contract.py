@@ -117,6 +117,12 @@ def test_measure_deadline_names_the_phase_and_exits_nonzero():
     r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True, timeout=60)
     assert r.returncode == 3
     assert "rank 5 still in phase 'warm-up and timed allreduces'" in r.stderr
+    assert r.stdout.strip() == ""  # only rank 0 prints the line
+    code0 = code.replace("_PhaseWatch(0.2, 5)", "_PhaseWatch(0.2, 0)")
+    r = subprocess.run([sys.executable, "-c", code0], cwd=ROOT, capture_output=True, text=True, timeout=60)
+    assert r.returncode == 3
+    line = json.loads(r.stdout.strip())
+    assert line["value"] is None and line["phase"] == "warm-up and timed allreduces"
 
 
 def test_relay_keeps_one_stdout_line_and_the_exit_status(capsys):
