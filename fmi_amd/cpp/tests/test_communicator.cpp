@@ -7,6 +7,7 @@
 //   test_communicator --proc-channel P           device collectives over the Rccl channel with the PROC
 //        transport, P fork()ed peers on GPU 0, against the same collectives on host buckets
 //   test_communicator --dump KIND P N OUT [--device|--offload]
+//   test_communicator --dump-move bcast|gather|scatter P N ROOT OUT
 //        run KIND (allreduce|reduce|scan|reduce_ltr|allreduce_ltr|scan_ltr) over P peers holding
 //        synthetic f32 buckets of N elements (seed 42, peer p) and write every peer's recvbuf, then every
 //        peer's sendbuf, as raw f32 to OUT — compared against the oracle by the Python wrapper.
@@ -1040,6 +1041,34 @@ static int dump(const std::string& kind, peer_num P, std::size_t n, const std::s
     return g_failures.load() ? 1 : 0;
 }
 
+// --dump-move KIND P N ROOT OUT (KIND = bcast | gather | scatter, host buckets over the Loopback channel): the
+// data-movement collectives, for a check against the reference's own PeerToPeer (tests/test_cpp_communicator.py).
+// Written per peer: bcast the peer's bucket after the call (n); gather the root's P x n receive buffer on the
+// root, zeros elsewhere; scatter the peer's received n-element slice of the root's P x n bucket.
+static int dump_move(const std::string& kind, peer_num P, std::size_t n, peer_num root, const std::string& out) {
+    std::vector<std::vector<float>> got(P);
+    with_peers(P, [&](Communicator& c, peer_num p) {
+        if (kind == "bcast") {
+            Data<std::vector<float>> b(synth_f32(n, 42, p));
+            c.bcast(b, root);
+            got[p] = b.get();
+        } else if (kind == "gather") {
+            Data<std::vector<float>> a(synth_f32(n, 42, p)), r(p == root ? P * n : n);
+            c.gather(a, r, root);
+            got[p] = p == root ? r.get() : std::vector<float>(P * n, 0.0f);
+        } else if (kind == "scatter") {
+            Data<std::vector<float>> a(synth_f32(P * n, 42, p)), r(n);
+            c.scatter(a, r, root);
+            got[p] = r.get();
+        } else {
+            throw std::runtime_error("unknown kind " + kind);
+        }
+    });
+    std::ofstream f(out, std::ios::binary);
+    for (auto& v : got) f.write(reinterpret_cast<const char*>(v.data()), static_cast<std::streamsize>(v.size() * 4));
+    return g_failures.load() ? 1 : 0;
+}
+
 // --proc-channel P: P peers as fork()ed processes (forked before anything touches the GPU), each with a
 // LocalSocket channel and an Rccl channel over the PROC transport (every process on GPU 0). Device-bucket
 // allreduce / scan / reduce / bcast through the Rccl channel must equal, bit for bit, the same collectives
@@ -1106,6 +1135,9 @@ static int proc_channel(peer_num P) {
 int main(int argc, char** argv) {
     std::vector<std::string> args(argv + 1, argv + argc);
     if (args.size() == 2 && args[0] == "--proc-channel") return proc_channel(static_cast<peer_num>(std::stoul(args[1])));
+    if (args.size() == 6 && args[0] == "--dump-move")
+        return dump_move(args[1], static_cast<peer_num>(std::stoul(args[2])), std::stoull(args[3]),
+                         static_cast<peer_num>(std::stoul(args[4])), args[5]);
     if (!args.empty() && args[0] == "--dump") {
         if (args.size() < 5) return 2;
         const std::string mode = args.size() > 5 ? args[5].substr(2) : "host";
