@@ -486,7 +486,22 @@ def c3_single(reps: int = 60) -> dict:
     n64 = 64 * MIB // 8
     pairs = [(Bucket(n64, np.int64).fill_synthetic(42 + s, 0), Bucket(n64, np.int64).fill_synthetic(42 + s, 1))
              for s in range(C3_PAIR_SETS)]
-    ms_max = timed(lambda i: fmi_amd.reduce_pair(Op.MAX, *pairs[i % C3_PAIR_SETS]), reps)
+    win = 4096
+    offs = [0, (n64 // 2) // 64 * 64, n64 - win]
+    before = [[(a.view(o, win).numpy(), b.view(o, win).numpy()) for o in offs] for a, b in pairs]
+    used = [0] * C3_PAIR_SETS
+
+    def launch_max(i):
+        used[i % C3_PAIR_SETS] += 1
+        fmi_amd.reduce_pair(Op.MAX, *pairs[i % C3_PAIR_SETS])
+
+    ms_max = timed(launch_max, reps)
+    # in-run check: max is idempotent, so a pair combined at least once holds max(a0, b0) (std::max on int64)
+    # and one never combined still holds a0 — on the head, middle and tail window of every pair, bit for bit
+    bad = sum(int(np.count_nonzero(a.view(o, win).numpy() != (np.maximum(a0, b0) if k else a0)))
+              for (a, b), wins, k in zip(pairs, before, used) for o, (a0, b0) in zip(offs, wins))
+    max_check = {"ok": bad == 0, "mismatches": bad, "elements_checked": len(pairs) * len(offs) * win,
+                 "against": "numpy maximum of the pair's initial windows (int64, idempotent), bit-exact"}
     for a, b in pairs:
         a.free()
         b.free()
@@ -515,7 +530,7 @@ def c3_single(reps: int = 60) -> dict:
                 "traffic": traffic, "traffic_source": src}
 
     return {"i64_max_pair_64MiB": dict(row(ms_max, 3 * 64 * MIB, "pair_tile<fmi::dev::OpMax, long, 4, 3>"),
-                                       rotating_sets=C3_PAIR_SETS),
+                                       rotating_sets=C3_PAIR_SETS, self_check=max_check),
             "f32_scan_P8_64MiB": dict(row(ms_scan, 2 * P * 64 * MIB, "scan_kernel<fmi::dev::OpSum, float, 3, 8>"),
                                       rotating_sets=C3_SCAN_SETS, per_set_launch_us=per_set_us),
             "timing": "two HIP events around back-to-back launches on the library stream (gaps included)"}
