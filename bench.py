@@ -520,6 +520,7 @@ def c3_single(reps: int = 60) -> dict:
     for a, b in per_set:
         a.destroy()
         b.destroy()
+    scan_check = scan_self_check(ins, outs, n32)
     for b in [x for s in ins + outs for x in s]:
         b.free()
 
@@ -532,8 +533,59 @@ def c3_single(reps: int = 60) -> dict:
     return {"i64_max_pair_64MiB": dict(row(ms_max, 3 * 64 * MIB, "pair_tile<fmi::dev::OpMax, long, 4, 3>"),
                                        rotating_sets=C3_PAIR_SETS, self_check=max_check),
             "f32_scan_P8_64MiB": dict(row(ms_scan, 2 * P * 64 * MIB, "scan_kernel<fmi::dev::OpSum, float, 3, 8>"),
-                                      rotating_sets=C3_SCAN_SETS, per_set_launch_us=per_set_us),
+                                      rotating_sets=C3_SCAN_SETS, per_set_launch_us=per_set_us,
+                                      self_check=scan_check),
             "timing": "two HIP events around back-to-back launches on the library stream (gaps included)"}
+
+
+def eval_bracketing(expr: str, xs):
+    """Evaluates a bracketing such as "((x1+x0)+x2)" on numpy float32 windows: x<p> = xs[p], (a+b) = a + b
+    with a the left operand (IEEE round-to-nearest, the reference's std::plus<float>)."""
+    pos = 0
+
+    def term():
+        nonlocal pos
+        if expr[pos] == "(":
+            pos += 1
+            left = term()
+            assert expr[pos] == "+"
+            pos += 1
+            right = term()
+            assert expr[pos] == ")"
+            pos += 1
+            return left + right
+        end = pos + 1
+        while end < len(expr) and expr[end].isdigit():
+            end += 1
+        peer = int(expr[pos + 1:end])
+        pos = end
+        return xs[peer]
+
+    return term()
+
+
+def scan_self_check(ins, outs, n: int, win: int = 4096) -> dict:
+    """C3's scan checked in the run: on the head, middle and tail window of every set, each peer's output must
+    equal numpy's float32 evaluation of that peer's scan_no_order bracketing (fmi_schedule_expr, the program
+    the kernel runs, pinned to the reference's own bracketing by tests/test_ref_pinning.py), bit for bit."""
+    import numpy as np
+
+    import fmi_amd
+    from fmi_amd import Alg
+
+    P = len(ins[0])
+    exprs = [fmi_amd.schedule_expr(Alg.SCAN, P, r) for r in range(P)]
+    bad = checked = 0
+    for set_in, set_out in zip(ins, outs):
+        for o in (0, (n // 2) // 64 * 64, n - win):
+            xs = [b.view(o, win).numpy() for b in set_in]
+            for r in range(P):
+                want = eval_bracketing(exprs[r], xs)
+                bad += int(np.count_nonzero(set_out[r].view(o, win).numpy().view(np.uint32) != want.view(np.uint32)))
+                checked += win
+    return {"ok": bad == 0, "mismatches": bad, "elements_checked": checked,
+            "against": "numpy float32 evaluation of each peer's scan_no_order bracketing on three windows per set, "
+                       "bit-exact"}
 
 
 QUIET_S = 1.0

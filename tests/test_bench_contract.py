@@ -270,3 +270,21 @@ def test_failed_n_gt_1_run_leaves_one_error_line(monkeypatch, capsys):
     with pytest.raises(RuntimeError):
         bench.main()
     assert capsys.readouterr().out.strip() == ""
+
+
+def test_scan_self_check_bracketing_evaluator_equals_the_oracle():
+    """bench.py's C3 scan self-check evaluates each peer's program bracketing (fmi_schedule_expr) in numpy: for
+    order-sensitive f32 buckets it must give the oracle's scan bit for bit (and a plain left fold must not)."""
+    import numpy as np
+
+    import bench
+    import fmi_amd
+    from oracle import fmi_oracle as orc
+
+    rng = np.random.default_rng(11)
+    for P in (1, 2, 3, 5, 8, 13):
+        xs = [(rng.standard_normal(257) * 2.0 ** (7 * p % 13 - 6)).astype(np.float32) for p in range(P)]
+        want, _ = orc.scan(xs, orc.op_sum)
+        for r in range(P):
+            got = bench.eval_bracketing(fmi_amd.schedule_expr(fmi_amd.Alg.SCAN, P, r), xs)
+            assert np.array_equal(got.view(np.uint32), want[r].view(np.uint32)), (P, r)
