@@ -26,8 +26,9 @@ Also reported (one JSON line on rank 0):
                   xGMI links' peak.
   c4            — (N > 1) config C4 itself: N peers × 1 GiB f32, paths TREE and RCCL, algbw / busbw, each
                   self-checked (TREE bit-exact, RCCL within (N−1)·2^-24·Σ|x|).
-  c5            — config C5: the 1 GiB page-locked host bucket through fmi_comm_allreduce_host (H2D +
-                  allreduce + D2H pipelined), N = 1 one rank, N > 1 every rank.
+  c5            — config C5: N = 1 three self-checked blocks (c5_single: the P = 1 copy, a 1 GiB page-locked
+                  pair through fmi_host_reduce_pair, and the whole 8 x 1 GiB workload as 8 LOCAL ranks on
+                  this GPU); N > 1 every rank's 1 GiB page-locked bucket through fmi_comm_allreduce_host.
   cpu_baseline  — (N = 1) oracle/cpu_baseline (a C++ port of the reference's CPU path) on this host.
   c3            — (N = 1) config C3's kernels: i64 max pair 64 MiB, f32 peer scan 8 x 64 MiB, fraction of peak.
   diagnostics   — (N > 1) the replicated-pair rate (C2 on every GPU, no exchange), the per-phase breakdown
@@ -158,6 +159,7 @@ def cpu_baseline(args):
                              "median_ms": round(omp["median_ms"], 3)},
         "c1": c1_host(),
         "c1_reference": c1_reference(),
+        "c2_reference": c2_reference(args.bucket_mib, adapter["median_ms"]),
     }
 
 
@@ -191,11 +193,55 @@ def c1_reference(reps: int = 41) -> dict:
         bi = fmi_ref.time_allreduce(2, n, reps, adapter=False)
     except Exception as e:  # reported, never required
         return {"error": f"{type(e).__name__}: {e}"}
-    return {"config": "C1", "kind": "reference", "peers": 2, "bucket_mib": 1, "reps": reps,
+    out = {"config": "C1", "kind": "reference", "peers": 2, "bucket_mib": 1, "reps": reps,
+           "code": "reference src/comm/PeerToPeer.cpp (allreduce_no_order), compiled unmodified (oracle/_ref)",
+           "transport": "peer threads, in-memory FIFOs (oracle/ref_harness.cpp)",
+           "adapter_ms": round(ad, 4), "builtin_inplace_ms": round(bi, 4),
+           "adapter_gib_s": round(1 / 1024 / (ad * 1e-3), 4), "builtin_inplace_gib_s": round(1 / 1024 / (bi * 1e-3), 4)}
+    try:  # the same reference allreduce with f.f bound to the product's C-ABI
+        from fmi_amd import _lib
+
+        gpu = fmi_ref.time_allreduce_bound(2, n, reps, fmi_ref.Binding.from_library(_lib.load()))
+        out["gpu_combine_ms"] = round(gpu, 4)
+        out["gpu_combine"] = ("every f.f is fmi_host_reduce_pair from libfmi_dev.so (passed by address; the "
+                              "reference's pageable buckets: staged H2D / kernel / D2H per combine); bit-identity "
+                              "with the CPU combine: tests/test_gpu_ref_binding.py")
+    except Exception as e:  # reported, never required
+        out["gpu_combine_ms"] = None
+        out["gpu_combine_error"] = f"{type(e).__name__}: {e}"
+    return out
+
+
+def c2_reference(bucket_mib: int, port_combine_ms: float, reps: int = 5) -> dict:
+    """The headline size through the REFERENCE's own code: its 2-peer f32 sum-allreduce of `bucket_mib` buckets
+    (src/comm/PeerToPeer.cpp:96-130: per peer one exchange, one combine f.f at :119, the result memcpy at :129),
+    peers as threads over in-memory FIFOs, with the vector adapter and with std::transform in place. A third
+    run with the reference's no-op combine (its barrier's, PeerToPeer.cpp:30) times the transport and copies
+    alone, so allreduce - no-op = the combine inside the reference, set beside the port's adapter combine
+    (`value`): they agree when the ratio is within 1 +- 0.10."""
+    try:
+        from oracle import fmi_ref
+
+        if not fmi_ref.available():
+            return {"error": "oracle/_ref not built"}
+        n = bucket_mib * MIB // 4
+        ad = fmi_ref.time_allreduce(2, n, reps, adapter=True)
+        bi = fmi_ref.time_allreduce(2, n, reps, adapter=False)
+        nop = fmi_ref.time_allreduce(2, n, reps, adapter="nop")
+    except Exception as e:  # reported, never required
+        return {"error": f"{type(e).__name__}: {e}"}
+    combine = ad - nop
+    ratio = combine / port_combine_ms
+    return {"config": "C2 size", "kind": "reference", "peers": 2, "bucket_mib": bucket_mib, "reps": reps,
             "code": "reference src/comm/PeerToPeer.cpp (allreduce_no_order), compiled unmodified (oracle/_ref)",
-            "transport": "peer threads, in-memory FIFOs (oracle/ref_harness.cpp)",
-            "adapter_ms": round(ad, 4), "builtin_inplace_ms": round(bi, 4),
-            "adapter_gib_s": round(1 / 1024 / (ad * 1e-3), 4), "builtin_inplace_gib_s": round(1 / 1024 / (bi * 1e-3), 4)}
+            "adapter_allreduce_ms": round(ad, 2), "builtin_inplace_allreduce_ms": round(bi, 2),
+            "nop_combine_allreduce_ms": round(nop, 2),
+            "adapter_allreduce_gib_s": round(bucket_mib / 1024 / (ad * 1e-3), 4),
+            "combine_in_reference_ms": round(combine, 2), "port_adapter_combine_ms": round(port_combine_ms, 2),
+            "reference_over_port": round(ratio, 3), "agrees_within_10pct": bool(abs(ratio - 1) <= 0.10),
+            "note": "2 peer threads combine concurrently in the reference (one per peer); the port times one "
+                    "combine on one thread: a ratio above 1 is the two concurrent combines sharing the host's "
+                    "memory bandwidth"}
 
 
 _JSON_OUT = None
@@ -254,15 +300,38 @@ class _Emitter:
         os._exit(0)
 
 
-_HEADLINE_KEYS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
-                  "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "xgmi_roofline", "self_check",
-                  "cpu_baseline")
+_HEADLINE_KEYS = ("metric", "value", "unit", "n_gpus", "workload", "steps", "warmup", "ms_per_step",
+                  "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "xgmi_roofline",
+                  "self_check", "cpu_baseline")
+
+# What `value` measures, at top level of every line: the metric's 1/2/4/8-GPU curve spans two workloads. N = 1
+# is the HBM-bound pairwise combine (config C2); N > 1 the xGMI-bound sharded allreduce of one bucket per GPU
+# (config C4's shape at the metric's bucket size). The driver's N-over-1 ratio therefore compares two different
+# workloads; each N > 1 line carries its own one-GPU anchor (`local_equivalent`, `allreduce_1peer` at N = 1).
+WORKLOAD_N1 = "local_combine"
+WORKLOAD_DIST = "sharded_allreduce"
+
+
+def _error_line(world, error, phase, **extra):
+    """The one line of a failed N > 1 run: what failed, where, and the runtime it failed on (librccl version and
+    path, device visibility), so a first 8-GPU failure is diagnosable from the line alone."""
+    try:
+        from fmi_amd.comm import runtime_info
+
+        runtime = runtime_info()
+    except Exception as e:  # the library itself may be what failed
+        runtime = {"error": f"{type(e).__name__}: {e}"}
+    line = {"metric": METRIC, "value": None, "unit": "GiB/s", "n_gpus": world, "workload": WORKLOAD_DIST,
+            "higher_is_better": True, "error": error, "phase": phase, "runtime": runtime}
+    line.update(extra)
+    return line
 
 
 def _headline(args, value, step_ms, workload, parallelism, n, roofline):
     return {
         "metric": METRIC,
         "value": round(value, 2),
+        "workload": WORKLOAD_N1 if args.gpus == 1 and not args.force_dist else WORKLOAD_DIST,
         "unit": "GiB/s",
         "n_gpus": args.gpus,
         "steps": args.steps,
@@ -377,16 +446,30 @@ def run_single(args):
         except Exception as e:  # reported, never fails the measured line
             line["c3"] = f"failed: {type(e).__name__}: {e}"
     if not args.no_c5:
-        try:
-            quiet_device()
-            line["c5"] = c5_single(args.c5_mib)
-            line["c5"]["after_pause_s"] = QUIET_S
-        except Exception as e:  # reported, never fails the measured line
-            line["c5"] = f"failed: {type(e).__name__}: {e}"
+        line["c5"] = c5_single(args.c5_mib)
     print(json.dumps(line), file=json_out(), flush=True)
-    if not check["ok"]:
-        print("bench: C2 self-check FAILED", file=sys.stderr, flush=True)
+    failed = failed_checks(line)
+    if failed:
+        print("bench: self-check FAILED: " + ", ".join(failed), file=sys.stderr, flush=True)
         sys.exit(1)
+
+
+def failed_checks(line) -> list:
+    """Every in-run check of an N = 1 line that ran and did not pass (C2, the P = 1 allreduce, C3's two kernels,
+    C5's three blocks): any of them makes the run exit 1, as the headline's own check does. A block that raised
+    instead of producing a result is reported in the line (its "error"), not counted here."""
+    failed = [] if line["self_check"]["ok"] else ["c2"]
+    if not line.get("allreduce_1peer", {}).get("result_ok", True):
+        failed.append("allreduce_1peer")
+    c3 = line.get("c3")
+    if isinstance(c3, dict):
+        for k in ("i64_max_pair_64MiB", "f32_scan_P8_64MiB"):
+            if not c3[k]["self_check"]["ok"]:
+                failed.append(f"c3 {k}")
+    for k, block in (line.get("c5") or {}).items():
+        if "error" not in block and not block["self_check"]["ok"]:
+            failed.append(f"c5 {k}")
+    return failed
 
 
 def c2_self_check(sets, offs, win, before, launches) -> dict:
@@ -595,7 +678,7 @@ def quiet_device():
     """Let the device go idle before a host-ingress measurement. The driver clears freed VRAM
     asynchronously on the copy engines: right after the C3 / C4 loops free their buckets (GiBs), the H2D
     and D2H copies of C5 share those engines for ~0.3 s and C5 reads 39 ms instead of 23.5 ms
-    (tools/c5_pinned_probe.py: the same buffers, 23.4 ms once 0.3 s have passed). A pause of QUIET_S
+    (profiles/archive/r02_c5_after_free_probe.jsonl: the same buffers, 23.4 ms once 0.3 s have passed). A pause of QUIET_S
     seconds, outside every timed region."""
     import fmi_amd
 
@@ -603,11 +686,30 @@ def quiet_device():
     time.sleep(QUIET_S)
 
 
-def c5_single(mib: int, iters: int = 3) -> dict:
-    """Config C5 at N = 1: a `mib` (1 GiB) f32 bucket in page-locked host memory (a channel recv buffer) through
-    fmi_comm_allreduce_host on a one-rank communicator — H2D, the (one-peer) allreduce and D2H pipelined in
-    64 MiB chunks. Median wall time of `iters` after one warm-up; the result must equal the input bit for
-    bit (a one-peer allreduce is a copy, reference PeerToPeer.cpp:96-130 with P = 1)."""
+def c5_single(mib: int, peers: int = 8) -> dict:
+    """Config C5 at N = 1, three blocks, each self-checked:
+      p1_copy          the `mib` page-locked host bucket through fmi_comm_allreduce_host on a one-rank
+                       communicator: the reference's P = 1 allreduce, a copy (H2D + D2H pipelined).
+      host_pair_reduce the combine at the reference's site on host buckets: a `mib` page-locked pair through
+                       fmi_host_reduce_pair (the zero-copy kernel over PCIe), a += b.
+      local_peers      C5's whole workload on this one GPU: `peers` LOCAL ranks (threads), each with a `mib`
+                       page-locked f32 bucket, fmi_comm_allreduce_host (H2D, sharded allreduce in the reference's
+                       order, D2H pipelined in 64 MiB chunks) — every byte of the 8-GPU config through one PCIe
+                       link and one GPU, sized down only if the host's MemAvailable cannot hold it."""
+    out = {}
+    for name, fn in (("p1_copy", lambda: c5_p1_copy(mib)), ("host_pair_reduce", lambda: c5_host_pair(mib)),
+                     ("local_peers", lambda: c5_local_peers(peers, mib))):
+        try:
+            quiet_device()
+            out[name] = dict(fn(), after_pause_s=QUIET_S)
+        except Exception as e:  # reported, never fails the measured line
+            out[name] = {"error": f"{type(e).__name__}: {e}"}
+    return out
+
+
+def c5_p1_copy(mib: int, iters: int = 3) -> dict:
+    """fmi_comm_allreduce_host of a `mib` page-locked bucket on a one-rank communicator: a copy (reference
+    PeerToPeer.cpp:96-130 with P = 1). Median wall time of `iters` after one warm-up; bit-exact copy check."""
     import statistics
 
     import numpy as np
@@ -633,10 +735,178 @@ def c5_single(mib: int, iters: int = 3) -> dict:
         recv.free()
         comm.destroy()
     ms = statistics.median(times) * 1e3
-    return {"workload": f"C5 at N = 1: {mib} MiB f32 page-locked host bucket, H2D + allreduce + D2H, 64 MiB chunks",
+    return {"workload": f"{mib} MiB f32 page-locked host bucket, one-rank allreduce (P = 1: a copy), H2D + D2H, "
+                        "64 MiB chunks",
             "ms": round(ms, 3), "host_bucket_GiB_s": round(n * 4 / GIB / (ms * 1e-3), 2),
-            "pcie_GB_s_both_directions": round(2 * n * 4 / (ms * 1e-3) / 1e9, 1), "result_bit_exact": ok,
-            "iters": iters}
+            "pcie_GB_s_both_directions": round(2 * n * 4 / (ms * 1e-3) / 1e9, 1), "iters": iters,
+            "self_check": {"ok": ok, "against": "the send bucket, whole, bit-exact"}}
+
+
+def _pinned_synthetic(n: int, seed: int, peers):
+    """Page-locked f32 host buckets filled with the synthetic generator on the device (fast) and copied down."""
+    import numpy as np
+
+    import fmi_amd
+    from fmi_amd import Bucket, PinnedArray, _lib
+
+    scratch = Bucket(n, np.float32)
+    out = []
+    try:
+        for p in peers:
+            h = PinnedArray(n, np.float32)
+            out.append(h)
+            scratch.fill_synthetic(seed, p)
+            _lib.call("fmi_dev_d2h_async", h.ptr, scratch.ptr, n * 4, None)
+            fmi_amd.sync()
+    except BaseException:
+        for h in out:
+            h.free()
+        raise
+    finally:
+        scratch.free()
+    return out
+
+
+def _windows(n: int, win: int = 4096):
+    return [0, (n // 2) // 64 * 64, n - win], win
+
+
+def c5_host_pair(mib: int, iters: int = 3) -> dict:
+    """fmi_host_reduce_pair on a `mib` page-locked f32 pair (a channel recv buffer and the peer's bucket): the
+    reference's f.f(a, b) (PeerToPeer.cpp:119) with both host buckets streamed through the kernel over PCIe
+    (zero-copy: 2 reads + 1 write of the bucket per combine). Median of `iters` after one warm-up; then a must
+    equal numpy's float32 a + b repeated once per call, bit for bit, on three windows."""
+    import statistics
+
+    import numpy as np
+
+    import fmi_amd
+    from fmi_amd import Op
+
+    n = mib * MIB // 4
+    a, b = _pinned_synthetic(n, 61, (0, 1))
+    try:
+        offs, win = _windows(n)
+        before = [(a.array[o:o + win].copy(), b.array[o:o + win].copy()) for o in offs]
+        times = []
+        for k in range(iters + 1):
+            t0 = time.perf_counter()
+            fmi_amd.host_reduce_pair(Op.SUM, a.array, b.array)
+            if k:
+                times.append(time.perf_counter() - t0)
+        bad = 0
+        for o, (a0, b0) in zip(offs, before):
+            want = a0
+            for _ in range(iters + 1):
+                want = want + b0
+            bad += int(np.count_nonzero(a.array[o:o + win].view(np.uint32) != want.view(np.uint32)))
+    finally:
+        a.free()
+        b.free()
+    ms = statistics.median(times) * 1e3
+    S = n * 4
+    return {"workload": f"{mib} MiB f32 page-locked host pair, a += b through fmi_host_reduce_pair (zero-copy "
+                        "kernel over PCIe)",
+            "ms": round(ms, 3), "host_bucket_GiB_s": round(S / GIB / (ms * 1e-3), 2),
+            "pcie_GB_s": round(3 * S / (ms * 1e-3) / 1e9, 1), "pcie_bytes_per_combine": 3 * S, "iters": iters,
+            "self_check": {"ok": bad == 0, "mismatches": bad, "elements_checked": len(offs) * win,
+                           "against": "numpy float32 a + b repeated once per call, three windows, bit-exact"}}
+
+
+def mem_available_bytes():
+    try:
+        for line in open("/proc/meminfo"):
+            if line.startswith("MemAvailable:"):
+                return int(line.split()[1]) * 1024
+    except OSError:
+        pass
+    return None
+
+
+C5_HEADROOM = 16 * GIB  # host memory left free beside C5's page-locked buckets
+
+
+def c5_size_mib(peers: int, mib: int, avail) -> int:
+    """The bucket size C5's local_peers block runs at: `mib`, halved until 2 x peers page-locked buckets plus
+    C5_HEADROOM fit in MemAvailable (unknown MemAvailable: `mib`)."""
+    size = mib
+    while avail is not None and size > 1 and 2 * peers * size * MIB + C5_HEADROOM > avail:
+        size //= 2
+    return size
+
+
+def c5_local_peers(peers: int, mib: int, iters: int = 2) -> dict:
+    """C5's workload on ONE GPU: `peers` LOCAL ranks (threads of this process), each with a page-locked f32
+    bucket of `mib` (1 GiB: 8 GiB in, 8 GiB out over this GPU's one PCIe link), fmi_comm_allreduce_host with
+    64 MiB chunks. Per iteration every rank starts at a barrier; the iteration's time is the slowest rank's;
+    median of `iters` after one warm-up. Self-check: every rank's result on three windows equals numpy's
+    float32 evaluation of that rank's allreduce_no_order bracketing (PeerToPeer.cpp:96-130) over the peers'
+    windows, bit-exact."""
+    import statistics
+    import threading
+
+    import numpy as np
+
+    import fmi_amd
+    from fmi_amd import Alg, Op, PinnedArray
+    from fmi_amd.comm import Comm, Transport, unique_id
+
+    avail = mem_available_bytes()
+    size = c5_size_mib(peers, mib, avail)
+    n = size * MIB // 4
+    send = _pinned_synthetic(n, 91, range(peers))
+    recv = []
+    try:
+        recv = [PinnedArray(n, np.float32) for _ in range(peers)]
+        uid = unique_id(Transport.LOCAL)
+        bar = threading.Barrier(peers)
+        times = [[0.0] * (iters + 1) for _ in range(peers)]
+        errors = []
+
+        def rank(r):
+            try:
+                c = Comm(uid, peers, r, timeout_s=120)
+                try:
+                    for k in range(iters + 1):
+                        bar.wait(timeout=300)
+                        t0 = time.perf_counter()
+                        c.allreduce_host(Op.SUM, send[r].array, recv[r].array, chunk=64 * MIB // 4)
+                        times[r][k] = time.perf_counter() - t0
+                finally:
+                    c.destroy()
+            except BaseException as e:  # noqa: BLE001 - reported below
+                bar.abort()
+                errors.append(f"rank {r}: {type(e).__name__}: {e}")
+
+        threads = [threading.Thread(target=rank, args=(r,)) for r in range(peers)]
+        for t in threads:
+            t.start()
+        for t in threads:
+            t.join(timeout=600)
+        if errors:
+            raise RuntimeError(errors[0])
+        per_iter = [max(times[r][k] for r in range(peers)) for k in range(1, iters + 1)]
+        offs, win = _windows(n)
+        bad = 0
+        for o in offs:
+            xs = [s.array[o:o + win] for s in send]
+            for r in range(peers):
+                want = eval_bracketing(fmi_amd.schedule_expr(Alg.ALLREDUCE, peers, r), xs)
+                bad += int(np.count_nonzero(recv[r].array[o:o + win].view(np.uint32) != want.view(np.uint32)))
+    finally:
+        for h in send + recv:
+            h.free()
+    ms = statistics.median(per_iter) * 1e3
+    S = n * 4
+    return {"workload": f"C5 on one GPU: {peers} LOCAL ranks x {size} MiB f32 page-locked host buckets, "
+                        "fmi_comm_allreduce_host (H2D + sharded allreduce + D2H pipelined, 64 MiB chunks)",
+            "peers": peers, "bucket_mib": size, "requested_bucket_mib": mib,
+            "mem_available_gib": round(avail / GIB, 1) if avail else None,
+            "ms": round(ms, 2), "host_buckets_GiB_s": round(peers * S / GIB / (ms * 1e-3), 2),
+            "pcie_GB_s_both_directions": round(2 * peers * S / (ms * 1e-3) / 1e9, 1), "iters": iters,
+            "self_check": {"ok": bad == 0, "mismatches": bad, "elements_checked": len(offs) * win * peers,
+                           "against": "numpy float32 evaluation of each rank's allreduce_no_order bracketing "
+                                      "(fmi_schedule_expr) over the peers' windows, three windows, bit-exact"}}
 
 
 # ------------------------------------------------------------------------------------------------------
@@ -687,9 +957,9 @@ class _PhaseWatch:
         print(f"bench: rank {self.rank} still in phase '{self.phase}' after {time.time() - self.t0:.0f} s "
               f"(--measure-deadline); exiting", file=sys.stderr, flush=True)
         if self.rank == 0 and not _LINE_PRINTED:  # the one line says where the run hung
-            print(json.dumps({"metric": METRIC, "value": None, "unit": "GiB/s", "error": "measure deadline reached",
-                              "phase": self.phase, "seconds": round(time.time() - self.t0)}),
-                  file=json_out(), flush=True)
+            world = int(os.environ.get("WORLD_SIZE", "1"))
+            print(json.dumps(_error_line(world, "measure deadline reached", self.phase,
+                                         seconds=round(time.time() - self.t0))), file=json_out(), flush=True)
         os._exit(3)
 
     def done(self):
@@ -730,9 +1000,8 @@ def run_dist(args, world, rank, local_rank):
     if not topo["ok"]:  # RCCL did not see `world` ranks, or two ranks share a GPU: the line would be wrong
         print("bench: topology check FAILED: " + json.dumps(topo), file=sys.stderr, flush=True)
         if rank == 0:
-            print(json.dumps({"metric": METRIC, "value": None, "unit": "GiB/s", "n_gpus": world,
-                              "higher_is_better": True, "error": "topology check failed", "phase": "topology check",
-                              "topology": topo}), file=json_out(), flush=True)
+            print(json.dumps(_error_line(world, "topology check failed", "topology check", topology=topo)),
+                  file=json_out(), flush=True)
         os._exit(1)
     n = args.bucket_mib * MIB // 4
     S = n * 4
@@ -806,9 +1075,12 @@ def after_value(args, ar, world, dist, line, proc):
     """The single-GPU anchor, config C4 at its own size, config C5, then the diagnostics — each max over
     ranks, recorded into `line` as it completes (a deadline prints whatever is there)."""
     if ar.rank == 0:  # the same N x S allreduce on ONE GPU (no exchange): separates xGMI cost from HBM cost
-        line["local_equivalent"] = ar.local_equivalent(args.bucket_mib * MIB // 4)
-        line["local_equivalent"]["value_over_local"] = round(line["value"] / line["local_equivalent"][
-            "GiB_s_reduced_buckets"], 4)
+        try:  # rank 0 alone: a failure here must not skip the barrier the other ranks wait in
+            le = ar.local_equivalent(args.bucket_mib * MIB // 4)
+            le["value_over_local"] = round(line["value"] / le["GiB_s_reduced_buckets"], 4)
+            line["local_equivalent"] = le
+        except Exception as e:  # reported; every rank still runs the same sequence of collectives
+            line["local_equivalent"] = {"error": f"{type(e).__name__}: {e}"}
     dist.barrier()
     n4 = args.c4_mib * MIB // 4
     steps4, warm4 = max(5, args.steps // 10), 2
@@ -974,9 +1246,8 @@ def main():
             run_dist(args, world, rank, local_rank)
         except Exception as e:  # a failed N > 1 run still leaves one line saying where and why, then fails
             if rank == 0 and not _LINE_PRINTED:
-                print(json.dumps({"metric": METRIC, "value": None, "unit": "GiB/s", "n_gpus": world,
-                                  "higher_is_better": True, "error": f"{type(e).__name__}: {e}",
-                                  "phase": _WATCH.phase if _WATCH else "start"}), file=json_out(), flush=True)
+                print(json.dumps(_error_line(world, f"{type(e).__name__}: {e}", _WATCH.phase if _WATCH else "start")),
+                      file=json_out(), flush=True)
             raise
     else:
         run_single(args)

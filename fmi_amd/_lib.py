@@ -102,6 +102,7 @@ SIGNATURES = {
     "fmi_comm_size": (_i, [_vp, _c.POINTER(_i), _c.POINTER(_i)]),
     "fmi_comm_sync": (_i, [_vp, _vp]),
     "fmi_comm_query": (_i, [_vp, _c.POINTER(_i), _c.POINTER(_i), _c.POINTER(_i)]),
+    "fmi_comm_rccl_info": (_i, [_c.POINTER(_i), _c.c_char_p, _sz]),
     "fmi_comm_window_alloc": (_i, [_vp, _sz, _c.POINTER(_vp)]),
     "fmi_comm_window_free": (_i, [_vp, _vp]),
     "fmi_comm_timing": (_i, [_vp, _i]),

@@ -267,11 +267,13 @@ class CommAllreduce:
         and the GPU's PCI bus id. ok: the transport saw exactly `world` ranks, each rank at its own index,
         and (RCCL) no two ranks share a GPU. PROC ranks may share one GPU by design: labelled, not an error."""
         from . import device as fdev
+        from .comm import runtime_info
 
         q = self.comm.query()
         dev = torch.cuda.current_device()
         mine = {"rank": self.rank, "transport_count": q["count"], "transport_rank": q["rank"],
-                "transport_device": q["device"], "torch_device": dev, "pci_bus_id": fdev.pci_bus_id(dev)}
+                "transport_device": q["device"], "torch_device": dev, "pci_bus_id": fdev.pci_bus_id(dev),
+                "runtime": runtime_info()}
         every = [None] * self.world
         dist.all_gather_object(every, mine, group=self.group)
         return judge_topology(every, self.world, self.transport)
@@ -587,6 +589,12 @@ def judge_topology(every: List[dict], world: int, transport: str) -> dict:
            "ranks": [{k: e[k] for k in ("transport_rank", "transport_device", "torch_device", "pci_bus_id")}
                      for e in every],
            "distinct_gpus": distinct, "ok": bool(ranks_ok and (distinct or shared_ok))}
+    # the librccl and visibility environment: rank 0's, plus every rank that differs from it
+    rt = [e.get("runtime") or {} for e in every]
+    res["runtime"] = rt[0]
+    differ = {e["rank"]: r for e, r in zip(every, rt) if r != rt[0]}
+    if differ:
+        res["runtime_differs"] = differ
     if transport != "rccl":
         res["rccl_ranks"] = None
         res["transport_ranks"] = counts[0] if len(counts) == 1 else counts

@@ -10,6 +10,7 @@ from __future__ import annotations
 
 import ctypes
 import enum
+import os
 from typing import Optional
 
 from . import _lib
@@ -38,6 +39,25 @@ def unique_id(transport: Transport = Transport.RCCL) -> bytes:
     buf = ctypes.create_string_buffer(ID_BYTES)
     _lib.call("fmi_comm_unique_id", int(transport), buf, ID_BYTES)
     return buf.raw
+
+
+VISIBILITY_ENV = ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "GPU_MAX_HW_QUEUES")
+
+
+def runtime_info() -> dict:
+    """What a multi-GPU run needs to be diagnosable from one line: the librccl the RCCL transport runs on
+    (fmi_comm_rccl_info: ncclGetVersion and the real path of the mapped object) and the device-visibility /
+    hardware-queue environment of this process. Never raises: a failure is reported in the dict."""
+    info = {k: os.environ.get(k) for k in VISIBILITY_ENV}
+    try:
+        v = ctypes.c_int(0)
+        path = ctypes.create_string_buffer(4096)
+        _lib.call("fmi_comm_rccl_info", ctypes.byref(v), path, len(path))
+        info["rccl_version"] = v.value
+        info["rccl_path"] = path.value.decode(errors="replace")
+    except Exception as e:  # reported, never raised: this runs on error paths
+        info["rccl_error"] = f"{type(e).__name__}: {e}"
+    return info
 
 
 def _p(x) -> Optional[int]:

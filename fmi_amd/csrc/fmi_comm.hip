@@ -88,6 +88,7 @@ struct RcclApi {
     ncclResult_t (*CommAbort)(ncclComm_t);
     ncclResult_t (*CommFinalize)(ncclComm_t);
     ncclResult_t (*CommCount)(const ncclComm_t, int*);
+    ncclResult_t (*GetVersion)(int*);
     ncclResult_t (*CommUserRank)(const ncclComm_t, int*);
     ncclResult_t (*CommCuDevice)(const ncclComm_t, int*);
     bool bounded() const { return CommInitRankConfig && CommGetAsyncError && CommAbort; }
@@ -133,6 +134,7 @@ const RcclApi* rccl_api() {
         FMI_RCCL_OPT(CommCount)
         FMI_RCCL_OPT(CommUserRank)
         FMI_RCCL_OPT(CommCuDevice)
+        FMI_RCCL_OPT(GetVersion)
 #undef FMI_RCCL_OPT
         ok = true;
     });
@@ -193,14 +195,24 @@ public:
     // Abort and report a timeout.
     int timed_out(const std::string& what) {
         abort();
-        return fail(FMI_ERR_TIMEOUT, "Timeout was reached: " + what + " (no peer progress within " +
+        return fail(FMI_ERR_TIMEOUT, "Timeout was reached: " + what + " (not complete within " +
                                          std::to_string(timeout_s_) + " s; communicator aborted)");
     }
-    // Wait for the work on s within the timeout, watching for transport errors.
+    // Wait for the work on s within the timeout, watching for transport errors. The limit covers everything
+    // queued on s when the wait starts: callers that queue long pipelines wait per stage (wait_event), so the
+    // limit bounds one stage's progress, not the whole call.
     int wait_stream(hipStream_t s, const char* what) {
+        return wait_until_done([s] { return hipStreamQuery(s); }, s, what);
+    }
+    // Wait for `ev`'s last record within the timeout (a fresh deadline per call), watching for transport errors.
+    int wait_event(hipEvent_t ev, hipStream_t s, const char* what) {
+        return wait_until_done([ev] { return hipEventQuery(ev); }, s, what);
+    }
+    template <class Query>
+    int wait_until_done(Query&& query, hipStream_t s, const char* what) {
         const auto t0 = Clock::now();
         for (int k = 0;; ++k) {
-            const hipError_t e = hipStreamQuery(s);
+            const hipError_t e = query();
             if (e == hipSuccess) return FMI_OK;
             if (e != hipErrorNotReady) return fail(FMI_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
             if (int rc = poll()) {
@@ -217,9 +229,16 @@ public:
     }
     // Bounded wait for s (after an abort: never block forever). True if it drained.
     static bool drain(hipStream_t s, double seconds) {
+        return drain_query([s] { return hipStreamQuery(s); }, seconds);
+    }
+    static bool drain_event(hipEvent_t ev, double seconds) {
+        return drain_query([ev] { return hipEventQuery(ev); }, seconds);
+    }
+    template <class Query>
+    static bool drain_query(Query&& query, double seconds) {
         const auto t0 = Clock::now();
         for (int k = 0;; ++k) {
-            const hipError_t e = hipStreamQuery(s);
+            const hipError_t e = query();
             if (e != hipErrorNotReady) return e == hipSuccess;
             if (std::chrono::duration<double>(Clock::now() - t0).count() > seconds) return false;
             backoff(k);
@@ -586,10 +605,15 @@ struct Hub {
         bool done;
     };
     std::map<std::pair<int, int>, std::deque<Msg*>> box;
+    // Set when any rank's wait on the hub times out. A timed-out rank has left its barrier (its arrival
+    // withdrawn) and may free the buffer it published: no later barrier, exchange or mailbox wait of this hub
+    // may complete and read it, so every one of them fails as a timeout instead (the communicator is aborted).
+    bool poisoned = false;
 
-    // false: not every rank arrived before the deadline
+    // false: not every rank arrived before the deadline, or the hub is poisoned
     bool barrier(Clock::time_point deadline) {
         std::unique_lock<std::mutex> lk(mu);
+        if (poisoned) return false;
         const uint64_t g = generation;
         if (++arrived == n) {
             arrived = 0;
@@ -597,7 +621,14 @@ struct Hub {
             cv.notify_all();
             return true;
         }
-        return cv.wait_until(lk, deadline, [&] { return generation != g; });
+        if (cv.wait_until(lk, deadline, [&] { return generation != g || poisoned; }) && generation != g) return true;
+        if (generation == g) --arrived;  // withdraw: this rank no longer waits in this barrier
+        poison_locked();
+        return false;
+    }
+    void poison_locked() {
+        poisoned = true;
+        cv.notify_all();
     }
 };
 
@@ -652,13 +683,14 @@ public:
         q.push_back(&msg);
         hub_->cv.notify_all();
         // rendezvous: the receiver has copied it
-        if (!hub_->cv.wait_until(lk, deadline(), [&] { return msg.done; })) {
+        if (!hub_->cv.wait_until(lk, deadline(), [&] { return msg.done || hub_->poisoned; }) || !msg.done) {
             const auto it = std::find(q.begin(), q.end(), &msg);
             if (it == q.end()) {  // the receiver took it and is copying: it is alive, let it finish
                 hub_->cv.wait(lk, [&] { return msg.done; });
                 return FMI_OK;
             }
             q.erase(it);  // never leave a pointer to this frame behind
+            hub_->poison_locked();
             lk.unlock();
             return timed_out("local transport send to rank " + std::to_string(peer));
         }
@@ -669,7 +701,8 @@ public:
         {
             std::unique_lock<std::mutex> lk(hub_->mu);
             auto& q = hub_->box[{peer, rank_}];
-            if (!hub_->cv.wait_until(lk, deadline(), [&] { return !q.empty(); })) {
+            if (!hub_->cv.wait_until(lk, deadline(), [&] { return !q.empty() || hub_->poisoned; }) || q.empty()) {
+                hub_->poison_locked();
                 lk.unlock();
                 return timed_out("local transport recv from rank " + std::to_string(peer));
             }
@@ -1182,6 +1215,19 @@ struct Comm {
     HostPipe pipe;
     ChunkPipe chunks;
     std::map<char*, Window> windows;  // keyed by this rank's base
+    // The end of the last collective queued on each caller stream (not the library's): an aborted communicator
+    // must not free scratch that work on those streams may still read (events outlive the caller's streams).
+    std::map<hipStream_t, hipEvent_t> user_tail;
+
+    void note_user_stream(hipStream_t s) {
+        if (!s || s == library_stream()) return;
+        hipEvent_t& ev = user_tail[s];
+        if (!ev && hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+            user_tail.erase(s);
+            return;
+        }
+        (void)hipEventRecord(ev, s);
+    }
 
     ~Comm() {
         if (t && t->aborted()) {
@@ -1191,6 +1237,7 @@ struct Comm {
             bool drained = Transport::drain(library_stream(), 10.0);
             for (hipStream_t st : {pipe.cs, pipe.h2d, pipe.d2h, chunks.gs})
                 if (st) drained = Transport::drain(st, 10.0) && drained;
+            for (auto& [st, ev] : user_tail) drained = Transport::drain_event(ev, 10.0) && drained;
             if (!drained) {
                 pipe.cs = pipe.h2d = pipe.d2h = chunks.gs = nullptr;
                 for (void*& b : buf) b = nullptr;
@@ -1208,6 +1255,10 @@ struct Comm {
         }
         if (pipe.cs) (void)hipStreamSynchronize(pipe.cs);
         if (chunks.gs) (void)hipStreamSynchronize(chunks.gs);
+        for (auto& [st, ev] : user_tail) {
+            (void)hipEventSynchronize(ev);
+            (void)hipEventDestroy(ev);
+        }
         // Windows are read by the peers: wait until every rank is done with them (communicators are torn
         // down collectively, as the reference's Communicator destructor finalizes every channel). A path
         // DIRECT collective may have run on any stream of this process and still be reading a peer's window
@@ -1801,7 +1852,13 @@ static int comm_allreduce_host_impl(fmi_comm_t comm, int op, int dtype, int alg,
         if (k + 1 < nchunks) FMI_COMM_RC(load(k + 1));
         const int j = static_cast<int>(k & 1);
         FMI_COMM_HIP(hipStreamWaitEvent(p.cs, p.loaded[j], 0));
-        if (k >= 2) FMI_COMM_HIP(hipStreamWaitEvent(p.cs, p.drained[j], 0));
+        if (k >= 2) {
+            // Host-side too: chunk k - 2 has drained before chunk k is queued. The device would wait for it anyway
+            // (the stream wait above); waiting here as well gives the communicator's timeout a fresh deadline per
+            // chunk, so it bounds the progress of one chunk, never the whole bucket's transfer time.
+            FMI_COMM_HIP(hipStreamWaitEvent(p.cs, p.drained[j], 0));
+            FMI_COMM_RC(c->t->wait_event(p.drained[j], p.d2h, "fmi_comm_allreduce_host (a chunk's exchange)"));
+        }
         FMI_COMM_RC(allreduce_device(c, op, dtype, alg, path, in[j], out[j], span(k), p.cs));
         FMI_COMM_HIP(hipEventRecord(p.reduced[j], p.cs));
         FMI_COMM_HIP(hipStreamWaitEvent(p.d2h, p.reduced[j], 0));
@@ -2006,7 +2063,23 @@ static int comm_barrier_impl(fmi_comm_t comm, fmi_stream_t stream) {
 }
 
 
+}  // extern "C"
+
 // ---- entry points: no C++ exception crosses the C-ABI (guarded) ----
+// A collective on a caller stream: afterwards (whatever its status — a failure may follow enqueued work) the
+// stream's tail is noted, so destroying an aborted communicator waits for it before freeing scratch.
+template <class F>
+int on_stream(const char* name, fmi_comm_t comm, fmi_stream_t stream, F&& f) {
+    const int rc = guarded(name, f);
+    if (comm && stream) {
+        Comm* c = static_cast<Comm*>(comm);
+        std::lock_guard<std::mutex> lk(c->mu);
+        c->note_user_stream(static_cast<hipStream_t>(stream));
+    }
+    return rc;
+}
+
+extern "C" {
 int fmi_comm_window_alloc(fmi_comm_t comm, size_t bytes, void** ptr) {
     return guarded("fmi_comm_window_alloc", [&] { return comm_window_alloc_impl(comm, bytes, ptr); });
 }
@@ -2017,7 +2090,7 @@ int fmi_comm_window_free(fmi_comm_t comm, void* ptr) {
 
 int fmi_comm_allreduce(fmi_comm_t comm, int op, int dtype, int alg, int path, const void* send, void* recv, size_t n,
                        fmi_stream_t stream) {
-    return guarded("fmi_comm_allreduce", [&] { return comm_allreduce_impl(comm, op, dtype, alg, path, send, recv, n, stream); });
+    return on_stream("fmi_comm_allreduce", comm, stream, [&] { return comm_allreduce_impl(comm, op, dtype, alg, path, send, recv, n, stream); });
 }
 
 int fmi_comm_allreduce_host(fmi_comm_t comm, int op, int dtype, int alg, int path, const void* send, void* recv,
@@ -2027,41 +2100,41 @@ int fmi_comm_allreduce_host(fmi_comm_t comm, int op, int dtype, int alg, int pat
 
 int fmi_comm_reduce(fmi_comm_t comm, int op, int dtype, int alg, const void* send, void* recv, size_t n, int root,
                     fmi_stream_t stream) {
-    return guarded("fmi_comm_reduce", [&] { return comm_reduce_impl(comm, op, dtype, alg, send, recv, n, root, stream); });
+    return on_stream("fmi_comm_reduce", comm, stream, [&] { return comm_reduce_impl(comm, op, dtype, alg, send, recv, n, root, stream); });
 }
 
 int fmi_comm_reduce_sendbuf(fmi_comm_t comm, int op, int dtype, int alg, void* send, void* recv, size_t n, int root,
                             fmi_stream_t stream) {
-    return guarded("fmi_comm_reduce_sendbuf", [&] { return comm_reduce_sendbuf_impl(comm, op, dtype, alg, send, recv, n, root, stream); });
+    return on_stream("fmi_comm_reduce_sendbuf", comm, stream, [&] { return comm_reduce_sendbuf_impl(comm, op, dtype, alg, send, recv, n, root, stream); });
 }
 
 int fmi_comm_scan(fmi_comm_t comm, int op, int dtype, int alg, const void* send, void* recv, size_t n,
                   fmi_stream_t stream) {
-    return guarded("fmi_comm_scan", [&] { return comm_scan_impl(comm, op, dtype, alg, send, recv, n, stream); });
+    return on_stream("fmi_comm_scan", comm, stream, [&] { return comm_scan_impl(comm, op, dtype, alg, send, recv, n, stream); });
 }
 
 int fmi_comm_bcast(fmi_comm_t comm, void* buf, size_t bytes, int root, fmi_stream_t stream) {
-    return guarded("fmi_comm_bcast", [&] { return comm_bcast_impl(comm, buf, bytes, root, stream); });
+    return on_stream("fmi_comm_bcast", comm, stream, [&] { return comm_bcast_impl(comm, buf, bytes, root, stream); });
 }
 
 int fmi_comm_gather(fmi_comm_t comm, const void* send, void* recv, size_t bytes, int root, fmi_stream_t stream) {
-    return guarded("fmi_comm_gather", [&] { return comm_gather_impl(comm, send, recv, bytes, root, stream); });
+    return on_stream("fmi_comm_gather", comm, stream, [&] { return comm_gather_impl(comm, send, recv, bytes, root, stream); });
 }
 
 int fmi_comm_scatter(fmi_comm_t comm, const void* send, void* recv, size_t bytes, int root, fmi_stream_t stream) {
-    return guarded("fmi_comm_scatter", [&] { return comm_scatter_impl(comm, send, recv, bytes, root, stream); });
+    return on_stream("fmi_comm_scatter", comm, stream, [&] { return comm_scatter_impl(comm, send, recv, bytes, root, stream); });
 }
 
 int fmi_comm_send(fmi_comm_t comm, const void* buf, size_t bytes, int peer, fmi_stream_t stream) {
-    return guarded("fmi_comm_send", [&] { return comm_send_impl(comm, buf, bytes, peer, stream); });
+    return on_stream("fmi_comm_send", comm, stream, [&] { return comm_send_impl(comm, buf, bytes, peer, stream); });
 }
 
 int fmi_comm_recv(fmi_comm_t comm, void* buf, size_t bytes, int peer, fmi_stream_t stream) {
-    return guarded("fmi_comm_recv", [&] { return comm_recv_impl(comm, buf, bytes, peer, stream); });
+    return on_stream("fmi_comm_recv", comm, stream, [&] { return comm_recv_impl(comm, buf, bytes, peer, stream); });
 }
 
 int fmi_comm_barrier(fmi_comm_t comm, fmi_stream_t stream) {
-    return guarded("fmi_comm_barrier", [&] { return comm_barrier_impl(comm, stream); });
+    return on_stream("fmi_comm_barrier", comm, stream, [&] { return comm_barrier_impl(comm, stream); });
 }
 
 int fmi_comm_unique_id(int transport, void* id, size_t len) {
@@ -2086,6 +2159,26 @@ int fmi_comm_query(fmi_comm_t comm, int* count, int* rank, int* device) {
         std::lock_guard<std::mutex> lk(c->mu);
         if (c->t->aborted()) return aborted_error();
         return c->t->query(count, rank, device);
+    });
+}
+
+int fmi_comm_rccl_info(int* version, char* path, size_t len) {
+    return guarded("fmi_comm_rccl_info", [&]() -> int {
+        const RcclApi* api = rccl_api();
+        if (!api) return FMI_ERR_COMM;  // rccl_api() set the message (librccl missing or incomplete)
+        int v = 0;
+        if (api->GetVersion && api->GetVersion(&v) != ncclSuccess) v = 0;
+        if (version) *version = v;
+        if (path && len) {
+            path[0] = '\0';
+            Dl_info info{};
+            if (dladdr(reinterpret_cast<void*>(api->GetUniqueId), &info) && info.dli_fname) {
+                char real[4096];
+                const char* name = realpath(info.dli_fname, real) ? real : info.dli_fname;
+                std::snprintf(path, len, "%s", name);
+            }
+        }
+        return FMI_OK;
     });
 }
 

@@ -450,9 +450,9 @@ int reduce_superblocks(int op, int dtype, void* out, const void* const* ins, int
     return rc;
 }
 
-// allreduce_no_order over P = 2^k >= 128 peers as superblocks of 64 peers (tools/ab_allreduce_super.py, 1 GiB of
+// allreduce_no_order over P = 2^k >= 128 peers as superblocks of 64 peers (profiles/archive/r02_ab_allreduce_superblocks64.jsonl, 1 GiB of
 // input: P = 256 / 512 / 1024 19 / 24 / 4 % faster than the 16-peer block launches; P = 128 28-31 % faster
-// than its one-pass 128-peer kernel, tools/ab_allreduce128.py; superblocks of 128 were slower than the
+// than its one-pass 128-peer kernel, profiles/archive/r02_ab_allreduce128.jsonl; superblocks of 128 were slower than the
 // launches, above): recursive-doubling rounds 0..5 stay inside each superblock — its
 // one-pass 64-peer allreduce for rank r % 64, the same for every superblock — and rounds 6+ are the
 // allreduce over the P / 64 superblock values for rank r / 64 (fused up to 16 values, one pass beyond).

@@ -217,7 +217,7 @@ __device__ __forceinline__ void store_tile(void* bucket, size_t tile_byte, unsig
 // communicator): the pair tile's shape with one stream in and one out — U 16-B vectors per thread, one tile
 // per workgroup. Whole tiles load nontemporal and store with sc1 through a buffer descriptor (the tree kernel's
 // policy, above): 4.6 % faster than global nontemporal stores at 256 MiB, 3 % at 64 MiB, with no set
-// re-read from the MALL (tools/microbench_copypol.hip, profiles/r03_copypol.jsonl). The partial last tile
+// re-read from the MALL (profiles/archive/r03_copypol.jsonl). The partial last tile
 // goes through bounds-checked global accesses; workgroup 0 copies the sub-16-B tail. Algorithmic HBM bytes:
 // 2 x bytes. Both pointers 16-B aligned.
 template <int U>

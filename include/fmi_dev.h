@@ -262,6 +262,10 @@ int fmi_comm_sync(fmi_comm_t comm, fmi_stream_t stream);
  * RCCL bound this rank to); LOCAL / PROC the communicator's size, rank and the calling thread's device.
  * Lets a caller prove the topology it runs on (bench.py: RCCL saw N ranks on N distinct GPUs). */
 int fmi_comm_query(fmi_comm_t comm, int* count, int* rank, int* device);
+/* The librccl the RCCL transport uses (loaded on first use: with torch imported first, torch's copy): its
+ * ncclGetVersion (0 if it lacks the symbol) and the real path of the mapped object, NUL-terminated into
+ * path. FMI_ERR_COMM if librccl cannot be loaded. Lets a failed multi-GPU run name the RCCL it ran on. */
+int fmi_comm_rccl_info(int* version, char* path, size_t len);
 /* Symmetric window for FMI_PATH_DIRECT (collective: every rank calls it with the same `bytes`). Returns a
  * device bucket of `bytes` that every peer of the communicator can read directly (RCCL transport: HIP IPC
  * handles exchanged by all-gather, mapped with peer access over xGMI). All-or-nothing: if any rank cannot

@@ -28,7 +28,10 @@
 //   fmi_ref_run   numeric collective over P peers' buckets: every peer's recvbuf and sendbuf after the call.
 //   fmi_ref_expr  symbolic run: each element is a handle to an expression; f.f(a, b) makes "(a+b)" (left operand
 //                 = arg 0 of f.f), so the result is the exact bracketing the reference evaluates.
-//   fmi_ref_time_allreduce  CPU time of the reference's allreduce (bench.py's C1 row of the CPU baseline).
+//   fmi_ref_time_allreduce  CPU time of the reference's allreduce (bench.py's C1 / C2 rows of the CPU baseline).
+//   fmi_ref_run_bound / fmi_ref_time_allreduce_bound  the same reference collectives with f.f bound to a
+//                 bucket-reduction C-ABI whose entry points the caller passes by address (INTEGRATION.md §B.2;
+//                 tests/test_gpu_ref_binding.py binds libfmi_dev.so). Nothing of that library is linked here.
 #include "comm/PeerToPeer.h"
 
 #include <algorithm>
@@ -301,6 +304,106 @@ FMI_REF_API long fmi_ref_expr(int coll, int ordered, int P, int rank, int root, 
     return static_cast<long>(s.size());
 }
 
+// ---- The reference's combine site bound to a bucket-reduction C-ABI --------------------
+// The entry points of such a library, passed in BY ADDRESS by the caller (tests/test_gpu_ref_binding.py takes
+// them from libfmi_dev.so with ctypes): this file links nothing of the product and names none of its symbols.
+// The signatures are those of include/fmi_dev.h; op ids (0 sum, 1 prod, 2 max, 3 min) and dtype ids (0 f32,
+// 1 f64, 2 i32, 3 i64, 4 u32, 5 u64) coincide with this harness's own.
+struct RefBinding {
+    int (*host_pair)(int op, int dtype, void* inout, const void* in, size_t n);             // fmi_host_reduce_pair
+    int (*dev_pair)(int op, int dtype, void* inout, const void* in, size_t n, void* stream); // fmi_dev_reduce_pair
+    int (*stream_sync)(void* stream);                                                        // fmi_stream_sync
+    const char* (*last_error)(void);                                                         // fmi_last_error
+};
+
+namespace {
+
+// The raw_func §B.2 builds for a tagged Function: f.f(a, b) = "a = op(a, b)" through the library.
+//   host entry point (dev_pair null): fmi_host_reduce_pair on whatever host memory the reference hands the
+//     combine — the caller's buckets and the reference's own `new char[]` temporaries (PeerToPeer.cpp:47,63).
+//   device entry point: fmi_dev_reduce_pair on the library stream + fmi_stream_sync, for buckets the GPU
+//     addresses directly (page-locked, mapped). Operands outside [lo[k], lo[k] + len) of the `mapped` ranges
+//     (the reference's pageable temporaries) are refused with an exception, never handed to a kernel.
+raw_func bound_combine(const RefBinding& b, int op, int dtype, size_t n, std::vector<std::pair<const char*, size_t>> mapped) {
+    const size_t bytes = n * dtype_size(dtype);
+    return [b, op, dtype, n, bytes, mapped](char* x, char* y) {
+        int rc;
+        if (b.dev_pair) {
+            for (const char* p : {static_cast<const char*>(x), static_cast<const char*>(y)}) {
+                bool inside = false;
+                for (const auto& r : mapped) inside = inside || (p >= r.first && p + bytes <= r.first + r.second);
+                if (!inside) throw std::runtime_error("device binding: a combine operand is not a device-mapped bucket "
+                                                      "(the reference's pageable temporary); use the host entry point");
+            }
+            rc = b.dev_pair(op, dtype, x, y, n, nullptr);
+            if (rc == 0) rc = b.stream_sync(nullptr);
+        } else {
+            rc = b.host_pair(op, dtype, x, y, n);
+        }
+        if (rc != 0)
+            throw std::runtime_error(std::string("bound combine failed (") + std::to_string(rc) + "): " +
+                                     (b.last_error ? b.last_error() : ""));
+    };
+}
+
+}  // namespace
+
+// fmi_ref_run with the reference's combine bound to a C-ABI (struct RefBinding above) instead of the harness's
+// std functors: the same PeerToPeer code, the same transport, only f.f differs. bufs: null (every peer's
+// sendbuf / recvbuf are the harness's pageable vectors), or 2 * P caller-owned host-addressable buckets —
+// bufs[p] = peer p's sendbuf, bufs[P + p] its recvbuf, each of n elements (page-locked and device-mapped for
+// the device entry point, which requires them). ins / recv_init / recv_out / send_out as for fmi_ref_run
+// (allreduce / reduce / scan only). Returns 0, or -1 with the first failure in err.
+FMI_REF_API int fmi_ref_run_bound(int coll, int op, int dtype, int ordered, int P, int root, size_t n, const void* ins,
+                                  const void* recv_init, void* recv_out, void* send_out, const RefBinding* binding,
+                                  void* const* bufs, char* err, size_t errlen) {
+    const size_t es = dtype_size(dtype);
+    if (P < 1 || es == 0 || root < 0 || root >= P || !ins || !binding || coll < kAllreduce || coll > kScan ||
+        op < kSum || op > kMin || (!binding->host_pair && !binding->dev_pair) ||
+        (binding->dev_pair && (!binding->stream_sync || !bufs))) {
+        set_err(err, errlen, "invalid argument");
+        return -1;
+    }
+    const size_t S = n * es;
+    std::vector<std::vector<char>> own(bufs ? 0 : 2 * static_cast<size_t>(P), std::vector<char>(S));
+    std::vector<char*> send(P), recv(P);
+    std::vector<std::pair<const char*, size_t>> mapped;
+    for (int p = 0; p < P; ++p) {
+        send[p] = bufs ? static_cast<char*>(bufs[p]) : own[p].data();
+        recv[p] = bufs ? static_cast<char*>(bufs[P + p]) : own[P + p].data();
+        if (S) {
+            std::memcpy(send[p], static_cast<const char*>(ins) + p * S, S);
+            if (recv_init) std::memcpy(recv[p], static_cast<const char*>(recv_init) + p * S, S);
+            else std::memset(recv[p], 0, S);
+        }
+        mapped.emplace_back(send[p], S);
+        mapped.emplace_back(recv[p], S);
+    }
+    const raw_function f{bound_combine(*binding, op, dtype, n, mapped), /*associative=*/true,
+                         /*commutative=*/ordered == 0};
+    const std::string e = run_peers(
+        P,
+        [&](Loopback& ch, int p) {
+            channel_data sd{send[p], S};
+            channel_data rd{recv[p], S};
+            switch (coll) {
+                case kAllreduce: ch.allreduce(sd, rd, f); break;
+                case kReduce: ch.reduce(sd, rd, static_cast<peer_num>(root), f); break;
+                default: ch.scan(sd, rd, f); break;
+            }
+        },
+        nullptr);
+    if (!e.empty()) {
+        set_err(err, errlen, e);
+        return -1;
+    }
+    for (int p = 0; p < P && S; ++p) {
+        if (recv_out) std::memcpy(static_cast<char*>(recv_out) + p * S, recv[p], S);
+        if (send_out) std::memcpy(static_cast<char*>(send_out) + p * S, send[p], S);
+    }
+    return 0;
+}
+
 namespace {
 
 // Reusable barrier for the peer threads of fmi_ref_time.
@@ -329,42 +432,13 @@ private:
 
 }  // namespace
 
-// CPU timing of the reference's own allreduce (PeerToPeer::allreduce -> allreduce_no_order, f32 sum) over P
-// peer threads and the in-memory transport: bench.py's cpu_baseline leg reports it for config C1 (2 peers,
-// 1 MiB) beside the C++ port. adapter = 1: the combine is the reference's vector adapter as Communicator
-// builds it for Data<std::vector<float>> (include/Communicator.h:180-189: both buckets copied into vectors,
-// the user's Function called by value, the result memcpy'd back) around the Python layer's
-// std::transform(std::plus) (python/PythonCommunicator.h:131-149) — restated here, since Communicator.h
-// cannot be compiled (boost::property_tree); adapter = 0: std::transform in place. Every repetition starts
-// from the same buckets (restored outside the timed span); the time of one repetition is peer 0's, from a
-// barrier that releases every peer to a barrier every peer reaches after its allreduce. Writes the median.
-FMI_REF_API int fmi_ref_time_allreduce(int P, size_t n, int reps, int adapter, double* median_ms, char* err,
-                                       size_t errlen) {
-    if (P < 1 || reps < 1 || !median_ms) {
-        set_err(err, errlen, "invalid argument");
-        return -1;
-    }
+namespace {
+
+int time_allreduce(int P, size_t n, int reps, const raw_func& f, double* median_ms, char* err, size_t errlen) {
     const size_t S = n * sizeof(float);
     std::vector<std::vector<float>> init(P, std::vector<float>(n)), send(P), recv(P, std::vector<float>(n));
     for (int p = 0; p < P; ++p)
         for (size_t i = 0; i < n; ++i) init[p][i] = static_cast<float>((i * 2654435761u + p * 40503u) % 2048) / 1024.0f - 1.0f;
-    raw_func f;
-    if (adapter) {
-        const std::function<std::vector<float>(std::vector<float>, std::vector<float>)> user =
-            [](std::vector<float> a, std::vector<float> b) {
-                std::vector<float> res(a.size());
-                std::transform(a.begin(), a.end(), b.begin(), res.begin(), std::plus<float>());
-                return res;
-            };
-        f = [user, S](char* a, char* b) {
-            std::vector<float> va(reinterpret_cast<float*>(a), reinterpret_cast<float*>(a + S));
-            std::vector<float> vb(reinterpret_cast<float*>(b), reinterpret_cast<float*>(b + S));
-            std::vector<float> res = user(va, vb);
-            std::memcpy(a, res.data(), S);
-        };
-    } else {
-        f = make_combine(kSum, kF32, n);
-    }
     const raw_function rf{f, true, true};
     Barrier bar(P);
     std::vector<double> ms(reps);
@@ -388,4 +462,58 @@ FMI_REF_API int fmi_ref_time_allreduce(int P, size_t n, int reps, int adapter, d
     std::sort(ms.begin(), ms.end());
     *median_ms = ms[ms.size() / 2];
     return 0;
+}
+
+}  // namespace
+
+// fmi_ref_time_allreduce with the combine bound to a C-ABI's host entry point (the
+// reference's own allreduce, every f.f a fmi_host_reduce_pair on the harness's pageable buckets).
+FMI_REF_API int fmi_ref_time_allreduce_bound(int P, size_t n, int reps, const RefBinding* binding, double* median_ms,
+                                             char* err, size_t errlen) {
+    if (P < 1 || reps < 1 || !median_ms || !binding || !binding->host_pair) {
+        set_err(err, errlen, "invalid argument");
+        return -1;
+    }
+    RefBinding host_only = *binding;
+    host_only.dev_pair = nullptr;
+    return time_allreduce(P, n, reps, bound_combine(host_only, kSum, kF32, n, {}), median_ms, err, errlen);
+}
+
+// CPU timing of the reference's own allreduce (PeerToPeer::allreduce -> allreduce_no_order, f32 sum) over P
+// peer threads and the in-memory transport: bench.py's cpu_baseline leg reports it for config C1 (2 peers,
+// 1 MiB) beside the C++ port. adapter = 1: the combine is the reference's vector adapter as Communicator
+// builds it for Data<std::vector<float>> (include/Communicator.h:180-189: both buckets copied into vectors,
+// the user's Function called by value, the result memcpy'd back) around the Python layer's
+// std::transform(std::plus) (python/PythonCommunicator.h:131-149) — restated here, since Communicator.h
+// cannot be compiled (boost::property_tree); adapter = 0: std::transform in place; adapter = 2: a no-op
+// combine, i.e. the collective's transport and copies alone (what separates the allreduce from its combine). Every repetition starts
+// from the same buckets (restored outside the timed span); the time of one repetition is peer 0's, from a
+// barrier that releases every peer to a barrier every peer reaches after its allreduce. Writes the median.
+FMI_REF_API int fmi_ref_time_allreduce(int P, size_t n, int reps, int adapter, double* median_ms, char* err,
+                                       size_t errlen) {
+    if (P < 1 || reps < 1 || !median_ms) {
+        set_err(err, errlen, "invalid argument");
+        return -1;
+    }
+    const size_t S = n * sizeof(float);
+    raw_func f;
+    if (adapter) {
+        const std::function<std::vector<float>(std::vector<float>, std::vector<float>)> user =
+            [](std::vector<float> a, std::vector<float> b) {
+                std::vector<float> res(a.size());
+                std::transform(a.begin(), a.end(), b.begin(), res.begin(), std::plus<float>());
+                return res;
+            };
+        f = [user, S](char* a, char* b) {
+            std::vector<float> va(reinterpret_cast<float*>(a), reinterpret_cast<float*>(a + S));
+            std::vector<float> vb(reinterpret_cast<float*>(b), reinterpret_cast<float*>(b + S));
+            std::vector<float> res = user(va, vb);
+            std::memcpy(a, res.data(), S);
+        };
+    } else if (adapter == 2) {
+        f = [](char*, char*) {};  // the reference's own no-op combine (its barrier, PeerToPeer.cpp:30)
+    } else {
+        f = make_combine(kSum, kF32, n);
+    }
+    return time_allreduce(P, n, reps, f, median_ms, err, errlen);
 }

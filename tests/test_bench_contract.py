@@ -288,3 +288,50 @@ def test_scan_self_check_bracketing_evaluator_equals_the_oracle():
         for r in range(P):
             got = bench.eval_bracketing(fmi_amd.schedule_expr(fmi_amd.Alg.SCAN, P, r), xs)
             assert np.array_equal(got.view(np.uint32), want[r].view(np.uint32)), (P, r)
+
+
+def test_every_line_names_its_workload_and_failed_lines_name_the_runtime(monkeypatch):
+    """The 1/2/4/8 curve spans two workloads, so every line says at top level which one `value` measures
+    (local_combine at N = 1, sharded_allreduce at N > 1), and an N > 1 error line carries the librccl version and
+    path and the device-visibility environment it failed under."""
+    import argparse
+
+    args = argparse.Namespace(gpus=1, force_dist=False, steps=1, warmup=1, bucket_mib=256, sets=16)
+    assert bench._headline(args, 1.0, 1.0, "w", "p", 4, {})["workload"] == bench.WORKLOAD_N1 == "local_combine"
+    args.gpus = 8
+    assert bench._headline(args, 1.0, 1.0, "w", "p", 4, {})["workload"] == bench.WORKLOAD_DIST == "sharded_allreduce"
+    args.gpus, args.force_dist = 1, True
+    assert bench._headline(args, 1.0, 1.0, "w", "p", 4, {})["workload"] == "sharded_allreduce"
+    assert "workload" in bench._HEADLINE_KEYS
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0,1,2,3")
+    line = bench._error_line(4, "RuntimeError: boom", "topology check", topology={"ok": False})
+    assert line["value"] is None and line["workload"] == "sharded_allreduce" and line["phase"] == "topology check"
+    assert line["runtime"]["HIP_VISIBLE_DEVICES"] == "0,1,2,3" and line["topology"] == {"ok": False}
+    assert "rccl_version" in line["runtime"] or "rccl_error" in line["runtime"] or "error" in line["runtime"]
+
+
+def test_failed_checks_fail_the_n1_run():
+    """a wrong C3 or P = 1 result, or a wrong C5 block, makes bench.py exit 1 like a wrong C2; a block
+    that raised is reported in the line, not counted as a wrong result."""
+    ok = {"self_check": {"ok": True}}
+    line = {"self_check": {"ok": True}, "allreduce_1peer": {"result_ok": True},
+            "c3": {"i64_max_pair_64MiB": dict(ok), "f32_scan_P8_64MiB": dict(ok)},
+            "c5": {"p1_copy": dict(ok), "host_pair_reduce": dict(ok), "local_peers": {"error": "MemoryError"}}}
+    assert bench.failed_checks(line) == []
+    line["c3"]["f32_scan_P8_64MiB"] = {"self_check": {"ok": False}}
+    line["allreduce_1peer"]["result_ok"] = False
+    line["c5"]["host_pair_reduce"] = {"self_check": {"ok": False}}
+    assert bench.failed_checks(line) == ["allreduce_1peer", "c3 f32_scan_P8_64MiB", "c5 host_pair_reduce"]
+    line["self_check"]["ok"] = False
+    assert bench.failed_checks(line)[0] == "c2"
+
+
+def test_c5_size_follows_mem_available():
+    """C5's 8-peer block runs 8 x 1 GiB page-locked send + recv buckets (16 GiB) when MemAvailable holds them
+    with C5_HEADROOM to spare, and halves the bucket until it fits otherwise."""
+    G = bench.GIB
+    assert bench.c5_size_mib(8, 1024, None) == 1024
+    assert bench.c5_size_mib(8, 1024, 64 * G) == 1024
+    assert bench.c5_size_mib(8, 1024, 32 * G) == 1024  # 16 + 16 fits exactly
+    assert bench.c5_size_mib(8, 1024, 31 * G) == 512
+    assert bench.c5_size_mib(8, 1024, 20 * G) == 256

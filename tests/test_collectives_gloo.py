@@ -166,3 +166,23 @@ def test_topology_verdict():
     swapped = [rep(0, trank=1), rep(1, trank=0), rep(2), rep(3)]
     assert not judge_topology(swapped, 4, "rccl")["ok"]
     assert judge_topology([rep(0, count=1)], 1, "rccl")["ok"]
+    # the librccl and visibility environment travel with the verdict: rank 0's, and any rank that differs
+    rt = {"rccl_version": 22703, "rccl_path": "/opt/rocm/lib/librccl.so.1.0", "HIP_VISIBLE_DEVICES": None}
+    v = judge_topology([dict(rep(r), runtime=rt) for r in range(4)], 4, "rccl")
+    assert v["runtime"] == rt and "runtime_differs" not in v
+    odd = dict(rt, HIP_VISIBLE_DEVICES="3")
+    v = judge_topology([dict(rep(r), runtime=odd if r == 2 else rt) for r in range(4)], 4, "rccl")
+    assert v["runtime"] == rt and v["runtime_differs"] == {2: odd}
+
+
+def test_runtime_info_names_the_rccl_and_never_raises(monkeypatch):
+    """fmi_amd.comm.runtime_info (config.topology.runtime and every N > 1 error line): the librccl the RCCL
+    transport maps (fmi_comm_rccl_info: ncclGetVersion, real path) and the visibility environment; on a host
+    where librccl cannot be loaded it reports the error instead of raising."""
+    from fmi_amd.comm import runtime_info
+
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0,1")
+    info = runtime_info()
+    assert info["HIP_VISIBLE_DEVICES"] == "0,1"
+    if "rccl_error" not in info:
+        assert info["rccl_version"] > 0 and "librccl" in info["rccl_path"] and os.path.isabs(info["rccl_path"])

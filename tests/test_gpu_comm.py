@@ -511,21 +511,29 @@ def test_c4_8peer_1gib_allreduce_full_size(device):
         b.free()
 
 
-def test_c5_host_allreduce_full_size(device):
-    """BASELINE config C5 at the largest size the one-GPU box takes comfortably: 8 LOCAL ranks, each with a
-    256 MiB f32 bucket in page-locked host memory (2 GiB in, 2 GiB out), fmi_comm_allreduce_host with the
-    default 64 MiB chunks (H2D, sharded allreduce and D2H of successive chunks overlapped). Every rank's host
-    result must equal, bit for bit, the single-GPU fused kernel over the same 8 buckets, and the oracle's
-    simulation of the reference's 8-peer allreduce on 2^16 sampled indices."""
+def test_c5_host_allreduce_full_size(device, record_property):
+    """BASELINE config C5 at its size: 8 LOCAL ranks, each with a 1 GiB f32 bucket in page-locked host memory
+    (8 GiB in, 8 GiB out, all through this one GPU), fmi_comm_allreduce_host with the default 64 MiB chunks (H2D,
+    sharded allreduce and D2H of successive chunks overlapped). The bucket is halved only if the host's
+    MemAvailable cannot hold the 16 GiB of page-locked buckets plus bench.C5_HEADROOM (the size and the limit are
+    printed and recorded). Every rank's host result must equal, bit for bit, the single-GPU fused kernel over the
+    same 8 buckets (compared in 64 MiB pieces), and the oracle's simulation of the reference's 8-peer allreduce on
+    2^16 sampled indices."""
+    import bench
     from fmi_amd import Alg, _lib
 
-    N, n = 8, (256 << 20) // 4
+    N = 8
+    avail = bench.mem_available_bytes()
+    mib = bench.c5_size_mib(N, 1024, avail)
+    record_property("c5_bucket_mib", mib)
+    record_property("mem_available_gib", round(avail / 2 ** 30, 1) if avail else None)
+    print(f"C5 full size: {N} x {mib} MiB page-locked (MemAvailable {avail and avail / 2 ** 30:.1f} GiB)")
+    n = (mib << 20) // 4
     ins = [Bucket(n, np.float32).fill_synthetic(42, r) for r in range(N)]
     ref = Bucket(n, np.float32)
     fmi_amd.reduce_tree(Op.SUM, Alg.ALLREDUCE, ref, ins)
     fmi_amd.sync()
-    want_full = ref.numpy()
-    ref.free()
+    piece = (64 << 20) // 4
 
     def body(c, r):
         s, out = PinnedArray(n, np.float32), PinnedArray(n, np.float32)
@@ -534,7 +542,11 @@ def test_c5_host_allreduce_full_size(device):
             _lib.call("fmi_stream_sync", None)
             out.array[:] = np.float32(np.nan)
             c.allreduce_host(Op.SUM, s.array, out.array)  # chunk 0 = FMI_TUNE_HOST_CHUNK (64 MiB)
-            same = bool(np.array_equal(out.array.view(np.uint32), want_full.view(np.uint32)))
+            same = True
+            for o in range(0, n, piece):
+                k = min(piece, n - o)
+                same = same and bool(np.array_equal(out.array[o:o + k].view(np.uint32),
+                                                    ref.view(o, k).numpy().view(np.uint32)))
             kept = bool(np.array_equal(s.array[:4096], ins[r].view(0, 4096).numpy()))
         finally:
             s.free()
@@ -548,6 +560,9 @@ def test_c5_host_allreduce_full_size(device):
     idx = np.sort(np.random.default_rng(1).choice(n, size=1 << 16, replace=False)).astype(np.uint64)
     xs = [orc.synthetic_at(np.float32, idx, 42, r) for r in range(N)]
     want, _ = orc.allreduce(xs, orc.op_sum)
-    assert_bit_equal(want_full[idx.astype(np.int64)], want[0], "sampled oracle check")
+    full = ref.numpy()
+    assert_bit_equal(full[idx.astype(np.int64)], want[0], "sampled oracle check")
+    del full
+    ref.free()
     for b in ins:
         b.free()

@@ -56,6 +56,42 @@ def test_local_absent_rank_times_out(device):
     assert res.get("joined")
 
 
+@pytest.mark.parametrize("call", ["barrier", "allreduce"])
+def test_local_late_rank_after_a_timeout_times_out_too(device, call):
+    """ranks 0 and 1 time out waiting for rank 2 and return (their published buckets may
+    then be freed); rank 2 arrives afterwards. Rank 2 must get Timeout too — never a barrier that releases on
+    the departed ranks' stale arrivals and then reads their buckets."""
+    uid = unique_id(Transport.LOCAL)
+    n = 4099
+    outcome = {}
+
+    def rank(r, delay):
+        c = Comm(uid, 3, r, timeout_s=1.0)
+        x, o = Bucket.from_numpy(np.full(n, r + 1, np.float32)), Bucket(n, np.float32)
+        time.sleep(delay)
+        try:
+            if call == "barrier":
+                c.barrier()
+            else:
+                c.allreduce(Op.SUM, x, o)
+                fmi_amd.sync()
+            outcome[r] = "completed"
+        except Timeout:
+            outcome[r] = "timeout"
+        except fmi_amd.FmiError as e:
+            outcome[r] = f"error: {e}"
+        x.free()
+        o.free()
+        c.destroy()
+
+    threads = [threading.Thread(target=rank, args=(r, 2.5 if r == 2 else 0.0)) for r in range(3)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=60)
+    assert outcome == {0: "timeout", 1: "timeout", 2: "timeout"}, outcome
+
+
 def _run(cmd, timeout):
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=timeout,
                        env=dict(os.environ, OMP_NUM_THREADS="1"))

@@ -7,7 +7,7 @@ bucket sizes and rotating-set counts. Also checks that every budget gives identi
 
 Rotating sets: the sc1 tiles' lines stay in the 256 MB MALL (nontemporal reads do not displace them), so a
 set re-read within ~256 MB of sc1 writes partly hits the MALL — use enough sets that it cannot (sets x
-sc1 bytes per launch >> 256 MB) to measure the combine itself (profiles/r02_ab_pair_sc1_*).
+sc1 bytes per launch >> 256 MB) to measure the combine itself (profiles/archive/r02_ab_pair_sc1_*).
 """
 import argparse
 import json

@@ -336,7 +336,7 @@ def host_allreduce_rows():
             s.array[:] = np.float32(r + 1)
         for chunk in chunks:
             # a quiet device first: VRAM freed by the rows before is cleared asynchronously on the copy
-            # engines these H2D / D2H copies use (profiles/r02_c5_after_free_probe.jsonl)
+            # engines these H2D / D2H copies use (profiles/archive/r02_c5_after_free_probe.jsonl)
             fmi_amd.sync()
             time.sleep(1.0)
             uid = unique_id(Transport.LOCAL)

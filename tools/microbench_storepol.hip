@@ -4,7 +4,7 @@
 // the last X MiB), on an interleave (k of every m tiles — consecutive workgroups land on different XCDs, so
 // k of 8 = k XCDs), on the individual store instruction, or on the bucket size and placement (in / out of
 // place)? One parametrised harness; round 2 asked these questions with six forks of it (tailpol, tailsweep,
-// sc1mix 1/2/3, sc1tail; git history at cabc6be), whose evidence stays in profiles/r02_{tailpol,tailsweep,
+// sc1mix 1/2/3, sc1tail; git history at cabc6be), whose evidence stays in profiles/archive/r02_{tailpol,tailsweep,
 // sc1mix*,sc1tail*}*.jsonl. The library's answer is FMI_TUNE_PAIR_SC1_OF_8 (k = 1: one XCD's tiles sc1,
 // tools/ab_pair_sc1.py, measured with no MALL re-use).
 //

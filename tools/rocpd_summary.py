@@ -3,7 +3,7 @@ calls, mean / median / min duration (us), VGPRs and scratch bytes. One launch sh
 tools/bench_configs.py, so the rows line up with its JSON lines (the time per launch there comes from HIP
 events; here from the profiler's own dispatch timestamps).
 
-    python tools/rocpd_summary.py gpurun_out/cfgprof/run_results.db > profiles/r01_configs_kernel_stats.csv
+    python tools/rocpd_summary.py gpurun_out/cfgprof/run_results.db > profiles/archive/r01_configs_kernel_stats.csv
 """
 import csv
 import sqlite3
