@@ -952,6 +952,9 @@ class _PhaseWatch:
 
     def enter(self, phase):
         self.phase = phase
+        # test hook (tests/test_gpu_bench_dist.py): every rank fails in the named phase, as a real failure would
+        if os.environ.get("FMI_BENCH_TEST_RAISE_IN") and phase.startswith(os.environ["FMI_BENCH_TEST_RAISE_IN"]):
+            raise RuntimeError(f"injected failure in phase '{phase}' (FMI_BENCH_TEST_RAISE_IN)")
 
     def _expire(self):
         print(f"bench: rank {self.rank} still in phase '{self.phase}' after {time.time() - self.t0:.0f} s "

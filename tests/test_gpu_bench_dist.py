@@ -13,6 +13,10 @@ ranks on one GPU).
 - test_bench_py_launches_its_own_ranks: `python bench.py --gpus 2 …` with no launcher starts its ranks itself
   and prints the same one self-checked line.
 - test_bench_py_force_dist_rccl_world1: the RCCL transport's own rank count (ncclCommCount) in the line.
+Every N > 1 line must name its workload (`sharded_allreduce`) and the librccl version and path plus the
+visibility environment it ran under (`config.topology.runtime`); the N = 1 line says `local_combine`.
+- test_bench_py_error_line_names_the_runtime: ranks that fail before `value` leave one line with the error,
+  the phase and the same runtime fields.
 """
 import json
 import os
@@ -83,8 +87,12 @@ def test_bench_py_proc_transport(world):
 
 
 def _check_topology_and_anchor(line, world, transport):
+    assert line["workload"] == "sharded_allreduce", line.get("workload")
     topo = line["config"]["topology"]
     assert topo["ok"] and topo["transport"] == transport and len(topo["ranks"]) == world, topo
+    rt = topo["runtime"]  # the librccl and visibility environment the run used
+    assert rt["rccl_version"] > 0 and "librccl" in rt["rccl_path"] and os.path.isabs(rt["rccl_path"]), rt
+    assert "HIP_VISIBLE_DEVICES" in rt and "GPU_MAX_HW_QUEUES" in rt and "runtime_differs" not in topo, topo
     assert [r["transport_rank"] for r in topo["ranks"]] == list(range(world)), topo
     assert all(r["pci_bus_id"] for r in topo["ranks"]), topo
     if transport == "proc":
@@ -151,4 +159,25 @@ def test_bench_py_n1_line_self_checks_the_timed_combines():
     line = json.loads(lines[0])
     chk = line["self_check"]
     assert line["n_gpus"] == 1 and line["value"] > 0 and chk["ok"] and chk["mismatches"] == 0
+    assert line["workload"] == "local_combine"
     assert chk["elements_checked"] == 4 * 3 * 4096
+
+
+def test_bench_py_error_line_names_the_runtime():
+    """A failed N > 1 run is diagnosable from its one line: every rank fails in the phase right after the
+    communicator bootstrap (FMI_BENCH_TEST_RAISE_IN, bench._PhaseWatch.enter), and rank 0's line must carry the
+    error, the phase and the runtime (librccl version and path, visibility environment)."""
+    env = dict(os.environ, FMI_PROC_TIMEOUT_S="60", OMP_NUM_THREADS="1", FMI_BENCH_TEST_RAISE_IN="topology check")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
+           "--transport", "proc", "--steps", "2", "--warmup", "1", "--bucket-mib", "1", "--no-c5",
+           "--no-diagnostics"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode != 0
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout + r.stderr[-3000:]
+    line = json.loads(lines[0])
+    assert line["value"] is None and line["workload"] == "sharded_allreduce", line
+    assert line["phase"] == "topology check" and "injected failure" in line["error"], line
+    rt = line["runtime"]
+    assert rt["rccl_version"] > 0 and "librccl" in rt["rccl_path"] and "HIP_VISIBLE_DEVICES" in rt, rt

@@ -1,6 +1,6 @@
 set -o pipefail
 cd /root/repo
 mkdir -p gpurun_out
-timeout -k 10 700 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_ref_binding.py tests/test_gpu_timeout.py tests/test_gpu_comm.py::test_c5_host_allreduce_full_size -rA > gpurun_out/r04_a_tests.log 2>&1 &&
+timeout -k 10 1000 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_ref_binding.py tests/test_gpu_timeout.py tests/test_gpu_comm.py::test_c5_host_allreduce_full_size tests/test_gpu_bench_dist.py -rA > gpurun_out/r04_a_tests.log 2>&1 &&
 timeout -k 10 600 python bench.py > gpurun_out/r04_a_bench.json 2> gpurun_out/r04_a_bench.err &&
 cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /root/repo/gpurun_out/r04_scanlds -o run -- /root/repo/build/mbscanlds 3 > /root/repo/gpurun_out/r04_scanlds.jsonl 2> /root/repo/gpurun_out/r04_scanlds.err
