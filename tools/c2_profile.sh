@@ -5,7 +5,7 @@ R=$PWD
 mkdir -p gpurun_out/c2t gpurun_out/c2f gpurun_out/c2w
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/c2t -o run -- python3 $R/bench.py > $R/gpurun_out/c2_bench_under_rocprof.txt 2> $R/gpurun_out/c2t.err
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $R/gpurun_out/c2f -o run -- python3 $R/bench.py --no-cpu-baseline --steps 40 --warmup 5 > $R/gpurun_out/c2f.log 2>&1
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $R/gpurun_out/c2w -o run -- python3 $R/bench.py --no-cpu-baseline --steps 40 --warmup 5 > $R/gpurun_out/c2w.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $R/gpurun_out/c2f -o run -- python3 $R/bench.py --no-cpu-baseline --no-c5 --steps 40 --warmup 5 > $R/gpurun_out/c2f.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $R/gpurun_out/c2w -o run -- python3 $R/bench.py --no-cpu-baseline --no-c5 --steps 40 --warmup 5 > $R/gpurun_out/c2w.log 2>&1
 cd $R
 timeout -k 10 200 python3 bench.py --no-cpu-baseline > gpurun_out/c2_bench_plain.json
