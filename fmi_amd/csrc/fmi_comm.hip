@@ -836,6 +836,9 @@ constexpr size_t kProcCtrlBytes = size_t(64) << 10;
 struct ProcCtrl {  // lives in the shared segment; all-zero is the initial state
     std::atomic<uint64_t> arrived;
     std::atomic<uint64_t> generation;
+    // set by a rank whose wait for the peers timed out: its arrival may still be counted and its slot may be
+    // stale, so no later barrier or mailbox wait of any rank may complete on it (the LOCAL hub's rule)
+    std::atomic<int> poisoned;
     struct Mail {  // what rank src's slot holds for point-to-point: a message for `dst` until ack == seq
         std::atomic<int> dst;
         std::atomic<uint64_t> bytes;
@@ -1067,6 +1070,8 @@ private:
     }
 
     int host_barrier(const char* what) {
+        if (ctrl_->poisoned.load(std::memory_order_acquire))
+            return timed_out(std::string("PROC transport: a peer timed out earlier (") + what + ")");
         const uint64_t g = ctrl_->generation.load(std::memory_order_acquire);
         if (ctrl_->arrived.fetch_add(1, std::memory_order_acq_rel) + 1 == static_cast<uint64_t>(n_)) {
             ctrl_->arrived.store(0, std::memory_order_relaxed);
@@ -1083,8 +1088,14 @@ private:
         const auto t0 = Clock::now();
         for (int k = 0; !ready(); ++k) {
             backoff(k);
-            if (k >= 1000 && (k & 255) == 0 && std::chrono::duration<double>(Clock::now() - t0).count() > timeout_s_)
-                return timed_out(std::string("PROC transport: waiting for peers (") + what + ")");
+            if (k >= 1000 && (k & 255) == 0) {
+                if (ctrl_->poisoned.load(std::memory_order_acquire))
+                    return timed_out(std::string("PROC transport: a peer timed out (") + what + ")");
+                if (std::chrono::duration<double>(Clock::now() - t0).count() > timeout_s_) {
+                    ctrl_->poisoned.store(1, std::memory_order_release);
+                    return timed_out(std::string("PROC transport: waiting for peers (") + what + ")");
+                }
+            }
         }
         return FMI_OK;
     }
