@@ -95,6 +95,7 @@ SIGNATURES = {
     "fmi_dev_reduce_tree": (_i, [_i, _i, _i, _vp, _c.POINTER(_vp), _i, _i, _sz, _vp]),
     "fmi_dev_scan_peers": (_i, [_i, _i, _i, _c.POINTER(_vp), _c.POINTER(_vp), _i, _sz, _vp]),
     "fmi_host_reduce_pair": (_i, [_i, _i, _vp, _vp, _sz]),
+    "fmi_host_device_ptr": (_i, [_vp, _sz, _c.POINTER(_vp)]),
     "fmi_comm_unique_id": (_i, [_i, _vp, _sz]),
     "fmi_comm_init": (_i, [_c.POINTER(_vp), _vp, _i, _i]),
     "fmi_comm_init_timeout": (_i, [_c.POINTER(_vp), _vp, _i, _i, _c.c_double]),

@@ -895,6 +895,15 @@ int fmi_host_unregister(void* ptr) {
     return FMI_OK;
 }
 
+int fmi_host_device_ptr(const void* host, size_t bytes, void** dev) {
+    if (!host || !dev || bytes == 0) return fail(FMI_ERR_INVALID, "fmi_host_device_ptr: null pointer or empty range");
+    if (int rc = require_device()) return rc;
+    if (!host_mapped(const_cast<void*>(host), bytes, dev))
+        return fail(FMI_ERR_INVALID, "fmi_host_device_ptr: the range is not wholly inside one page-locked, device-mapped "
+                                     "range (fmi_host_pin_alloc / fmi_host_register)");
+    return FMI_OK;
+}
+
 static int copy_async(void* dst, const void* src, size_t bytes, hipMemcpyKind kind, fmi_stream_t stream) {
     if (bytes == 0) return FMI_OK;
     if (!dst || !src) return fail(FMI_ERR_INVALID, "null buffer");

@@ -114,6 +114,10 @@ int fmi_host_pin_free(void* ptr);
  * (FMI_ERR_INVALID otherwise). */
 int fmi_host_register(void* ptr, size_t bytes);
 int fmi_host_unregister(void* ptr);
+/* The device address of [host, host + bytes), a range wholly inside one page-locked, device-mapped range
+ * (fmi_host_pin_alloc / fmi_host_register): what a caller hands to fmi_dev_reduce_pair to combine host recv
+ * buffers in place over PCIe. FMI_ERR_INVALID for pageable or straddling ranges. */
+int fmi_host_device_ptr(const void* host, size_t bytes, void** dev);
 int fmi_dev_h2d_async(void* dst, const void* src, size_t bytes, fmi_stream_t stream);
 int fmi_dev_d2h_async(void* dst, const void* src, size_t bytes, fmi_stream_t stream);
 int fmi_dev_d2d_async(void* dst, const void* src, size_t bytes, fmi_stream_t stream);

@@ -20,6 +20,7 @@ import ctypes
 import numpy as np
 import pytest
 
+import fmi_amd
 from fmi_amd import PinnedArray, _lib
 from oracle import fmi_ref as ref
 from tests.test_gpu_parity import assert_bit_equal, inputs
@@ -73,13 +74,12 @@ def _pinned_buckets(P, n, dtype):
     return bufs, [b.ptr for b in bufs]
 
 
-def _assert_device_addressable(ptrs):
+def _assert_device_addressable(ptrs, nbytes):
     """The device entry point hands the caller's host pointers to a kernel: each must be the address the GPU
-    maps the page-locked bucket at (hipHostGetDevicePointer), checked before any launch."""
-    hip = ctypes.CDLL("libamdhip64.so.7")
+    maps the page-locked bucket at (fmi_host_device_ptr), checked before any launch."""
     for p in ptrs:
         dp = ctypes.c_void_p()
-        assert hip.hipHostGetDevicePointer(ctypes.byref(dp), ctypes.c_void_p(p), 0) == 0
+        _lib.call("fmi_host_device_ptr", p, nbytes, ctypes.byref(dp))
         assert dp.value == p, "page-locked bucket is mapped at another device address"
 
 
@@ -92,7 +92,7 @@ def test_reference_collectives_on_pinned_buckets(binding, device_binding, P):
         xs = _peers(dtype, P, N, seed=100 + P)
         bufs, ptrs = _pinned_buckets(P, N, dtype)
         try:
-            _assert_device_addressable(ptrs)
+            _assert_device_addressable(ptrs, N * np.dtype(dtype).itemsize)
             for op in OPS:
                 for ordered in (False, True):
                     for coll, roots in (("allreduce", [0]), ("scan", [0]), ("reduce", range(P))):
@@ -118,7 +118,7 @@ def test_c1_shape_through_both_entries(binding, device_binding):
     _check(ref.run_bound("allreduce", "sum", xs, binding), want, "C1 host entry, pageable")
     bufs, ptrs = _pinned_buckets(2, n, np.float32)
     try:
-        _assert_device_addressable(ptrs)
+        _assert_device_addressable(ptrs, n * 4)
         _check(ref.run_bound("allreduce", "sum", xs, binding, bufs=ptrs), want, "C1 host entry, pinned")
         _check(ref.run_bound("allreduce", "sum", xs, device_binding, bufs=ptrs), want, "C1 device entry, pinned")
     finally:
@@ -141,3 +141,18 @@ def test_library_errors_reach_the_reference_caller(binding):
     b = ref.Binding(ctypes.cast(bad_op, ctypes.c_void_p).value, None, binding.stream_sync, binding.last_error)
     with pytest.raises(ref.RefError, match="unknown op 9"):
         ref.run_bound("allreduce", "sum", _peers(np.float32, 2, 64), b)
+
+
+def test_host_device_ptr(device):
+    """fmi_host_device_ptr: the device address of a page-locked range (the same address for fmi_host_pin_alloc
+    memory on MI355X); a pageable range is refused."""
+    a = PinnedArray(1024, np.float32)
+    try:
+        dp = ctypes.c_void_p()
+        _lib.call("fmi_host_device_ptr", a.ptr + 64, 512, ctypes.byref(dp))
+        assert dp.value == a.ptr + 64
+        pageable = np.zeros(1024, np.float32)
+        with pytest.raises(fmi_amd.FmiError, match="page-locked"):
+            _lib.call("fmi_host_device_ptr", pageable.ctypes.data, 64, ctypes.byref(dp))
+    finally:
+        a.free()
