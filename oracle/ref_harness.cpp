@@ -497,7 +497,7 @@ FMI_REF_API int fmi_ref_time_allreduce(int P, size_t n, int reps, int adapter, d
     }
     const size_t S = n * sizeof(float);
     raw_func f;
-    if (adapter) {
+    if (adapter == 1) {
         const std::function<std::vector<float>(std::vector<float>, std::vector<float>)> user =
             [](std::vector<float> a, std::vector<float> b) {
                 std::vector<float> res(a.size());

@@ -1,3 +1,7 @@
+# Round 4, first GPU call (profiles/r04_a_*, r04_scan_lds*): the round's new GPU tests, the default bench line,
+# and the LDS-staged scan experiment under rocprofv3. Its third step ran build/mbscanlds, built from
+# tools/microbench_scan_lds.hip, which was deleted after the experiment failed its stop rule (the
+# source is in git history at the commit that added profiles/r04_scan_lds.jsonl).
 set -o pipefail
 cd /root/repo
 mkdir -p gpurun_out
