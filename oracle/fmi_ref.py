@@ -192,6 +192,21 @@ def time_allreduce_bound(P: int, n: int, reps: int, binding: Binding) -> float:
     return ms.value
 
 
+def time_combine(threads: int, n: int, reps: int, adapter: bool) -> float:
+    """Median ms of the f32 sum combine alone (adapter=True: the reference's vector adapter; False: std::transform
+    in place) applied by `threads` threads at once, each to its own pair of n-element buckets (slowest thread)."""
+    lib = _load()
+    f = lib.fmi_ref_time_combine
+    f.restype = ctypes.c_int
+    f.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
+                  ctypes.c_char_p, ctypes.c_size_t]
+    ms = ctypes.c_double(0.0)
+    err = ctypes.create_string_buffer(512)
+    if f(threads, n, reps, int(bool(adapter)), ctypes.byref(ms), err, len(err)) != 0:
+        raise RefError(err.value.decode())
+    return ms.value
+
+
 def time_allreduce(P: int, n: int, reps: int, adapter) -> float:
     """Median ms of the reference's own f32 sum-allreduce (PeerToPeer::allreduce) over P peer threads and the
     in-memory transport; adapter=True combines through the reference's vector adapter (include/Communicator.h

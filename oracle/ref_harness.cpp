@@ -29,6 +29,7 @@
 //   fmi_ref_expr  symbolic run: each element is a handle to an expression; f.f(a, b) makes "(a+b)" (left operand
 //                 = arg 0 of f.f), so the result is the exact bracketing the reference evaluates.
 //   fmi_ref_time_allreduce  CPU time of the reference's allreduce (bench.py's C1 / C2 rows of the CPU baseline).
+//   fmi_ref_time_combine    CPU time of the combine alone, on 1 or several concurrent threads (C2 row).
 //   fmi_ref_run_bound / fmi_ref_time_allreduce_bound  the same reference collectives with f.f bound to a
 //                 bucket-reduction C-ABI whose entry points the caller passes by address (INTEGRATION.md §B.2;
 //                 tests/test_gpu_ref_binding.py binds libfmi_dev.so). Nothing of that library is linked here.
@@ -466,6 +467,72 @@ int time_allreduce(int P, size_t n, int reps, const raw_func& f, double* median_
 
 }  // namespace
 
+namespace {
+
+// The raw_func Communicator::convert_to_raw_function builds for a Data<std::vector<float>> bucket
+// (include/Communicator.h:180-189, restated: that header needs boost) around the reference's own
+// FMI::Utils::Function (include/utils/Function.h, compiled here: its operator() takes both buckets by value and
+// calls the std::function, which copies them again) holding the Python layer's built-in sum
+// (python/PythonCommunicator.h:131-149: std::transform with std::plus).
+raw_func reference_adapter(size_t n) {
+    const size_t S = n * sizeof(float);
+    const FMI::Utils::Function<std::vector<float>> user(
+        [](std::vector<float> a, std::vector<float> b) {
+            std::vector<float> res(a.size());
+            std::transform(a.begin(), a.end(), b.begin(), res.begin(), std::plus<float>());
+            return res;
+        },
+        true, true);
+    return [user, S](char* a, char* b) {
+        std::vector<float> va(reinterpret_cast<float*>(a), reinterpret_cast<float*>(a + S));
+        std::vector<float> vb(reinterpret_cast<float*>(b), reinterpret_cast<float*>(b + S));
+        std::vector<float> res = user(va, vb);
+        std::memcpy(a, res.data(), S);
+    };
+}
+
+}  // namespace
+
+// The combine alone, outside any collective: `threads` threads each apply the f32 sum combine (adapter = 1: the
+// reference's vector adapter; 0: std::transform in place) to their own pair of n-element buckets at the same
+// time, released together by a barrier; the time of one repetition is the slowest thread's. With threads = 1 it
+// is what oracle/cpu_baseline.cpp times; with threads = P it is the load the P peers of an allreduce put on the
+// host at once (bench.py's cpu_baseline.c2_reference separates the two). Writes the median of `reps`.
+FMI_REF_API int fmi_ref_time_combine(int threads, size_t n, int reps, int adapter, double* median_ms, char* err,
+                                     size_t errlen) {
+    if (threads < 1 || reps < 1 || !median_ms) {
+        set_err(err, errlen, "invalid argument");
+        return -1;
+    }
+    const raw_func f = adapter ? reference_adapter(n) : make_combine(kSum, kF32, n);
+    std::vector<std::vector<float>> a(threads, std::vector<float>(n)), b(threads, std::vector<float>(n));
+    for (int t = 0; t < threads; ++t)
+        for (size_t i = 0; i < n; ++i) {
+            a[t][i] = static_cast<float>((i * 2654435761u + t * 40503u) % 2048) / 1024.0f - 1.0f;
+            b[t][i] = static_cast<float>((i * 40503u + t * 2654435761u) % 2048) / 1024.0f - 1.0f;
+        }
+    Barrier bar(threads);
+    std::vector<std::vector<double>> ms(threads, std::vector<double>(reps));
+    std::vector<std::thread> th;
+    for (int t = 0; t < threads; ++t)
+        th.emplace_back([&, t] {
+            for (int r = 0; r < reps; ++r) {
+                bar.wait();
+                const auto t0 = std::chrono::steady_clock::now();
+                f(reinterpret_cast<char*>(a[t].data()), reinterpret_cast<char*>(b[t].data()));
+                ms[t][r] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+                bar.wait();
+            }
+        });
+    for (auto& x : th) x.join();
+    std::vector<double> slowest(reps, 0.0);
+    for (int r = 0; r < reps; ++r)
+        for (int t = 0; t < threads; ++t) slowest[r] = std::max(slowest[r], ms[t][r]);
+    std::sort(slowest.begin(), slowest.end());
+    *median_ms = slowest[reps / 2];
+    return 0;
+}
+
 // fmi_ref_time_allreduce with the combine bound to a C-ABI's host entry point (the
 // reference's own allreduce, every f.f a fmi_host_reduce_pair on the harness's pageable buckets).
 FMI_REF_API int fmi_ref_time_allreduce_bound(int P, size_t n, int reps, const RefBinding* binding, double* median_ms,
@@ -483,9 +550,9 @@ FMI_REF_API int fmi_ref_time_allreduce_bound(int P, size_t n, int reps, const Re
 // peer threads and the in-memory transport: bench.py's cpu_baseline leg reports it for config C1 (2 peers,
 // 1 MiB) beside the C++ port. adapter = 1: the combine is the reference's vector adapter as Communicator
 // builds it for Data<std::vector<float>> (include/Communicator.h:180-189: both buckets copied into vectors,
-// the user's Function called by value, the result memcpy'd back) around the Python layer's
-// std::transform(std::plus) (python/PythonCommunicator.h:131-149) — restated here, since Communicator.h
-// cannot be compiled (boost::property_tree); adapter = 0: std::transform in place; adapter = 2: a no-op
+// the reference's own FMI::Utils::Function called by value, the result memcpy'd back) around the Python layer's
+// std::transform(std::plus) (python/PythonCommunicator.h:131-149) — the lambda restated (reference_adapter),
+// since Communicator.h cannot be compiled (boost::property_tree); adapter = 0: std::transform in place; adapter = 2: a no-op
 // combine, i.e. the collective's transport and copies alone (what separates the allreduce from its combine). Every repetition starts
 // from the same buckets (restored outside the timed span); the time of one repetition is peer 0's, from a
 // barrier that releases every peer to a barrier every peer reaches after its allreduce. Writes the median.
@@ -495,21 +562,9 @@ FMI_REF_API int fmi_ref_time_allreduce(int P, size_t n, int reps, int adapter, d
         set_err(err, errlen, "invalid argument");
         return -1;
     }
-    const size_t S = n * sizeof(float);
     raw_func f;
     if (adapter == 1) {
-        const std::function<std::vector<float>(std::vector<float>, std::vector<float>)> user =
-            [](std::vector<float> a, std::vector<float> b) {
-                std::vector<float> res(a.size());
-                std::transform(a.begin(), a.end(), b.begin(), res.begin(), std::plus<float>());
-                return res;
-            };
-        f = [user, S](char* a, char* b) {
-            std::vector<float> va(reinterpret_cast<float*>(a), reinterpret_cast<float*>(a + S));
-            std::vector<float> vb(reinterpret_cast<float*>(b), reinterpret_cast<float*>(b + S));
-            std::vector<float> res = user(va, vb);
-            std::memcpy(a, res.data(), S);
-        };
+        f = reference_adapter(n);
     } else if (adapter == 2) {
         f = [](char*, char*) {};  // the reference's own no-op combine (its barrier, PeerToPeer.cpp:30)
     } else {

@@ -293,7 +293,7 @@ def test_reference_library_is_built_from_the_reference_alone():
                          text=True).stdout
     exported = sorted(line.split()[-1] for line in dyn.splitlines() if " T " in line)
     assert exported == ["fmi_ref_expr", "fmi_ref_run", "fmi_ref_run_bound", "fmi_ref_time_allreduce",
-                        "fmi_ref_time_allreduce_bound"], exported
+                        "fmi_ref_time_allreduce_bound", "fmi_ref_time_combine"], exported
     # the product's C-ABI reaches the harness only by address (fmi_ref_run_bound): nothing of it is linked
     needed = subprocess.run(["readelf", "-d", ref.LIB_PATH], check=True, capture_output=True, text=True).stdout
     assert "libfmi_dev" not in needed and "fmi_" not in undefined, (needed, undefined)
