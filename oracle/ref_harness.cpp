@@ -473,14 +473,14 @@ namespace {
 // (include/Communicator.h:180-189, restated: that header needs boost) around the reference's own
 // FMI::Utils::Function (include/utils/Function.h, compiled here: its operator() takes both buckets by value and
 // calls the std::function, which copies them again) holding the Python layer's built-in sum
-// (python/PythonCommunicator.h:131-149: std::transform with std::plus).
+// (python/PythonCommunicator.h:131-149: get_vec_function's SUM, std::transform with std::plus into its first
+// by-value argument, which it returns).
 raw_func reference_adapter(size_t n) {
     const size_t S = n * sizeof(float);
-    const FMI::Utils::Function<std::vector<float>> user(
+    const FMI::Utils::Function<std::vector<float>> user(  // get_vec_function's SUM, PythonCommunicator.h:135
         [](std::vector<float> a, std::vector<float> b) {
-            std::vector<float> res(a.size());
-            std::transform(a.begin(), a.end(), b.begin(), res.begin(), std::plus<float>());
-            return res;
+            std::transform(a.begin(), a.end(), b.begin(), a.begin(), std::plus<float>());
+            return a;
         },
         true, true);
     return [user, S](char* a, char* b) {
@@ -497,7 +497,8 @@ raw_func reference_adapter(size_t n) {
 // reference's vector adapter; 0: std::transform in place) to their own pair of n-element buckets at the same
 // time, released together by a barrier; the time of one repetition is the slowest thread's. With threads = 1 it
 // is what oracle/cpu_baseline.cpp times; with threads = P it is the load the P peers of an allreduce put on the
-// host at once (bench.py's cpu_baseline.c2_reference separates the two). Writes the median of `reps`.
+// host at once (bench.py's cpu_baseline.c2_reference separates the two). Writes the median of `reps`, after one
+// untimed warm-up.
 FMI_REF_API int fmi_ref_time_combine(int threads, size_t n, int reps, int adapter, double* median_ms, char* err,
                                      size_t errlen) {
     if (threads < 1 || reps < 1 || !median_ms) {
@@ -516,11 +517,12 @@ FMI_REF_API int fmi_ref_time_combine(int threads, size_t n, int reps, int adapte
     std::vector<std::thread> th;
     for (int t = 0; t < threads; ++t)
         th.emplace_back([&, t] {
-            for (int r = 0; r < reps; ++r) {
+            for (int r = -1; r < reps; ++r) {  // r = -1: one untimed warm-up, as oracle/cpu_baseline.cpp does
                 bar.wait();
                 const auto t0 = std::chrono::steady_clock::now();
                 f(reinterpret_cast<char*>(a[t].data()), reinterpret_cast<char*>(b[t].data()));
-                ms[t][r] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+                if (r >= 0)
+                    ms[t][r] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
                 bar.wait();
             }
         });
