@@ -1255,6 +1255,7 @@ struct Comm {
                 windows.clear();
                 return;
             }
+            for (auto& [st, ev] : user_tail) (void)hipEventDestroy(ev);
             for (void* b : buf)
                 if (b) (void)hipFree(b);
             for (auto& [base, w] : windows) {
