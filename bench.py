@@ -156,7 +156,10 @@ def cpu_baseline(args):
                    f"{os.cpu_count()} CPUs visible"),
         "bare_loop_gib_s": round(bare["bucket_gib_s"], 4),
         "all_threads_loop": {"gib_s": round(omp["bucket_gib_s"], 4), "threads": omp["threads"],
-                             "median_ms": round(omp["median_ms"], 3)},
+                             "median_ms": round(omp["median_ms"], 3),
+                             "note": f"OMP_NUM_THREADS = {os.environ.get('OMP_NUM_THREADS')}: the CPU share the "
+                                     f"box allots one GPU's job; os.cpu_count() = {os.cpu_count()} counts the whole "
+                                     "machine, whose other cores belong to other GPUs' jobs"},
         "c1": c1_host(),
         "c1_reference": c1_reference(),
         "c2_reference": c2_reference(args.bucket_mib, adapter["median_ms"]),
