@@ -834,6 +834,7 @@ def mem_available_bytes():
 
 
 C5_HEADROOM = 16 * GIB  # host memory left free beside C5's page-locked buckets
+_LEAKED = []  # host buckets a stuck rank may still use: never freed in this process
 
 
 def c5_size_mib(peers: int, mib: int, avail) -> int:
@@ -866,6 +867,7 @@ def c5_local_peers(peers: int, mib: int, iters: int = 2) -> dict:
     n = size * MIB // 4
     send = _pinned_synthetic(n, 91, range(peers))
     recv = []
+    stuck = False
     try:
         recv = [PinnedArray(n, np.float32) for _ in range(peers)]
         uid = unique_id(Transport.LOCAL)
@@ -888,11 +890,14 @@ def c5_local_peers(peers: int, mib: int, iters: int = 2) -> dict:
                 bar.abort()
                 errors.append(f"rank {r}: {type(e).__name__}: {e}")
 
-        threads = [threading.Thread(target=rank, args=(r,)) for r in range(peers)]
+        threads = [threading.Thread(target=rank, args=(r,), daemon=True) for r in range(peers)]
         for t in threads:
             t.start()
         for t in threads:
             t.join(timeout=600)
+        if any(t.is_alive() for t in threads):  # a rank still inside the library: its buckets must outlive it
+            stuck = True
+            raise RuntimeError("C5 local_peers: a rank did not finish within 600 s (buckets leaked, not freed)")
         if errors:
             raise RuntimeError(errors[0])
         per_iter = [max(times[r][k] for r in range(peers)) for k in range(1, iters + 1)]
@@ -904,8 +909,11 @@ def c5_local_peers(peers: int, mib: int, iters: int = 2) -> dict:
                 want = eval_bracketing(fmi_amd.schedule_expr(Alg.ALLREDUCE, peers, r), xs)
                 bad += int(np.count_nonzero(recv[r].array[o:o + win].view(np.uint32) != want.view(np.uint32)))
     finally:
-        for h in send + recv:
-            h.free()
+        if stuck:
+            _LEAKED.extend(send + recv)  # kept referenced: PinnedArray frees itself when collected
+        else:
+            for h in send + recv:
+                h.free()
     ms = statistics.median(per_iter) * 1e3
     S = n * 4
     return {"workload": f"C5 on one GPU: {peers} LOCAL ranks x {size} MiB f32 page-locked host buckets, "
