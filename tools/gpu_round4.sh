@@ -6,6 +6,10 @@
 #   bash tools/gpu_round4.sh b   the default bench line after the C2-size reference baseline's no-op mode was
 #                                fixed, then the C2 profile of the round-4 library (tools/c2_profile.sh:
 #                                kernel trace + stats, separate FETCH_SIZE / WRITE_SIZE passes, an unprofiled line)
+#   bash tools/gpu_round4.sh c   C5's local_peers block (8 LOCAL ranks x 1 GiB) at GPU_MAX_HW_QUEUES = 4 / 8 / 16
+#                                (profiles/r04_c5_local_peers_hwq.jsonl)
+#   bash tools/gpu_round4.sh d   the DMA ceiling of that shape: 8 threads, each streaming 1 GiB H2D and 1 GiB D2H
+#                                on two streams in 64 / 256 MiB pieces, no compute (profiles/r04_pcie_8streams.jsonl)
 set -o pipefail
 cd /root/repo
 mkdir -p gpurun_out
@@ -20,8 +24,60 @@ b)
     timeout -k 10 600 python bench.py > gpurun_out/r04_b_bench.json 2> gpurun_out/r04_b_bench.err &&
     bash tools/c2_profile.sh
     ;;
+c)
+    for q in 4 8 16; do
+        GPU_MAX_HW_QUEUES=$q timeout -k 10 200 python -u -c "
+import json, bench, fmi_amd
+fmi_amd.init(0)
+r = bench.c5_local_peers(8, 1024)
+print(json.dumps({'GPU_MAX_HW_QUEUES': $q, 'ms': r['ms'], 'host_buckets_GiB_s': r['host_buckets_GiB_s'],
+                  'pcie_GB_s': r['pcie_GB_s_both_directions'], 'ok': r['self_check']['ok']}))
+" >> gpurun_out/r04_c5_local_peers_hwq.jsonl || exit 1
+    done
+    ;;
+d)
+    timeout -k 10 300 python -u - > gpurun_out/r04_pcie_8streams.jsonl <<'PY'
+import sys, os
+sys.path.insert(0, os.getcwd())
+import json, threading, time, ctypes
+import numpy as np
+import fmi_amd
+from fmi_amd import Bucket, PinnedArray, _lib, Stream
+fmi_amd.init(0)
+MIB = 1 << 20
+def run(peers, mib, chunk_mib, duplex=True):
+    n = mib * MIB
+    hs = [PinnedArray(n // 4, np.float32) for _ in range(peers)]
+    ho = [PinnedArray(n // 4, np.float32) for _ in range(peers)]
+    ds = [Bucket(n // 4, np.float32) for _ in range(peers)]
+    st = [(Stream(), Stream()) for _ in range(peers)]
+    bar = threading.Barrier(peers)
+    t = [0.0] * peers
+    def rank(r):
+        bar.wait()
+        t0 = time.perf_counter()
+        c = chunk_mib * MIB
+        for o in range(0, n, c):
+            _lib.call("fmi_dev_h2d_async", ds[r].ptr + o, hs[r].ptr + o, c, st[r][0].handle)
+            if duplex:
+                _lib.call("fmi_dev_d2h_async", ho[r].ptr + o, ds[r].ptr + o, c, st[r][1].handle)
+        _lib.call("fmi_stream_sync", st[r][0].handle)
+        _lib.call("fmi_stream_sync", st[r][1].handle)
+        t[r] = time.perf_counter() - t0
+    for _ in range(2):
+        th = [threading.Thread(target=rank, args=(r,)) for r in range(peers)]
+        [x.start() for x in th]; [x.join() for x in th]
+    ms = max(t) * 1e3
+    for x in hs + ho: x.free()
+    for x in ds: x.free()
+    return {"peers": peers, "mib": mib, "chunk_mib": chunk_mib, "duplex": duplex, "ms": round(ms, 2),
+            "GB_s_total": round((2 if duplex else 1) * peers * n / (ms * 1e-3) / 1e9, 1)}
+for args in [(1, 1024, 64), (8, 1024, 64), (8, 1024, 64, False), (8, 1024, 256)]:
+    print(json.dumps(run(*args)), flush=True)
+PY
+    ;;
 *)
-    echo "usage: bash tools/gpu_round4.sh a|b" >&2
+    echo "usage: bash tools/gpu_round4.sh a|b|c|d" >&2
     exit 2
     ;;
 esac
