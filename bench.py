@@ -236,6 +236,12 @@ def c2_reference(bucket_mib: int, port_combine_ms: float, reps: int = 5) -> dict
         two = fmi_ref.time_combine(2, n, reps, adapter=True)
     except Exception as e:  # reported, never required
         return {"error": f"{type(e).__name__}: {e}"}
+    try:  # the same allreduce with every f.f bound to the product's C-ABI
+        from fmi_amd import _lib
+
+        gpu = fmi_ref.time_allreduce_bound(2, n, reps, fmi_ref.Binding.from_library(_lib.load()))
+    except Exception as e:  # reported, never required
+        gpu = f"{type(e).__name__}: {e}"
     combine = ad - nop
     ratio = one / port_combine_ms
     return {"config": "C2 size", "kind": "reference", "peers": 2, "bucket_mib": bucket_mib, "reps": reps,
@@ -247,6 +253,9 @@ def c2_reference(bucket_mib: int, port_combine_ms: float, reps: int = 5) -> dict
             "reference_adapter_combine_1_thread_ms": round(one, 2),
             "reference_adapter_combine_2_threads_ms": round(two, 2),
             "port_adapter_combine_ms": round(port_combine_ms, 2),
+            "gpu_combine_allreduce_ms": round(gpu, 2) if isinstance(gpu, float) else gpu,
+            "gpu_combine": "the same reference allreduce with every f.f = fmi_host_reduce_pair (its pageable buckets, "
+                           "staged through the GPU); bits: tests/test_gpu_ref_binding.py",
             "reference_over_port": round(ratio, 3), "agrees_within_10pct": bool(abs(ratio - 1) <= 0.10),
             "note": "reference_over_port compares like with like: the reference's adapter combine on one thread "
                     "against the port's (value). Inside the 2-peer allreduce both peers combine at once; "
