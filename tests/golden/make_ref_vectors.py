@@ -30,6 +30,11 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 PEERS = list(range(1, 10)) + [12, 13, 16, 17, 24, 31, 32, 33, 48, 64]
 N = 19  # 16 + a 3-element tail (vector kernels' ragged end); element 0..7 carry edge values
 CASES = [(np.float32, op) for op in ("sum", "prod", "max", "min")] + [(np.float64, "sum"), (np.float64, "max")]
+# round 4: the rest of f64 and the integer types, at fewer peer counts (integer results do not depend on the
+# bracketing, so these pin the element semantics: wrapping sum / prod, std::max / std::min on the extremes)
+EXTRA_CASES = [(np.float64, "prod"), (np.float64, "min")] + [(dt, op) for dt in (np.int32, np.int64)
+                                                             for op in ("sum", "prod", "max", "min")]
+EXTRA_PEERS = [1, 2, 3, 5, 8, 13, 17, 33]
 EXPR_PEERS = range(1, 21)
 
 
@@ -37,6 +42,15 @@ def fixture_inputs(dtype, P, seed):
     """Peer p: the synthetic bucket scaled by 2^((7p mod 13) - 6) (exact), so that sums of peers of different
     magnitudes round differently under different bracketings; elements 0..7 carry the edge values (signed
     zeros, infinities, NaN, subnormals, the largest finite) rotated by peer, which decide max / min order."""
+    if np.issubdtype(dtype, np.integer):  # integers: the full-range synthetic bucket plus the extremes
+        ii = np.iinfo(dtype)
+        edge = np.array([ii.min, ii.max, 0, -1, 1, ii.min + 1, ii.max - 1, 2], dtype=dtype)
+        xs = []
+        for p in range(P):
+            x = orc.synthetic(dtype, N, seed=seed, peer=p)
+            x[:8] = np.roll(edge, p)
+            xs.append(x)
+        return np.stack(xs)
     fi = np.finfo(dtype)
     edge = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, fi.tiny / 4, -fi.max, fi.smallest_subnormal], dtype=dtype)
     xs = []
@@ -56,9 +70,9 @@ def main():
         raise SystemExit(f"{ref.LIB_PATH} missing: make -C oracle (needs /root/reference)")
     out = {}
     with np.errstate(all="ignore"):
-        for dtype, op in CASES:
+        for dtype, op, peers in [(d, o, PEERS) for d, o in CASES] + [(d, o, EXTRA_PEERS) for d, o in EXTRA_CASES]:
             dn = np.dtype(dtype).name
-            for P in PEERS:
+            for P in peers:
                 if dtype == np.float64 and P > 33:
                     continue
                 xs = fixture_inputs(dtype, P, seed=1000 + P)

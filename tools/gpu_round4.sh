@@ -6,6 +6,9 @@
 #   bash tools/gpu_round4.sh b   the default bench line after the C2-size reference baseline's no-op mode was
 #                                fixed, then the C2 profile of the round-4 library (tools/c2_profile.sh:
 #                                kernel trace + stats, separate FETCH_SIZE / WRITE_SIZE passes, an unprofiled line)
+#   bash tools/gpu_round4.sh e   the HIP path against the extended reference fixtures (f64 prod / min, i32 / i64 x
+#                                4 ops), then the default bench line with the GPU-bound reference allreduce at 256 MiB
+#                                (profiles/r04_ref_vectors_gpu.log, r04_e_bench.json)
 #   bash tools/gpu_round4.sh c   C5's local_peers block (8 LOCAL ranks x 1 GiB) at GPU_MAX_HW_QUEUES = 4 / 8 / 16
 #                                (profiles/r04_c5_local_peers_hwq.jsonl)
 #   bash tools/gpu_round4.sh d   the DMA ceiling of that shape: 8 threads, each streaming 1 GiB H2D and 1 GiB D2H
@@ -23,6 +26,11 @@ a)
 b)
     timeout -k 10 600 python bench.py > gpurun_out/r04_b_bench.json 2> gpurun_out/r04_b_bench.err &&
     bash tools/c2_profile.sh
+    ;;
+e)
+    timeout -k 10 600 python -u -m pytest tests/test_gpu_ref_vectors.py -x -q --timeout 300 --timeout-method thread \
+        > gpurun_out/r04_ref_vectors_gpu.log 2>&1 &&
+    timeout -k 10 600 python bench.py > gpurun_out/r04_e_bench.json 2> gpurun_out/r04_e_bench.err
     ;;
 c)
     for q in 4 8 16; do
@@ -77,7 +85,7 @@ for args in [(1, 1024, 64), (8, 1024, 64), (8, 1024, 64, False), (8, 1024, 256)]
 PY
     ;;
 *)
-    echo "usage: bash tools/gpu_round4.sh a|b|c|d" >&2
+    echo "usage: bash tools/gpu_round4.sh a|b|c|d|e" >&2
     exit 2
     ;;
 esac
