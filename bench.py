@@ -334,12 +334,16 @@ WORKLOAD_DIST = "sharded_allreduce"
 def _error_line(world, error, phase, **extra):
     """The one line of a failed N > 1 run: what failed, where, and the runtime it failed on (librccl version and
     path, device visibility), so a first 8-GPU failure is diagnosable from the line alone."""
-    try:
-        from fmi_amd.comm import runtime_info
-
-        runtime = runtime_info()
-    except Exception as e:  # the library itself may be what failed
-        runtime = {"error": f"{type(e).__name__}: {e}"}
+    comm_mod = sys.modules.get("fmi_amd.comm")  # never import from here: this may run on the deadline's thread
+    if comm_mod is None:
+        runtime = {k: os.environ.get(k) for k in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES",
+                                                  "GPU_MAX_HW_QUEUES")}
+        runtime["rccl_error"] = "the library was not loaded yet when the run failed"
+    else:
+        try:
+            runtime = comm_mod.runtime_info()
+        except Exception as e:  # the library itself may be what failed
+            runtime = {"error": f"{type(e).__name__}: {e}"}
     line = {"metric": METRIC, "value": None, "unit": "GiB/s", "n_gpus": world, "workload": WORKLOAD_DIST,
             "higher_is_better": True, "error": error, "phase": phase, "runtime": runtime}
     line.update(extra)
