@@ -734,9 +734,17 @@ int device_copy(void* dst, const void* src, size_t bytes, hipStream_t s) {
     const bool disjoint = d + bytes <= c || c + bytes <= d;
     if (bytes >= kDeviceCopyMin && disjoint && aligned16(dst) && aligned16(src) && device_memory(dst) &&
         device_memory(src)) {
-        constexpr int U = 4;
-        const size_t tiles = (bytes / 16 + U * 256 - 1) / (U * 256);
-        copy_tile<U><<<static_cast<unsigned>(std::max<size_t>(1, tiles)), 256, 0, s>>>(static_cast<char*>(dst), c, bytes);
+        // One 16-B vector per thread: 3.2 % faster than four at 256 MiB and 2 % at 64 MiB, interleaved on the same
+        // buffers with no MALL re-use (profiles/r04_copy_unroll.jsonl); four per thread only where one would
+        // pass HIP's 2^31-thread grid (copies beyond 32 GiB).
+        const size_t nvec = bytes / 16;
+        if (nvec <= (size_t(1) << 31)) {
+            const size_t tiles = (nvec + 255) / 256;
+            copy_tile<1><<<static_cast<unsigned>(std::max<size_t>(1, tiles)), 256, 0, s>>>(static_cast<char*>(dst), c, bytes);
+        } else {
+            const size_t tiles = (nvec + 4 * 256 - 1) / (4 * 256);
+            copy_tile<4><<<static_cast<unsigned>(tiles), 256, 0, s>>>(static_cast<char*>(dst), c, bytes);
+        }
         FMI_HIP_TRY(hipGetLastError());
         return FMI_OK;
     }

@@ -214,8 +214,8 @@ __device__ __forceinline__ void store_tile(void* bucket, size_t tile_byte, unsig
 }
 
 // Device copy (device_copy in fmi_dev.hip: the reference's P = 1 allreduce and every staging copy of the
-// communicator): the pair tile's shape with one stream in and one out — U 16-B vectors per thread, one tile
-// per workgroup. Whole tiles load nontemporal and store with sc1 through a buffer descriptor (the tree kernel's
+// communicator): the pair tile's shape with one stream in and one out — U 16-B vectors per thread (U = 1 in
+// the library, profiles/r04_copy_unroll.jsonl), one tile per workgroup. Whole tiles load nontemporal and store with sc1 through a buffer descriptor (the tree kernel's
 // policy, above): 4.6 % faster than global nontemporal stores at 256 MiB, 3 % at 64 MiB, with no set
 // re-read from the MALL (profiles/archive/r03_copypol.jsonl). The partial last tile
 // goes through bounds-checked global accesses; workgroup 0 copies the sub-16-B tail. Algorithmic HBM bytes:
