@@ -3,7 +3,9 @@
 #include <algorithm>
 #include <atomic>
 #include <cstring>
+#include <memory>
 #include <mutex>
+#include <shared_mutex>
 #include <string>
 #include <vector>
 
@@ -21,10 +23,6 @@ struct DeviceState {
     size_t lds_per_cu = 160 * 1024;  // gfx950
     size_t lds_per_wg = 160 * 1024;
     hipStream_t stream = nullptr;
-    // host-ingress pipeline scratch (fmi_host_reduce_pair): two slots of (a, b) staging + two streams
-    void* stage[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
-    size_t stage_bytes = 0;
-    hipStream_t pipe[2] = {nullptr, nullptr};
     // scratch arena for the pairwise-pass execution of P-way programs; arena_free marks when the work
     // that last used it has drained (the next user's stream waits on it)
     void* arena = nullptr;
@@ -34,6 +32,44 @@ struct DeviceState {
 
 std::mutex g_mu;
 DeviceState g_state;  // one process drives one device (one process per GPU, as FMI runs one peer per process)
+
+// Host-ingress pipeline of fmi_host_reduce_pair: two slots of (a, b) device staging and two streams, one set PER
+// CALLING THREAD. The reference's peers combine concurrently when they are threads of one process (its
+// allreduce's peers each call f.f at once), and one shared pipeline serialised them: 2 / 4 threads took exactly
+// 2 / 4 x one combine (profiles/r04_host_pair_threads.jsonl). Every set is registered so that
+// fmi_dev_finalize frees them all; a thread's cached pointer is trusted only for the generation it was made in.
+struct HostPipe {
+    int device = -1;
+    void* stage[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
+    size_t stage_bytes = 0;
+    hipStream_t pipe[2] = {nullptr, nullptr};
+    void release() {
+        for (int k = 0; k < 2; ++k) {
+            if (pipe[k]) (void)hipStreamSynchronize(pipe[k]);
+            for (int j = 0; j < 2; ++j)
+                if (stage[k][j]) (void)hipFree(stage[k][j]);
+            if (pipe[k]) (void)hipStreamDestroy(pipe[k]);
+        }
+        *this = HostPipe{};
+    }
+};
+std::mutex g_pipes_mu;
+std::shared_mutex g_pipes_life;  // shared by every fmi_host_reduce_pair in flight, exclusive in fmi_dev_finalize
+std::vector<std::unique_ptr<HostPipe>> g_pipes;
+std::atomic<uint64_t> g_pipes_gen{1};
+thread_local HostPipe* t_pipe = nullptr;
+thread_local uint64_t t_pipe_gen = 0;
+
+HostPipe* my_host_pipe() {
+    const uint64_t gen = g_pipes_gen.load();
+    if (t_pipe && t_pipe_gen == gen && t_pipe->device == g_state.device) return t_pipe;
+    std::lock_guard<std::mutex> lk(g_pipes_mu);
+    g_pipes.push_back(std::make_unique<HostPipe>());
+    t_pipe = g_pipes.back().get();
+    t_pipe->device = g_state.device;
+    t_pipe_gen = gen;
+    return t_pipe;
+}
 
 // Defaults from tools/tune_pair.py on MI355X (C2, 256 MiB f32): nontemporal one-shot tiles, 4 × 16 B per
 // operand per thread, 256-thread workgroups — 125 µs = 6.4 TB/s vs 142 µs for plain loads/stores.
@@ -818,10 +854,12 @@ int fmi_dev_finalize(void) {
     if (g_state.device < 0) return FMI_OK;
     (void)hipSetDevice(g_state.device);
     (void)hipDeviceSynchronize();
-    for (int k = 0; k < 2; ++k) {
-        for (int j = 0; j < 2; ++j)
-            if (g_state.stage[k][j]) (void)hipFree(g_state.stage[k][j]);
-        if (g_state.pipe[k]) (void)hipStreamDestroy(g_state.pipe[k]);
+    {
+        std::unique_lock<std::shared_mutex> life(g_pipes_life);
+        std::lock_guard<std::mutex> lk(g_pipes_mu);
+        for (auto& p : g_pipes) p->release();
+        g_pipes.clear();
+        g_pipes_gen.fetch_add(1);
     }
     if (g_state.arena) (void)hipFree(g_state.arena);
     if (g_state.arena_free) (void)hipEventDestroy(g_state.arena_free);
@@ -1205,59 +1243,61 @@ int fmi_host_reduce_pair(int op, int dtype, void* inout, const void* in, size_t 
             return fail(FMI_ERR_INVALID, "fmi_host_reduce_pair: a bucket straddles the end of a page-locked range "
                                          "(pin or register the whole bucket, or none of it)");
     }
+    std::shared_lock<std::shared_mutex> life(g_pipes_life);
+    HostPipe& hp = *my_host_pipe();  // this thread's streams and staging: concurrent callers do not serialise
+    for (int k = 0; k < 2; ++k)
+        if (!hp.pipe[k]) FMI_HIP_TRY(hipStreamCreateWithFlags(&hp.pipe[k], hipStreamNonBlocking));
     if (g_tune[FMI_TUNE_HOST_ZERO_COPY].load()) {
         // Page-locked buckets: the kernel streams them straight over PCIe (reads of both operands and the
         // write-back share the link concurrently, no staging copies, no DMA-engine serialisation).
         void* dx = nullptr;
         void* dy = nullptr;
         if (host_mapped(inout, n * esz, &dx) && host_mapped(const_cast<void*>(in), n * esz, &dy)) {
-            hipStream_t s = g_state.stream;
+            hipStream_t s = hp.pipe[0];
             int rc = launch_combine(op, dtype, dx, dx, dy, n, s);
             if (rc != FMI_OK) return rc;
             FMI_HIP_TRY(hipStreamSynchronize(s));
             return FMI_OK;
         }
     }
-    std::lock_guard<std::mutex> lk(g_mu);
     size_t chunk_elems = static_cast<size_t>(std::max<long long>(g_tune[FMI_TUNE_HOST_CHUNK].load(), 1 << 16)) / esz;
     chunk_elems = std::max<size_t>(16, chunk_elems / 16 * 16);
     const size_t chunk_bytes = chunk_elems * esz;
-    if (g_state.stage_bytes < chunk_bytes) {
+    if (hp.stage_bytes < chunk_bytes) {
+        for (int k = 0; k < 2; ++k) FMI_HIP_TRY(hipStreamSynchronize(hp.pipe[k]));
         for (int k = 0; k < 2; ++k)
             for (int j = 0; j < 2; ++j) {
-                if (g_state.stage[k][j]) FMI_HIP_TRY(hipFree(g_state.stage[k][j]));
-                g_state.stage[k][j] = nullptr;
+                if (hp.stage[k][j]) FMI_HIP_TRY(hipFree(hp.stage[k][j]));
+                hp.stage[k][j] = nullptr;
             }
         for (int k = 0; k < 2; ++k)
             for (int j = 0; j < 2; ++j) {
-                const hipError_t e = hipMalloc(&g_state.stage[k][j], chunk_bytes);
+                const hipError_t e = hipMalloc(&hp.stage[k][j], chunk_bytes);
                 if (e != hipSuccess) {
-                    g_state.stage_bytes = 0;
+                    hp.stage_bytes = 0;
                     return fail(FMI_ERR_ALLOC, std::string("hipMalloc (host pipeline staging): ") + hipGetErrorString(e));
                 }
             }
-        g_state.stage_bytes = chunk_bytes;
+        hp.stage_bytes = chunk_bytes;
     }
-    for (int k = 0; k < 2; ++k)
-        if (!g_state.pipe[k]) FMI_HIP_TRY(hipStreamCreateWithFlags(&g_state.pipe[k], hipStreamNonBlocking));
     char* hx = static_cast<char*>(inout);
     const char* hy = static_cast<const char*>(in);
     int rc = FMI_OK;
     size_t chunk = 0;
     for (size_t off = 0; off < n && rc == FMI_OK; off += chunk_elems, ++chunk) {
         const int slot = static_cast<int>(chunk & 1);
-        hipStream_t s = g_state.pipe[slot];
+        hipStream_t s = hp.pipe[slot];
         const size_t cnt = std::min(chunk_elems, n - off);
         const size_t bytes = cnt * esz;
-        void* da = g_state.stage[slot][0];
-        void* db = g_state.stage[slot][1];
+        void* da = hp.stage[slot][0];
+        void* db = hp.stage[slot][1];
         FMI_HIP_TRY(hipMemcpyAsync(da, hx + off * esz, bytes, hipMemcpyHostToDevice, s));
         FMI_HIP_TRY(hipMemcpyAsync(db, hy + off * esz, bytes, hipMemcpyHostToDevice, s));
         rc = launch_combine(op, dtype, da, da, db, cnt, s);
         if (rc != FMI_OK) break;
         FMI_HIP_TRY(hipMemcpyAsync(hx + off * esz, da, bytes, hipMemcpyDeviceToHost, s));
     }
-    for (int k = 0; k < 2; ++k) FMI_HIP_TRY(hipStreamSynchronize(g_state.pipe[k]));
+    for (int k = 0; k < 2; ++k) FMI_HIP_TRY(hipStreamSynchronize(hp.pipe[k]));
     return rc;
 }
 

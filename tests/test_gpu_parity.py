@@ -696,6 +696,103 @@ def test_host_reduce_pair_pinned(device, zero_copy, n):
         fmi_amd.tune_set(Tune.HOST_ZERO_COPY, old)
 
 
+_CONCURRENT_CASES = [(np.float32, Op.SUM, (1 << 20) + 7), (np.int64, Op.MIN, 4099), (np.float64, Op.PROD, 1 << 18),
+                     (np.int32, Op.MAX, (1 << 19) + 1), (np.float32, Op.MAX, 33), (np.float64, Op.SUM, (1 << 20) + 3)]
+
+
+def _host_pair_rounds(t, rounds, errors, start=None):
+    """Thread t's share of the concurrency test: `rounds` combines of its case, pinned buckets for odd t."""
+    from fmi_amd.device import PinnedArray
+
+    dtype, op, n = _CONCURRENT_CASES[t]
+    try:
+        if start is not None:
+            start.wait()
+        for r in range(rounds):
+            a, b = inputs(dtype, n, 10 * t + r), inputs(dtype, n, 10 * t + r + 1)
+            if t % 2:
+                pa, pb = PinnedArray(n, dtype), PinnedArray(n, dtype)
+                pa.array[:] = a
+                pb.array[:] = b
+                fmi_amd.host_reduce_pair(op, pa.array, pb.array)
+                got = pa.array.copy()
+                pa.free()
+                pb.free()
+            else:
+                got = a.copy()
+                fmi_amd.host_reduce_pair(op, got, b)
+            with np.errstate(all="ignore"):
+                want = orc.pairwise(OPNAME[op], a, b)
+            if got.tobytes() != want.tobytes():
+                errors.append(f"thread {t} round {r}: {op.name} {np.dtype(dtype).name} n={n}")
+    except Exception as e:  # noqa: BLE001 - reported by the caller
+        errors.append(f"thread {t}: {e!r}")
+
+
+def host_pair_concurrently(rounds=3):
+    """All of _CONCURRENT_CASES at once, one thread each; returns the list of failures."""
+    import threading
+
+    errors = []
+    start = threading.Barrier(len(_CONCURRENT_CASES))
+    threads = [threading.Thread(target=_host_pair_rounds, args=(t, rounds, errors, start))
+               for t in range(len(_CONCURRENT_CASES))]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join(timeout=120)
+    if any(th.is_alive() for th in threads):
+        errors.append("a host_reduce_pair caller did not finish")
+    return errors
+
+
+@pytest.mark.parametrize("zero_copy", [0, 1])
+def test_host_reduce_pair_concurrent_threads(device, zero_copy):
+    """Each calling thread has its own staging and streams (the reference's peers combine concurrently when
+    they are threads of one process): 6 threads x 3 rounds of mixed ops / dtypes / sizes, pageable and
+    pinned buckets, many pipeline chunks per call, every result bit-exact."""
+    old = (fmi_amd.tune_get(Tune.HOST_CHUNK), fmi_amd.tune_get(Tune.HOST_ZERO_COPY))
+    try:
+        fmi_amd.tune_set(Tune.HOST_CHUNK, 1 << 16)
+        fmi_amd.tune_set(Tune.HOST_ZERO_COPY, zero_copy)
+        errors = host_pair_concurrently()
+        assert not errors, errors
+    finally:
+        fmi_amd.tune_set(Tune.HOST_CHUNK, old[0])
+        fmi_amd.tune_set(Tune.HOST_ZERO_COPY, old[1])
+
+
+_REINIT_SCRIPT = """
+import sys
+sys.path.insert(0, {root!r})
+import fmi_amd
+from fmi_amd import Tune
+from tests import test_gpu_parity as t
+for phase in range(3):
+    fmi_amd.init(0)
+    fmi_amd.tune_set(Tune.HOST_CHUNK, 1 << 16)
+    errors = []
+    t._host_pair_rounds(0, 2, errors)  # the main thread's pipeline: made, then rebuilt after every re-init
+    errors += t.host_pair_concurrently(rounds=2)
+    assert not errors, (phase, errors)
+    fmi_amd.finalize()
+print("ok")
+"""
+
+
+def test_host_reduce_pair_pipelines_survive_reinit(device):
+    """fmi_dev_finalize frees every thread's pipeline; a thread that combined before it gets a fresh one after
+    fmi_dev_init (its cached pointer belongs to the old generation). In a child process, so the session's
+    device state is left alone."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", _REINIT_SCRIPT.format(root=root)], capture_output=True, text=True,
+                       timeout=240, cwd=root)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout[-2000:] + r.stderr[-4000:]
+
+
 def _page_aligned(n, dtype):
     """A contiguous numpy array of n elements starting on a 4 KiB boundary."""
     item = np.dtype(dtype).itemsize

@@ -9,6 +9,8 @@
 #   bash tools/gpu_round4.sh e   the HIP path against the extended reference fixtures (f64 prod / min, i32 / i64 x
 #                                4 ops), then the default bench line with the GPU-bound reference allreduce at 256 MiB
 #                                (profiles/r04_ref_vectors_gpu.log, r04_e_bench.json)
+#   bash tools/gpu_round4.sh f [tag]  fmi_host_reduce_pair on pageable 256 MiB pairs from 1, 2 and 4 threads at once (the
+#                                reference binding's peers combine concurrently; profiles/r04_host_pair_threads*.jsonl)
 #   bash tools/gpu_round4.sh c   C5's local_peers block (8 LOCAL ranks x 1 GiB) at GPU_MAX_HW_QUEUES = 4 / 8 / 16
 #                                (profiles/r04_c5_local_peers_hwq.jsonl)
 #   bash tools/gpu_round4.sh d   the DMA ceiling of that shape: 8 threads, each streaming 1 GiB H2D and 1 GiB D2H
@@ -26,6 +28,41 @@ a)
 b)
     timeout -k 10 600 python bench.py > gpurun_out/r04_b_bench.json 2> gpurun_out/r04_b_bench.err &&
     bash tools/c2_profile.sh
+    ;;
+f)
+    timeout -k 10 300 python -u - > "gpurun_out/r04_host_pair_threads${2:+_$2}.jsonl" <<'PY'
+import json, threading, time, sys, os
+sys.path.insert(0, os.getcwd())
+import numpy as np
+import fmi_amd
+from fmi_amd import Op
+fmi_amd.init(0)
+n = (256 << 20) // 4
+def run(threads, reps=4):
+    pairs = [(np.random.default_rng(t).random(n, dtype=np.float32), np.random.default_rng(100 + t).random(n, dtype=np.float32)) for t in range(threads)]
+    want = []
+    for a, b in pairs:  # the result after `reps` in-place sums, in the same order
+        w = a.copy()
+        for _ in range(reps):
+            w += b
+        want.append(w)
+    bar = threading.Barrier(threads)
+    times = [[0.0] * reps for _ in range(threads)]
+    def body(t):
+        a, b = pairs[t]
+        for r in range(reps):
+            bar.wait()
+            t0 = time.perf_counter()
+            fmi_amd.host_reduce_pair(Op.SUM, a, b)
+            times[t][r] = time.perf_counter() - t0
+    th = [threading.Thread(target=body, args=(t,)) for t in range(threads)]
+    [x.start() for x in th]; [x.join() for x in th]
+    per = sorted(max(times[t][r] for t in range(threads)) for r in range(1, reps))
+    exact = all(np.array_equal(pairs[t][0], want[t]) for t in range(threads))
+    return {"threads": threads, "pageable_256MiB_pairs": threads, "ms": round(per[len(per) // 2] * 1e3, 2), "bit_exact": exact}
+for k in (1, 2, 4):
+    print(json.dumps(run(k)), flush=True)
+PY
     ;;
 e)
     timeout -k 10 600 python -u -m pytest tests/test_gpu_ref_vectors.py -x -q --timeout 300 --timeout-method thread \
@@ -85,7 +122,7 @@ for args in [(1, 1024, 64), (8, 1024, 64), (8, 1024, 64, False), (8, 1024, 256)]
 PY
     ;;
 *)
-    echo "usage: bash tools/gpu_round4.sh a|b|c|d|e" >&2
+    echo "usage: bash tools/gpu_round4.sh a|b|c|d|e|f" >&2
     exit 2
     ;;
 esac
