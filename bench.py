@@ -1027,8 +1027,25 @@ def run_dist(args, world, rank, local_rank):
     one_rank_exchange = args.force_dist and world == 1
     if one_rank_exchange:  # the plumbing check runs the real exchange (RCCL calls with itself), not the P = 1 copy
         fmi_amd.tune_set(fmi_amd.Tune.COMM_ONE_RANK_EXCHANGE, 1)
-    watch.enter("fmi_comm init (communicator id broadcast, RCCL init)")
-    ar = CommAllreduce(dist.group.WORLD, path=args.path, transport=args.transport)
+    if proc:  # gloo cannot carry the device exchange: no fallback, a failure is the error line
+        watch.enter("fmi_comm init (communicator id broadcast, PROC init)")
+        ar = CommAllreduce(dist.group.WORLD, path=args.path, transport=args.transport)
+    else:
+        ar, comm_err = None, None
+        try:
+            watch.enter("fmi_comm init (communicator id broadcast, RCCL init)")  # (its test hook raises here)
+            ar = CommAllreduce(dist.group.WORLD, path=args.path, transport=args.transport)
+        except Exception as e:  # every rank reaches the agreement below, whether its own init raised or not
+            comm_err = f"{type(e).__name__}: {e}"
+            print(f"bench: rank {rank}: fmi_comm init failed: {comm_err}", file=sys.stderr, flush=True)
+        watch.enter("agreement on the fmi_comm init")
+        failed = torch.tensor([0 if comm_err is None else 1], dtype=torch.int32, device=torch.device("cuda", dev))
+        dist.all_reduce(failed, op=dist.ReduceOp.MAX)
+        if int(failed.item()):
+            if ar is not None:
+                ar.destroy()
+            run_dist_torch_exchange(args, world, rank, watch, comm_err or "fmi_comm init failed on another rank", numa)
+            return
     watch.enter("topology check")
     topo = ar.topology()
     if not topo["ok"]:  # RCCL did not see `world` ranks, or two ranks share a GPU: the line would be wrong
@@ -1099,6 +1116,111 @@ def run_dist(args, world, rank, local_rank):
     dist.barrier()
     dist.destroy_process_group()
     watchdog.cancel()
+    if not check["ok"]:
+        print("bench: self-check FAILED: the sharded allreduce differs from the single-GPU kernel", file=sys.stderr,
+              flush=True)
+        sys.exit(1)
+
+
+def run_dist_torch_exchange(args, world, rank, watch, comm_err, numa):
+    """The N > 1 line when the product communicator (fmi_comm over RCCL) cannot be built on this node: the same
+    workload — one f32 256 MiB bucket per GPU, sharded sum-allreduce, the fused tree kernel of libfmi_dev.so in the
+    reference's bracketing on every shard — with the two exchanges carried by torch.distributed's own RCCL
+    process group (all_to_all_single + all_gather_into_tensor, fmi_amd.collectives.ShardedAllreduce path "tree").
+    Same bytes, same result bits (self-checked the same way); the line says why (`config.exchange_fallback`).
+    C4 / C5 and the diagnostics need fmi_comm and are not run."""
+    import torch
+    import torch.distributed as dist
+
+    from fmi_amd import Alg, Op
+    from fmi_amd import device as fdev
+    from fmi_amd.collectives import ShardedAllreduce, check_windows, local_equivalent
+    from fmi_amd.comm import runtime_info
+
+    print(f"bench: rank {rank}: falling back to torch.distributed's exchange ({comm_err})", file=sys.stderr, flush=True)
+    watch.enter("fallback topology check")
+    dev = torch.cuda.current_device()
+    mine = {"rank": rank, "torch_device": dev, "pci_bus_id": fdev.pci_bus_id(dev), "runtime": runtime_info()}
+    every = [None] * world
+    dist.all_gather_object(every, mine)
+    buses = [e["pci_bus_id"] for e in every]
+    topo = {"ok": len(set(buses)) == world, "ranks": world, "distinct_gpus": len(set(buses)) == world,
+            "pci_bus_ids": buses, "runtime": every[0]["runtime"], "source": "torch.distributed all_gather_object"}
+    if not topo["ok"]:
+        print("bench: topology check FAILED: " + json.dumps(topo), file=sys.stderr, flush=True)
+        if rank == 0:
+            print(json.dumps(_error_line(world, "topology check failed", "fallback topology check", topology=topo,
+                                         fmi_comm_error=comm_err)), file=json_out(), flush=True)
+        os._exit(1)
+    n = args.bucket_mib * MIB // 4
+    S = n * 4
+    sar = ShardedAllreduce(dist.group.WORLD, path="tree", force_exchange=world == 1)
+    watch.enter("fallback warm-up and timed allreduces")
+    step_ms, _, extra = sar.bench(n, steps=args.steps, warmup=args.warmup, sets=args.dist_sets, peers_per_gpu=1,
+                                  return_result=True)
+    out, seed = extra.pop("result")
+    value = world * (S / GIB) / (step_ms * 1e-3)
+    watch.enter("fallback self-check")
+    torch.cuda.synchronize()
+    check = check_windows(world, rank, sar.shard_elems(n), n, seed, lambda st, w: out[st:st + w].cpu().numpy(),
+                          sar.max_over_ranks)
+    del out
+    watch.enter("fallback shard-kernel timing")
+    shard = sar.shard_elems(n)
+    parts = [[torch.empty(shard, dtype=torch.float32, device=sar.engine.device) for _ in range(world)] for _ in range(2)]
+    for s_, ps in enumerate(parts):
+        for p, t in enumerate(ps):
+            sar.engine.fill_synthetic(t, 42 + s_, p)
+    red = torch.empty(shard, dtype=torch.float32, device=sar.engine.device)
+    launches = max(10, min(args.steps, 50))
+    for k in range(2):
+        sar.engine.reduce_tree(Op.SUM, Alg.ALLREDUCE, red, parts[k % 2])
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()  # torch's current stream: the one HipEngine launches on
+    for k in range(launches):
+        sar.engine.reduce_tree(Op.SUM, Alg.ALLREDUCE, red, parts[k % 2])
+    e1.record()
+    e1.synchronize()
+    shard_ms = sar.max_over_ranks(e0.elapsed_time(e1) / launches)[0]
+    del parts, red
+    watch.done()
+    roof = _roofline("tree_kernel", (world + 1) * shard * 4, shard_ms,
+                     "torch.cuda.Event around back-to-back launches of the shard kernel on torch's current stream (the "
+                     "stream HipEngine launches on) after the timed region, max over ranks",
+                     {"note": "the allreduce step is xGMI-bound (xgmi_roofline); this is its HBM-bound kernel"},
+                     pmc_key=f"tree_kernel<fmi::dev::OpSum, float, 0, {world}, false>")
+    line = _headline(args, value, step_ms,
+                     f"C4-shaped at the metric's bucket size: {world}-peer float32 sum-allreduce, one FMI peer "
+                     f"(a {args.bucket_mib} MiB device-resident bucket) per GPU",
+                     f"{world} GPUs, one peer per GPU, buckets sharded {world} ways; all-to-all + fused tree kernel "
+                     f"+ all-gather (bit-exact), exchanges through torch.distributed (RCCL)", n, roof)
+    line["config"]["topology"] = topo
+    line["config"].update({"rotating_sets": args.dist_sets, "numa_binding_rank0": numa, "peers": world,
+                           "path": "tree", "transport": "torch.distributed (nccl backend = RCCL)",
+                           "algbw_GiB_s": extra["algbw_GiB_s"], "busbw_GiB_s": extra["busbw_GiB_s"],
+                           "shard_elems": shard})
+    line["config"]["exchange_fallback"] = {
+        "reason": comm_err,
+        "exchange": "torch.distributed all_to_all_single + all_gather_into_tensor on torch's RCCL process group "
+                    "(fmi_amd.collectives.ShardedAllreduce); the shard kernel is libfmi_dev.so's fused tree kernel"}
+    line["self_check"] = check
+    if world > 1:
+        egress = 2 * (world - 1) * S / world
+        xg = egress / (step_ms * 1e-3) / 1e9
+        xpeak = (world - 1) * XGMI_LINK_GBS_PER_DIR
+        line["xgmi_roofline"] = {"bound": "xgmi", "achieved": round(xg, 1), "peak": round(xpeak, 1), "unit": "GB/s",
+                                 "frac": round(xg / xpeak, 4), "bytes_per_step_per_gpu": int(egress)}
+    if rank == 0:
+        try:
+            le = local_equivalent(world, n)
+            le["value_over_local"] = round(line["value"] / le["GiB_s_reduced_buckets"], 4)
+            line["local_equivalent"] = le
+        except Exception as e:  # reported; the line is still printed
+            line["local_equivalent"] = {"error": f"{type(e).__name__}: {e}"}
+    line["c4"] = line["c5"] = "not run (needs the fmi_comm communicator)"
+    _Emitter(line, rank).emit()
+    dist.barrier()
+    dist.destroy_process_group()
     if not check["ok"]:
         print("bench: self-check FAILED: the sharded allreduce differs from the single-GPU kernel", file=sys.stderr,
               flush=True)

@@ -166,14 +166,18 @@ class ShardedAllreduce:
         return out
 
     # ------------------------------------------------------------------------------------------------
-    def bench(self, n: int, steps: int, warmup: int, sets: int = 2, peers_per_gpu: int = 2):
-        return self._bench(n, steps, warmup, sets, peers_per_gpu)
+    def bench(self, n: int, steps: int, warmup: int, sets: int = 2, peers_per_gpu: int = 2,
+              return_result: bool = False):
+        return self._bench(n, steps, warmup, sets, peers_per_gpu, return_result)
 
-    def _bench(self, n: int, steps: int, warmup: int, sets: int = 2, peers_per_gpu: int = 2):
+    def _bench(self, n: int, steps: int, warmup: int, sets: int = 2, peers_per_gpu: int = 2,
+               return_result: bool = False):
         """Timed loop for bench.py: returns (ms_per_step max over ranks, per-step local-kernel ms, extras).
 
         Exactly `steps` steps are timed, bracketed by barrier + device sync on both sides; the step time
         is the max over ranks. The local pairwise kernel is also timed on the stream it runs on.
+        return_result (one peer per GPU only: its bucket is never modified): extras["result"] = (out tensor,
+        synthetic seed of the last step's set), for check_windows.
         """
         import time
 
@@ -228,7 +232,114 @@ class ShardedAllreduce:
             "algbw_GiB_s": round((n * 4 / 2 ** 30) / (step_ms * 1e-3), 2),
             "busbw_GiB_s": round((n * 4 / 2 ** 30) / (step_ms * 1e-3) * 2 * (self.world - 1) / self.world, 2),
         }
+        if return_result and peers_per_gpu == 1 and steps > 0:
+            extra["result"] = (out, 42 + (steps - 1) % sets)
         return step_ms, kernel_ms, extra
+
+    def max_over_ranks(self, *vals: float) -> List[float]:
+        dev = (torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(self.group) == "nccl"
+               else torch.device("cpu"))
+        t = torch.tensor(vals, dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        return [float(v) for v in t.tolist()]
+
+
+def check_windows(world: int, rank: int, shard: int, n: int, seed: int, window, max_over_ranks,
+                  width: int = 4096, tolerance: bool = False) -> dict:
+    """Check a one-peer-per-GPU f32 sum allreduce result on sampled windows, on every rank: for each window
+    (the head, the tail and a random interior range of every shard) this rank regenerates every peer's
+    synthetic bucket over that range (fmi_dev_fill_synthetic_at) and reduces them on its own GPU with the
+    single-GPU fused kernel in allreduce_no_order order for its own rank (fmi_dev_reduce_tree). The sharded
+    result (`window(start, count)` -> numpy) must equal it bit for bit (tolerance=False: the reference's
+    bracketing) or lie within (N-1)·2^-24·Σ|x_p| of it (tolerance=True: RCCL's order). Returns the counts, max
+    over ranks; "ok" is the verdict every rank agrees on."""
+    import sys
+
+    import numpy as np
+
+    from . import device as fdev
+
+    N, r = world, rank
+    rng = np.random.default_rng(977 + r)
+    starts = set()
+    for j in range(N):
+        lo = j * shard
+        if lo >= n:
+            break
+        hi = min(n, lo + shard)
+        starts.update({lo, max(lo, hi - width), int(rng.integers(lo, max(lo + 1, hi - width)))})
+    peers = [fdev.Bucket(width, np.float32) for _ in range(N)]
+    ref = fdev.Bucket(width, np.float32)
+    mismatches = checked = 0
+    worst = 0.0
+    for st in sorted(starts):
+        w = min(width, n - st)
+        pv = [p.view(0, w) for p in peers]
+        for p in range(N):
+            pv[p].fill_synthetic(seed, p, first=st)
+        rv = ref.view(0, w)
+        fdev.reduce_tree(Op.SUM, Alg.ALLREDUCE, rv, pv, rank=r)
+        got, want = window(st, w), rv.numpy()
+        if tolerance:
+            xs = np.stack([v.numpy() for v in pv]).astype(np.float64)
+            bound = (N - 1) * 2.0 ** -24 * np.abs(xs).sum(axis=0)
+            err = np.abs(got.astype(np.float64) - want.astype(np.float64))
+            mismatches += int(np.count_nonzero(err > bound))
+            worst = max(worst, float(np.max(err / np.maximum(bound, 1e-300))) if w else 0.0)
+        else:
+            bad = np.nonzero(got.view(np.uint32) != want.view(np.uint32))[0]
+            if bad.size and mismatches == 0:  # where it went wrong, for the log (the line carries counts)
+                i = int(bad[0])
+                print(f"self_check rank {r}: first mismatch at element {st + i}: got {got[i]!r} want {want[i]!r} "
+                      f"(shard {(st + i) // shard} of {N})", file=sys.stderr, flush=True)
+            mismatches += int(bad.size)
+        checked += w
+    for b in peers + [ref]:
+        b.free()
+    mism, chk = max_over_ranks(float(mismatches), float(checked))
+    res = {"ok": mism == 0, "mismatches": int(mism), "elements_checked_per_rank": int(chk),
+           "windows_per_rank": len(starts),
+           "against": ("single-GPU fused reduce_tree (allreduce_no_order order, own rank) of the same "
+                       "synthetic buckets rebuilt on this GPU, " +
+                       ("within (N-1)*2^-24*sum|x|" if tolerance else "bit-exact"))}
+    if tolerance:
+        res["max_err_over_bound"] = round(max_over_ranks(worst)[0], 4)
+    return res
+
+
+def local_equivalent(world: int, n: int, launches: int = 10, sets: int = 2) -> dict:
+    """The like-for-like single-GPU anchor of the N > 1 line: the same world-peer f32 sum-allreduce of
+    n-element buckets computed on ONE GPU (this rank's) by the fused kernel (fmi_dev_reduce_tree,
+    allreduce_no_order order, every bucket resident in this GPU's HBM): HBM-bound, (N + 1)·S algorithmic
+    bytes per launch. `GiB_s_reduced_buckets` = N·S / t, the unit of the line's `value`. Rotating sets;
+    mean of back-to-back launches on the library stream (HIP events)."""
+    import numpy as np
+
+    from . import device as fdev
+
+    N = world
+    ins = [[fdev.Bucket(n, np.float32).fill_synthetic(42 + s, p) for p in range(N)] for s in range(sets)]
+    out = fdev.Bucket(n, np.float32)
+    for s in range(sets):
+        fdev.reduce_tree(Op.SUM, Alg.ALLREDUCE, out, ins[s])
+    fdev.sync()
+    e0, e1 = fdev.Event(), fdev.Event()
+    e0.record()
+    for k in range(launches):
+        fdev.reduce_tree(Op.SUM, Alg.ALLREDUCE, out, ins[k % sets])
+    e1.record()
+    e1.sync()
+    ms = e0.elapsed_ms(e1) / launches
+    e0.destroy()
+    e1.destroy()
+    for b in [out] + [x for s in ins for x in s]:
+        b.free()
+    S = n * 4
+    return {"workload": f"{N} peers x {S >> 20} MiB f32 sum-allreduce on ONE GPU (fused {N}-way kernel, "
+                        f"fmi_dev_reduce_tree): what the N-GPU step computes, without the exchange",
+            "ms": round(ms, 4), "GiB_s_reduced_buckets": round(N * S / 2 ** 30 / (ms * 1e-3), 2),
+            "hbm_frac": round((N + 1) * S / (ms * 1e-3) / 8e12, 4) if N > 1 else None,
+            "launches": launches, "rotating_sets": sets}
 
 
 class CommAllreduce:
@@ -279,38 +390,8 @@ class CommAllreduce:
         return judge_topology(every, self.world, self.transport)
 
     def local_equivalent(self, n: int, launches: int = 10, sets: int = 2) -> dict:
-        """The like-for-like single-GPU anchor of the N > 1 line: the same world-peer f32 sum-allreduce of
-        n-element buckets computed on ONE GPU (this rank's) by the fused kernel (fmi_dev_reduce_tree,
-        allreduce_no_order order, every bucket resident in this GPU's HBM): HBM-bound, (N + 1)·S algorithmic
-        bytes per launch. `GiB_s_reduced_buckets` = N·S / t, the unit of the line's `value`. Rotating sets;
-        mean of back-to-back launches on the library stream (HIP events)."""
-        import numpy as np
-
-        from . import device as fdev
-
-        N = self.world
-        ins = [[fdev.Bucket(n, np.float32).fill_synthetic(42 + s, p) for p in range(N)] for s in range(sets)]
-        out = fdev.Bucket(n, np.float32)
-        for s in range(sets):
-            fdev.reduce_tree(Op.SUM, Alg.ALLREDUCE, out, ins[s])
-        fdev.sync()
-        e0, e1 = fdev.Event(), fdev.Event()
-        e0.record()
-        for k in range(launches):
-            fdev.reduce_tree(Op.SUM, Alg.ALLREDUCE, out, ins[k % sets])
-        e1.record()
-        e1.sync()
-        ms = e0.elapsed_ms(e1) / launches
-        e0.destroy()
-        e1.destroy()
-        for b in [out] + [x for s in ins for x in s]:
-            b.free()
-        S = n * 4
-        return {"workload": f"{N} peers x {S >> 20} MiB f32 sum-allreduce on ONE GPU (fused {N}-way kernel, "
-                            f"fmi_dev_reduce_tree): what the N-GPU step computes, without the exchange",
-                "ms": round(ms, 4), "GiB_s_reduced_buckets": round(N * S / 2 ** 30 / (ms * 1e-3), 2),
-                "hbm_frac": round((N + 1) * S / (ms * 1e-3) / 8e12, 4) if N > 1 else None,
-                "launches": launches, "rotating_sets": sets}
+        """local_equivalent() for this communicator's world size."""
+        return local_equivalent(self.world, n, launches, sets)
 
     def max_over_ranks(self, *vals: float) -> List[float]:
         t = torch.tensor(vals, dtype=torch.float64, device=self._red_dev)
@@ -428,66 +509,9 @@ class CommAllreduce:
         return step_ms, kernel_ms, extra
 
     def self_check(self, out, n: int, seed: int, width: int = 4096, tolerance: bool = False) -> dict:
-        """Check a one-peer-per-GPU f32 sum allreduce result on sampled windows, on every rank: for each
-        window (the head, the tail and a random interior range of every shard) this rank regenerates every
-        peer's synthetic bucket over that range (fmi_dev_fill_synthetic_at) and reduces them on its own GPU
-        with the single-GPU fused kernel in allreduce_no_order order for its own rank (fmi_dev_reduce_tree).
-        The sharded result must equal it bit for bit (tolerance=False: paths TREE and DIRECT, the reference's
-        bracketing) or lie within (N-1)·2^-24·Σ|x_p| of it (tolerance=True: path RCCL, RCCL's order).
-        Returns the counts, max over ranks; "ok" is the verdict every rank agrees on."""
-        import numpy as np
-
-        from . import device as fdev
-
-        N, r = self.world, self.rank
-        shard = self.shard_elems(n)
-        rng = np.random.default_rng(977 + r)
-        starts = set()
-        for j in range(N):
-            lo = j * shard
-            if lo >= n:
-                break
-            hi = min(n, lo + shard)
-            starts.update({lo, max(lo, hi - width), int(rng.integers(lo, max(lo + 1, hi - width)))})
-        peers = [fdev.Bucket(width, np.float32) for _ in range(N)]
-        ref = fdev.Bucket(width, np.float32)
-        mismatches = checked = 0
-        worst = 0.0
-        for st in sorted(starts):
-            w = min(width, n - st)
-            pv = [p.view(0, w) for p in peers]
-            for p in range(N):
-                pv[p].fill_synthetic(seed, p, first=st)
-            rv = ref.view(0, w)
-            fdev.reduce_tree(Op.SUM, Alg.ALLREDUCE, rv, pv, rank=r)
-            got, want = out.view(st, w).numpy(), rv.numpy()
-            if tolerance:
-                xs = np.stack([v.numpy() for v in pv]).astype(np.float64)
-                bound = (N - 1) * 2.0 ** -24 * np.abs(xs).sum(axis=0)
-                err = np.abs(got.astype(np.float64) - want.astype(np.float64))
-                mismatches += int(np.count_nonzero(err > bound))
-                worst = max(worst, float(np.max(err / np.maximum(bound, 1e-300))) if w else 0.0)
-            else:
-                bad = np.nonzero(got.view(np.uint32) != want.view(np.uint32))[0]
-                if bad.size and mismatches == 0:  # where it went wrong, for the log (the line carries counts)
-                    i = int(bad[0])
-                    import sys
-
-                    print(f"self_check rank {r}: first mismatch at element {st + i}: got {got[i]!r} want {want[i]!r} "
-                          f"(shard {(st + i) // shard} of {N})", file=sys.stderr, flush=True)
-                mismatches += int(bad.size)
-            checked += w
-        for b in peers + [ref]:
-            b.free()
-        mism, chk = self.max_over_ranks(float(mismatches), float(checked))
-        res = {"ok": mism == 0, "mismatches": int(mism), "elements_checked_per_rank": int(chk),
-               "windows_per_rank": len(starts),
-               "against": ("single-GPU fused reduce_tree (allreduce_no_order order, own rank) of the same "
-                           "synthetic buckets rebuilt on this GPU, " +
-                           ("within (N-1)*2^-24*sum|x|" if tolerance else "bit-exact"))}
-        if tolerance:
-            res["max_err_over_bound"] = round(self.max_over_ranks(worst)[0], 4)
-        return res
+        """check_windows() of the out bucket of bench() (path TREE / DIRECT bit-exact, RCCL within tolerance)."""
+        return check_windows(self.world, self.rank, self.shard_elems(n), n, seed,
+                             lambda st, w: out.view(st, w).numpy(), self.max_over_ranks, width, tolerance)
 
     def shard_kernel(self, n: int, launches: int = 20, sets: int = 2) -> dict:
         """The dominant kernel of path TREE on this GPU: the fused N-way tree over n/N-element shards

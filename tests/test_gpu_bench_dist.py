@@ -181,3 +181,28 @@ def test_bench_py_error_line_names_the_runtime():
     assert line["phase"] == "topology check" and "injected failure" in line["error"], line
     rt = line["runtime"]
     assert rt["rccl_version"] > 0 and "librccl" in rt["rccl_path"] and "HIP_VISIBLE_DEVICES" in rt, rt
+
+
+def test_bench_py_falls_back_to_torch_exchange_when_fmi_comm_fails():
+    """If the product communicator cannot be built over RCCL (FMI_BENCH_TEST_RAISE_IN injects the failure inside
+    its init, on every rank), bench.py still measures the same sharded allreduce — the fused tree kernel of
+    libfmi_dev.so on every shard, the two exchanges through torch.distributed's own RCCL group — self-checks it
+    bit-exact, and names the reason in config.exchange_fallback. World size 1 with --force-dist: the exchange
+    runs with itself."""
+    env = dict(os.environ, OMP_NUM_THREADS="1", FMI_BENCH_TEST_RAISE_IN="fmi_comm init")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--force-dist",
+           "--steps", "4", "--warmup", "1", "--dist-sets", "2", "--bucket-mib", "8", "--no-diagnostics"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = r.stdout.strip().splitlines()
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    assert line["value"] > 0 and line["workload"] == "sharded_allreduce", line
+    fb = line["config"]["exchange_fallback"]
+    assert "injected failure" in fb["reason"] and "torch.distributed" in fb["exchange"], fb
+    chk = line["self_check"]
+    assert chk["ok"] and chk["mismatches"] == 0 and chk["elements_checked_per_rank"] > 0, chk
+    assert line["roofline"]["kernel_avg_us"] > 0 and line["config"]["topology"]["ok"], line
+    assert line["local_equivalent"]["GiB_s_reduced_buckets"] > 0, line
+    assert "falling back to torch.distributed" in r.stderr
