@@ -36,8 +36,10 @@ DeviceState g_state;  // one process drives one device (one process per GPU, as 
 // Host-ingress pipeline of fmi_host_reduce_pair: two slots of (a, b) device staging and two streams, one set PER
 // CALLING THREAD. The reference's peers combine concurrently when they are threads of one process (its
 // allreduce's peers each call f.f at once), and one shared pipeline serialised them: 2 / 4 threads took exactly
-// 2 / 4 x one combine (profiles/r04_host_pair_threads.jsonl). Every set is registered so that
-// fmi_dev_finalize frees them all; a thread's cached pointer is trusted only for the generation it was made in.
+// 2 / 4 x one combine (profiles/r04_host_pair_threads_shared.jsonl). A thread leases a set on its first call and
+// hands it back to the idle pool when it exits, so short-lived peer threads reuse sets instead of growing
+// device memory: at most one set per thread alive at once. fmi_dev_finalize frees every set; a lease is trusted
+// only for the generation it was taken in.
 struct HostPipe {
     int device = -1;
     void* stage[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
@@ -53,22 +55,58 @@ struct HostPipe {
         *this = HostPipe{};
     }
 };
-std::mutex g_pipes_mu;
 std::shared_mutex g_pipes_life;  // shared by every fmi_host_reduce_pair in flight, exclusive in fmi_dev_finalize
-std::vector<std::unique_ptr<HostPipe>> g_pipes;
 std::atomic<uint64_t> g_pipes_gen{1};
-thread_local HostPipe* t_pipe = nullptr;
-thread_local uint64_t t_pipe_gen = 0;
+struct PipeRegistry {
+    std::mutex mu;
+    std::vector<std::unique_ptr<HostPipe>> all;  // every set of this generation (owning)
+    std::vector<HostPipe*> idle;                 // sets whose thread has exited
+};
+// Never destroyed: a thread still running while the process exits may hand its set back after static
+// destruction has begun.
+PipeRegistry& pipes() {
+    static PipeRegistry* r = new PipeRegistry;
+    return *r;
+}
+
+struct PipeLease {
+    HostPipe* p = nullptr;
+    uint64_t gen = 0;
+    ~PipeLease() {  // thread exit: no HIP call here, the set's work was synchronised before its last call returned
+        if (!p) return;
+        std::lock_guard<std::mutex> lk(pipes().mu);
+        if (gen == g_pipes_gen.load()) pipes().idle.push_back(p);
+    }
+};
+thread_local PipeLease t_lease;
 
 HostPipe* my_host_pipe() {
     const uint64_t gen = g_pipes_gen.load();
-    if (t_pipe && t_pipe_gen == gen && t_pipe->device == g_state.device) return t_pipe;
-    std::lock_guard<std::mutex> lk(g_pipes_mu);
-    g_pipes.push_back(std::make_unique<HostPipe>());
-    t_pipe = g_pipes.back().get();
-    t_pipe->device = g_state.device;
-    t_pipe_gen = gen;
-    return t_pipe;
+    if (t_lease.p && t_lease.gen == gen && t_lease.p->device == g_state.device) return t_lease.p;
+    PipeRegistry& reg = pipes();
+    std::lock_guard<std::mutex> lk(reg.mu);
+    if (t_lease.p && t_lease.gen == gen) reg.idle.push_back(t_lease.p);  // another device's set: back to the pool
+    HostPipe* got = nullptr;
+    for (size_t i = 0; i < reg.idle.size(); ++i)
+        if (reg.idle[i]->device == g_state.device) {
+            got = reg.idle[i];
+            reg.idle.erase(reg.idle.begin() + static_cast<std::ptrdiff_t>(i));
+            break;
+        }
+    if (!got) {
+        reg.all.push_back(std::make_unique<HostPipe>());
+        got = reg.all.back().get();
+        got->device = g_state.device;
+    }
+    t_lease.p = got;
+    t_lease.gen = gen;
+    return got;
+}
+
+size_t host_pipe_count(size_t* idle) {
+    std::lock_guard<std::mutex> lk(pipes().mu);
+    if (idle) *idle = pipes().idle.size();
+    return pipes().all.size();
 }
 
 // Defaults from tools/tune_pair.py on MI355X (C2, 256 MiB f32): nontemporal one-shot tiles, 4 × 16 B per
@@ -856,9 +894,10 @@ int fmi_dev_finalize(void) {
     (void)hipDeviceSynchronize();
     {
         std::unique_lock<std::shared_mutex> life(g_pipes_life);
-        std::lock_guard<std::mutex> lk(g_pipes_mu);
-        for (auto& p : g_pipes) p->release();
-        g_pipes.clear();
+        std::lock_guard<std::mutex> lk(pipes().mu);
+        for (auto& p : pipes().all) p->release();
+        pipes().all.clear();
+        pipes().idle.clear();
         g_pipes_gen.fetch_add(1);
     }
     if (g_state.arena) (void)hipFree(g_state.arena);
@@ -881,6 +920,9 @@ int fmi_dev_describe(char* buf, size_t len) {
     FMI_HIP_TRY(hipGetDeviceProperties(&prop, g_state.device));
     std::string d = std::string(prop.name) + " " + prop.gcnArchName + " CUs=" + std::to_string(prop.multiProcessorCount) +
                     " HBM=" + std::to_string(prop.totalGlobalMem >> 20) + "MiB";
+    size_t idle = 0;
+    const size_t pipes = host_pipe_count(&idle);  // fmi_host_reduce_pair's per-thread staging sets
+    d += " host_pipelines=" + std::to_string(pipes) + " idle=" + std::to_string(idle);
     std::snprintf(buf, len, "%s", d.c_str());
     return FMI_OK;
 }

@@ -94,7 +94,9 @@ int fmi_dev_init(int device);
 int fmi_dev_finalize(void);
 /* Wait for all work on the selected device. */
 int fmi_dev_sync(void);
-/* Device name + arch string (e.g. "AMD Instinct MI355X gfx950"), NUL-terminated into buf. */
+/* Device name + arch string (e.g. "AMD Instinct MI355X gfx950"), CU count, HBM size, and the number of
+ * fmi_host_reduce_pair staging sets ("host_pipelines=N idle=M": one per calling thread alive, idle ones are
+ * those of exited threads, reused by the next new caller), NUL-terminated into buf. */
 int fmi_dev_describe(char* buf, size_t len);
 /* PCI bus id ("dddd:bb:dd.f") of a visible device, NUL-terminated into buf (hipDeviceGetPCIBusId): with
  * fmi_comm_query, lets the ranks of a communicator show they sit on distinct GPUs. */

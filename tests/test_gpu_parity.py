@@ -762,6 +762,43 @@ def test_host_reduce_pair_concurrent_threads(device, zero_copy):
         fmi_amd.tune_set(Tune.HOST_ZERO_COPY, old[1])
 
 
+def _host_pipelines():
+    import re
+
+    m = re.search(r"host_pipelines=(\d+) idle=(\d+)", fmi_amd.describe())
+    assert m, fmi_amd.describe()
+    return int(m.group(1)), int(m.group(2))
+
+
+def test_host_reduce_pair_short_lived_threads_reuse_staging(device):
+    """The reference spawns a thread per peer for every collective; each calling thread leases a staging set,
+    and an exited thread's set returns to the pool: 40 waves of 4 short-lived threads leave at most the sets
+    that were alive at once (not 160), and every combine is bit-exact."""
+    import threading
+
+    old = fmi_amd.tune_get(Tune.HOST_CHUNK)
+    try:
+        fmi_amd.tune_set(Tune.HOST_CHUNK, 1 << 16)
+        before, _ = _host_pipelines()
+        errors = []
+        for wave in range(40):
+            ts = [threading.Thread(target=_host_pair_rounds, args=(t % 3 * 2, 1, errors)) for t in range(4)]
+            for th in ts:
+                th.start()
+            for th in ts:
+                th.join(timeout=120)
+            assert not any(th.is_alive() for th in ts)
+        assert not errors, errors
+        import time
+
+        time.sleep(0.5)  # Thread.join returns before the OS thread runs its C++ thread_local destructors
+        after, idle = _host_pipelines()
+        # 4 alive at once, plus the sets of a wave whose OS threads had not quite exited when the next started
+        assert after - before <= 12 and idle >= 1, (before, after, idle)
+    finally:
+        fmi_amd.tune_set(Tune.HOST_CHUNK, old)
+
+
 _REINIT_SCRIPT = """
 import sys
 sys.path.insert(0, {root!r})
