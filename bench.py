@@ -1011,6 +1011,10 @@ def run_dist(args, world, rank, local_rank):
     watch = _WATCH = _PhaseWatch(args.measure_deadline, rank)
 
     proc = args.transport == "proc"
+    # every wait of the communicator for its peers (RCCL init included) gives up after this: a broken first
+    # init then leaves time for the exchange fallback within --measure-deadline
+    if not proc:  # (PROC runs keep their FMI_PROC_TIMEOUT_S)
+        os.environ.setdefault("FMI_COMM_TIMEOUT_S", "120")
     dev = local_rank % max(1, torch.cuda.device_count()) if proc else local_rank
     numa = bind_near_gpu(dev) if not args.no_numa_bind else {"bound": False, "disabled": True}
     torch.cuda.set_device(dev)

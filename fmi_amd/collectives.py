@@ -368,8 +368,15 @@ class CommAllreduce:
                          if dist.get_backend(self.group) == "nccl" else torch.device("cpu"))
         _lib.load()
         _lib.call("fmi_dev_init", torch.cuda.current_device())
-        box = [unique_id(tr) if self.rank == 0 else None]
+        box = [None]
+        if self.rank == 0:  # a failure here must still reach the broadcast every other rank is waiting in
+            try:
+                box[0] = unique_id(tr)
+            except Exception as e:  # noqa: BLE001 - re-raised on every rank below
+                box[0] = f"{type(e).__name__}: {e}"
         dist.broadcast_object_list(box, src=0, group=self.group)
+        if isinstance(box[0], str):
+            raise RuntimeError(f"communicator id on rank 0 failed: {box[0]}")
         self.comm = Comm(box[0], self.world, self.rank)
 
     def topology(self) -> dict:
