@@ -15,6 +15,8 @@
 #                                (profiles/r04_c5_local_peers_hwq.jsonl)
 #   bash tools/gpu_round4.sh d   the DMA ceiling of that shape: 8 threads, each streaming 1 GiB H2D and 1 GiB D2H
 #                                on two streams in 64 / 256 MiB pieces, no compute (profiles/r04_pcie_8streams.jsonl)
+#   bash tools/gpu_round4.sh g   the round-end sequence on the final library: the whole GPU suite, smoke(), the default
+#                                bench line, then the C2 profile (profiles/r04g_*)
 set -o pipefail
 cd /root/repo
 mkdir -p gpurun_out
@@ -27,6 +29,13 @@ a)
     ;;
 b)
     timeout -k 10 600 python bench.py > gpurun_out/r04_b_bench.json 2> gpurun_out/r04_b_bench.err &&
+    bash tools/c2_profile.sh
+    ;;
+g)
+    timeout -k 10 1500 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+        -p no:cacheprovider > gpurun_out/r04g_full_gpu.log 2>&1 &&
+    timeout -k 10 300 python -u -c 'import __graft_entry__ as g; g.smoke()' > gpurun_out/r04g_smoke.log 2>&1 &&
+    timeout -k 10 600 python bench.py > gpurun_out/r04g_bench.json 2> gpurun_out/r04g_bench.err &&
     bash tools/c2_profile.sh
     ;;
 f)
@@ -122,7 +131,7 @@ for args in [(1, 1024, 64), (8, 1024, 64), (8, 1024, 64, False), (8, 1024, 256)]
 PY
     ;;
 *)
-    echo "usage: bash tools/gpu_round4.sh a|b|c|d|e|f" >&2
+    echo "usage: bash tools/gpu_round4.sh a|b|c|d|e|f|g" >&2
     exit 2
     ;;
 esac
