@@ -1042,13 +1042,7 @@ def run_dist(args, world, rank, local_rank):
         except Exception as e:  # every rank reaches the agreement below, whether its own init raised or not
             comm_err = f"{type(e).__name__}: {e}"
             print(f"bench: rank {rank}: fmi_comm init failed: {comm_err}", file=sys.stderr, flush=True)
-        watch.enter("agreement on the fmi_comm init")
-        failed = torch.tensor([0 if comm_err is None else 1], dtype=torch.int32, device=torch.device("cuda", dev))
-        dist.all_reduce(failed, op=dist.ReduceOp.MAX)
-        if int(failed.item()):
-            if ar is not None:
-                ar.destroy()
-            run_dist_torch_exchange(args, world, rank, watch, comm_err or "fmi_comm init failed on another rank", numa)
+        if _fall_back(args, world, rank, watch, dev, numa, ar, comm_err, "fmi_comm init"):
             return
     watch.enter("topology check")
     topo = ar.topology()
@@ -1060,8 +1054,19 @@ def run_dist(args, world, rank, local_rank):
         os._exit(1)
     n = args.bucket_mib * MIB // 4
     S = n * 4
-    watch.enter("warm-up and timed allreduces")
-    step_ms, _, extra = ar.bench(n, steps=args.steps, warmup=args.warmup, sets=args.dist_sets, peers_per_gpu=1)
+    if proc:
+        watch.enter("warm-up and timed allreduces")
+        step_ms, _, extra = ar.bench(n, steps=args.steps, warmup=args.warmup, sets=args.dist_sets, peers_per_gpu=1)
+    else:  # a communicator that fails in its first real exchanges (a timeout aborts it on every rank) falls back too
+        run_err = None
+        try:
+            watch.enter("warm-up and timed allreduces")  # (its test hook raises here)
+            step_ms, _, extra = ar.bench(n, steps=args.steps, warmup=args.warmup, sets=args.dist_sets, peers_per_gpu=1)
+        except Exception as e:  # every rank reaches the agreement below
+            run_err = f"fmi_comm allreduce failed: {type(e).__name__}: {e}"
+            print(f"bench: rank {rank}: {run_err}", file=sys.stderr, flush=True)
+        if _fall_back(args, world, rank, watch, dev, numa, ar, run_err, "the fmi_comm allreduce"):
+            return
     out, seed = extra.pop("result")
     value = world * (S / GIB) / (step_ms * 1e-3)
     watch.enter("self-check")
@@ -1124,6 +1129,27 @@ def run_dist(args, world, rank, local_rank):
         print("bench: self-check FAILED: the sharded allreduce differs from the single-GPU kernel", file=sys.stderr,
               flush=True)
         sys.exit(1)
+
+
+def _fall_back(args, world, rank, watch, dev, numa, ar, err, what) -> bool:
+    """Every rank calls this at the same point, whether its own step raised (`err`) or not. If the step failed on
+    any rank, the communicator is destroyed and the line is measured through torch.distributed's exchange
+    (run_dist_torch_exchange); returns True then."""
+    import torch
+    import torch.distributed as dist
+
+    watch.enter(f"agreement on {what}")
+    failed = torch.tensor([0 if err is None else 1], dtype=torch.int32, device=torch.device("cuda", dev))
+    dist.all_reduce(failed, op=dist.ReduceOp.MAX)
+    if not int(failed.item()):
+        return False
+    if ar is not None:
+        try:
+            ar.destroy()
+        except Exception as e:  # an aborted communicator: its teardown is bounded, the fallback does not need it
+            print(f"bench: rank {rank}: destroying the failed communicator: {e}", file=sys.stderr, flush=True)
+    run_dist_torch_exchange(args, world, rank, watch, err or f"{what} failed on another rank", numa)
+    return True
 
 
 def run_dist_torch_exchange(args, world, rank, watch, comm_err, numa):

@@ -183,13 +183,14 @@ def test_bench_py_error_line_names_the_runtime():
     assert rt["rccl_version"] > 0 and "librccl" in rt["rccl_path"] and "HIP_VISIBLE_DEVICES" in rt, rt
 
 
-def test_bench_py_falls_back_to_torch_exchange_when_fmi_comm_fails():
-    """If the product communicator cannot be built over RCCL (FMI_BENCH_TEST_RAISE_IN injects the failure inside
-    its init, on every rank), bench.py still measures the same sharded allreduce — the fused tree kernel of
+@pytest.mark.parametrize("phase", ["fmi_comm init", "warm-up and timed allreduces"])
+def test_bench_py_falls_back_to_torch_exchange_when_fmi_comm_fails(phase):
+    """If the product communicator cannot be built over RCCL, or fails in its first allreduces
+    (FMI_BENCH_TEST_RAISE_IN injects the failure in that phase, on every rank), bench.py still measures the same sharded allreduce — the fused tree kernel of
     libfmi_dev.so on every shard, the two exchanges through torch.distributed's own RCCL group — self-checks it
     bit-exact, and names the reason in config.exchange_fallback. World size 1 with --force-dist: the exchange
     runs with itself."""
-    env = dict(os.environ, OMP_NUM_THREADS="1", FMI_BENCH_TEST_RAISE_IN="fmi_comm init")
+    env = dict(os.environ, OMP_NUM_THREADS="1", FMI_BENCH_TEST_RAISE_IN=phase)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--force-dist",
            "--steps", "4", "--warmup", "1", "--dist-sets", "2", "--bucket-mib", "8", "--no-diagnostics"]
