@@ -264,9 +264,10 @@ def test_comm_300_ranks(device):
         return got
 
     res = run_ranks(N, body)
-    want_ar, _ = orc.allreduce(xs, orc.op_sum)
-    want_red, _ = orc.reduce(xs, orc.op_sum, root=37)
-    want_sc, _ = orc.scan(xs, orc.op_sum)
+    with np.errstate(all="ignore"):  # the synthetic edge values include ±inf: inf + -inf = NaN, as on the GPU
+        want_ar, _ = orc.allreduce(xs, orc.op_sum)
+        want_red, _ = orc.reduce(xs, orc.op_sum, root=37)
+        want_sc, _ = orc.scan(xs, orc.op_sum)
     for r in range(N):
         assert_bit_equal(res[r][0], want_ar[r], f"allreduce rank {r}")
         assert_bit_equal(res[r][2], want_sc[r], f"scan rank {r}")
