@@ -31,6 +31,7 @@ Also reported (one JSON line on rank 0):
                   this GPU); N > 1 every rank's 1 GiB page-locked bucket through fmi_comm_allreduce_host.
   cpu_baseline  — (N = 1) oracle/cpu_baseline (a C++ port of the reference's CPU path) on this host.
   c3            — (N = 1) config C3's kernels: i64 max pair 64 MiB, f32 peer scan 8 x 64 MiB, fraction of peak.
+  c4_one_gpu    — (N = 1) config C4's data on one GPU: 8 peers x 1 GiB through the fused 8-way allreduce kernel.
   diagnostics   — (N > 1) the replicated-pair rate (C2 on every GPU, no exchange), the per-phase breakdown
                   of the exchange and, opt-in, path DIRECT.
 Everything after `value` runs under a per-rank deadline (--diag-deadline); if it expires, rank 0 prints the
@@ -78,6 +79,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-c5", action="store_true", help="skip the host-bucket (C5) measurement")
     ap.add_argument("--no-c3", action="store_true", help="N=1: skip the config C3 kernels (i64 max, peer scan)")
+    ap.add_argument("--no-c4", action="store_true",
+                    help="N=1: skip config C4 on one GPU (8 peers x 1 GiB through the fused 8-way allreduce kernel)")
     ap.add_argument("--c5-mib", type=int, default=1024, help="host bucket per rank of the c5 block (config C5)")
     ap.add_argument("--no-diagnostics", action="store_true", help="N>1: skip the untimed diagnostics")
     ap.add_argument("--no-numa-bind", action="store_true",
@@ -468,6 +471,11 @@ def run_single(args):
             line["c3"] = c3_single()
         except Exception as e:  # reported, never fails the measured line
             line["c3"] = f"failed: {type(e).__name__}: {e}"
+    if not args.no_c4:
+        try:
+            line["c4_one_gpu"] = c4_single()
+        except Exception as e:  # reported, never fails the measured line
+            line["c4_one_gpu"] = f"failed: {type(e).__name__}: {e}"
     if not args.no_c5:
         line["c5"] = c5_single(args.c5_mib)
     print(json.dumps(line), file=json_out(), flush=True)
@@ -489,6 +497,9 @@ def failed_checks(line) -> list:
         for k in ("i64_max_pair_64MiB", "f32_scan_P8_64MiB"):
             if not c3[k]["self_check"]["ok"]:
                 failed.append(f"c3 {k}")
+    c4 = line.get("c4_one_gpu")
+    if isinstance(c4, dict) and not c4["self_check"]["ok"]:
+        failed.append("c4_one_gpu")
     for k, block in (line.get("c5") or {}).items():
         if "error" not in block and not block["self_check"]["ok"]:
             failed.append(f"c5 {k}")
@@ -642,6 +653,54 @@ def c3_single(reps: int = 60) -> dict:
                                       rotating_sets=C3_SCAN_SETS, per_set_launch_us=per_set_us,
                                       self_check=scan_check),
             "timing": "two HIP events around back-to-back launches on the library stream (gaps included)"}
+
+
+def c4_single(peers: int = 8, mib: int = 1024, launches: int = 10) -> dict:
+    """Config C4's data on ONE GPU: 8 peers x 1 GiB f32 buckets resident in HBM, their sum-allreduce computed by
+    one pass of the fused 8-way kernel (fmi_dev_reduce_tree, allreduce_no_order: the reference's recursive-doubling
+    bracketing, PeerToPeer.cpp:96-130). The kernel the N > 1 path runs on every shard, at the whole bucket:
+    (P + 1) x 1 GiB algorithmic bytes per launch (9 GiB, far past the 256 MB MALL: one buffer set is honest).
+    Mean launch time from two HIP events around back-to-back launches on the library stream; the result is
+    checked on head / middle / tail windows against numpy's float32 evaluation of rank 0's bracketing."""
+    import numpy as np
+
+    import fmi_amd
+    from fmi_amd import Alg, Bucket, Event, Op
+
+    n = mib * MIB // 4
+    ins = [Bucket(n, np.float32).fill_synthetic(11, p) for p in range(peers)]
+    out = Bucket(n, np.float32)
+    for _ in range(2):
+        fmi_amd.reduce_tree(Op.SUM, Alg.ALLREDUCE, out, ins)
+    e0, e1 = Event(), Event()
+    e0.record()
+    for _ in range(launches):
+        fmi_amd.reduce_tree(Op.SUM, Alg.ALLREDUCE, out, ins)
+    e1.record()
+    e1.sync()
+    ms = e0.elapsed_ms(e1) / launches
+    e0.destroy()
+    e1.destroy()
+    expr = fmi_amd.schedule_expr(Alg.ALLREDUCE, peers, 0)
+    win, bad, checked = 4096, 0, 0
+    for o in (0, (n // 2) // 64 * 64, n - win):
+        want = eval_bracketing(expr, [b.view(o, win).numpy() for b in ins])
+        bad += int(np.count_nonzero(out.view(o, win).numpy().view(np.uint32) != want.view(np.uint32)))
+        checked += win
+    for b in ins + [out]:
+        b.free()
+    algo = (peers + 1) * n * 4
+    traffic, src = pmc_traffic(f"tree_kernel<fmi::dev::OpSum, float, 0, {peers}, false>", algo)
+    return {"workload": f"C4 on one GPU: {peers} peers x {mib} MiB f32 sum-allreduce, one pass of the fused "
+                        f"{peers}-way kernel (allreduce_no_order bracketing)",
+            "kernel_avg_us": round(ms * 1e3, 2), "algorithmic_bytes": algo,
+            "GB_s": round(algo / (ms * 1e-3) / 1e9, 1), "frac": round(algo / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "GiB_s_reduced_buckets": round(peers * n * 4 / GIB / (ms * 1e-3), 2),
+            "traffic": traffic, "traffic_source": src, "launches": launches,
+            "timing": "two HIP events around back-to-back launches on the library stream (gaps included)",
+            "self_check": {"ok": bad == 0, "mismatches": bad, "elements_checked": checked,
+                           "against": "numpy float32 evaluation of rank 0's allreduce_no_order bracketing "
+                                      "(fmi_schedule_expr) on three windows, bit-exact"}}
 
 
 def eval_bracketing(expr: str, xs):

@@ -316,12 +316,17 @@ def test_failed_checks_fail_the_n1_run():
     ok = {"self_check": {"ok": True}}
     line = {"self_check": {"ok": True}, "allreduce_1peer": {"result_ok": True},
             "c3": {"i64_max_pair_64MiB": dict(ok), "f32_scan_P8_64MiB": dict(ok)},
+            "c4_one_gpu": dict(ok),
             "c5": {"p1_copy": dict(ok), "host_pair_reduce": dict(ok), "local_peers": {"error": "MemoryError"}}}
+    assert bench.failed_checks(line) == []
+    line["c4_one_gpu"] = "failed: MemoryError: out of memory"  # raised: reported, not a wrong result
     assert bench.failed_checks(line) == []
     line["c3"]["f32_scan_P8_64MiB"] = {"self_check": {"ok": False}}
     line["allreduce_1peer"]["result_ok"] = False
+    line["c4_one_gpu"] = {"self_check": {"ok": False}}
     line["c5"]["host_pair_reduce"] = {"self_check": {"ok": False}}
-    assert bench.failed_checks(line) == ["allreduce_1peer", "c3 f32_scan_P8_64MiB", "c5 host_pair_reduce"]
+    assert bench.failed_checks(line) == ["allreduce_1peer", "c3 f32_scan_P8_64MiB", "c4_one_gpu",
+                                         "c5 host_pair_reduce"]
     line["self_check"]["ok"] = False
     assert bench.failed_checks(line)[0] == "c2"
 
