@@ -670,6 +670,9 @@ def c4_single(peers: int = 8, mib: int = 1024, launches: int = 10) -> dict:
     n = mib * MIB // 4
     ins = [Bucket(n, np.float32).fill_synthetic(11, p) for p in range(peers)]
     out = Bucket(n, np.float32)
+    # The driver clears the VRAM C3 just freed (9 GiB) in the background, on the same HBM: measured right after
+    # C3 this launch ran at 0.68 of peak, after a quiet second at 0.76-0.78 (profiles/r04_tree8_sizes.jsonl).
+    quiet_device()
     for _ in range(2):
         fmi_amd.reduce_tree(Op.SUM, Alg.ALLREDUCE, out, ins)
     e0, e1 = Event(), Event()

@@ -17,6 +17,8 @@
 #                                on two streams in 64 / 256 MiB pieces, no compute (profiles/r04_pcie_8streams.jsonl)
 #   bash tools/gpu_round4.sh g   the round-end sequence on the final library: the whole GPU suite, smoke(), the default
 #                                bench line, then the C2 profile (profiles/r04g_*)
+#   bash tools/gpu_round4.sh h   the fused 8-way allreduce kernel against bucket size per peer (64 MiB .. 1 GiB),
+#                                after a quiet second, events over back-to-back launches (profiles/r04_tree8_sizes.jsonl)
 set -o pipefail
 cd /root/repo
 mkdir -p gpurun_out
@@ -37,6 +39,42 @@ g)
     timeout -k 10 300 python -u -c 'import __graft_entry__ as g; g.smoke()' > gpurun_out/r04g_smoke.log 2>&1 &&
     timeout -k 10 600 python bench.py > gpurun_out/r04g_bench.json 2> gpurun_out/r04g_bench.err &&
     bash tools/c2_profile.sh
+    ;;
+h)
+    timeout -k 10 300 python -u - > gpurun_out/r04_tree8_sizes.jsonl <<'PY'
+import json, sys, os, time
+sys.path.insert(0, os.getcwd())
+import numpy as np
+import fmi_amd
+from fmi_amd import Alg, Bucket, Event, Op
+fmi_amd.init(0)
+def run(mib, sets, launches=12, peers=8):
+    n = mib * (1 << 20) // 4
+    ins = [[Bucket(n, np.float32).fill_synthetic(11 + s, p) for p in range(peers)] for s in range(sets)]
+    out = Bucket(n, np.float32)
+    fmi_amd.sync()
+    time.sleep(1.0)
+    for k in range(2):
+        fmi_amd.reduce_tree(Op.SUM, Alg.ALLREDUCE, out, ins[k % sets])
+    e0, e1 = Event(), Event()
+    e0.record()
+    for k in range(launches):
+        fmi_amd.reduce_tree(Op.SUM, Alg.ALLREDUCE, out, ins[k % sets])
+    e1.record()
+    e1.sync()
+    ms = e0.elapsed_ms(e1) / launches
+    per = []
+    for k in range(min(sets * 2, 8)):
+        a, b = Event(), Event()
+        a.record(); fmi_amd.reduce_tree(Op.SUM, Alg.ALLREDUCE, out, ins[k % sets]); b.record(); b.sync()
+        per.append(round(a.elapsed_ms(b) * 1e3, 1))
+    for b in [out] + [x for s in ins for x in s]:
+        b.free()
+    algo = (peers + 1) * n * 4
+    return {"mib_per_peer": mib, "sets": sets, "us": round(ms * 1e3, 2), "frac": round(algo / (ms * 1e-3) / 8e12, 4), "single_launch_us": per}
+for mib, sets in [(1024, 1), (512, 1), (256, 2), (128, 4), (64, 8), (1024, 1)]:
+    print(json.dumps(run(mib, sets)), flush=True)
+PY
     ;;
 f)
     timeout -k 10 300 python -u - > "gpurun_out/r04_host_pair_threads${2:+_$2}.jsonl" <<'PY'
@@ -131,7 +169,7 @@ for args in [(1, 1024, 64), (8, 1024, 64), (8, 1024, 64, False), (8, 1024, 256)]
 PY
     ;;
 *)
-    echo "usage: bash tools/gpu_round4.sh a|b|c|d|e|f|g" >&2
+    echo "usage: bash tools/gpu_round4.sh a|b|c|d|e|f|g|h" >&2
     exit 2
     ;;
 esac
