@@ -542,6 +542,7 @@ def one_peer_allreduce(n: int, launches: int = 20, sets: int = 4) -> dict:
     try:
         for src, dst in pairs:
             comm.allreduce(Op.SUM, src, dst)
+        quiet_device()  # C2 has just freed its 8 GiB of buckets (background VRAM clears share the HBM)
         e0, e1 = Event(), Event()
         e0.record()
         for k in range(launches):
@@ -612,6 +613,7 @@ def c3_single(reps: int = 60) -> dict:
         used[i % C3_PAIR_SETS] += 1
         fmi_amd.reduce_pair(Op.MAX, *pairs[i % C3_PAIR_SETS])
 
+    quiet_device()  # the buckets of the blocks before were just freed (background VRAM clears share the HBM)
     ms_max = timed(launch_max, reps)
     # in-run check: max is idempotent, so a pair combined at least once holds max(a0, b0) (std::max on int64)
     # and one never combined still holds a0 — on the head, middle and tail window of every pair, bit for bit
@@ -626,6 +628,7 @@ def c3_single(reps: int = 60) -> dict:
     S = C3_SCAN_SETS
     ins = [[Bucket(n32, np.float32).fill_synthetic(7 + s, p) for p in range(P)] for s in range(S)]
     outs = [[Bucket(n32, np.float32) for _ in range(P)] for _ in range(S)]
+    quiet_device()  # the 8 GiB of i64 pairs were just freed
     ms_scan = timed(lambda i: fmi_amd.scan_peers(Op.SUM, Alg.SCAN, outs[i % S], ins[i % S]), 3 * S)
     per_set = [(Event(), Event()) for _ in range(S)]  # diagnostic, untimed: one launch per set, its own events
     for i, (a, b) in enumerate(per_set):
@@ -760,7 +763,7 @@ QUIET_S = 1.0
 
 
 def quiet_device():
-    """Let the device go idle before a host-ingress measurement. The driver clears freed VRAM
+    """Let the device go idle before a measurement that follows freed buckets. The driver clears freed VRAM
     asynchronously on the copy engines: right after the C3 / C4 loops free their buckets (GiBs), the H2D
     and D2H copies of C5 share those engines for ~0.3 s and C5 reads 39 ms instead of 23.5 ms
     (profiles/archive/r02_c5_after_free_probe.jsonl: the same buffers, 23.4 ms once 0.3 s have passed). A pause of QUIET_S
