@@ -1232,6 +1232,16 @@ struct Comm {
 
     void note_user_stream(hipStream_t s) {
         if (!s || s == library_stream()) return;
+        if (user_tail.size() >= 64 && !user_tail.count(s)) {  // many caller streams: forget the drained ones
+            for (auto it = user_tail.begin(); it != user_tail.end();) {
+                if (hipEventQuery(it->second) == hipSuccess) {
+                    (void)hipEventDestroy(it->second);
+                    it = user_tail.erase(it);
+                } else {
+                    ++it;
+                }
+            }
+        }
         hipEvent_t& ev = user_tail[s];
         if (!ev && hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
             user_tail.erase(s);

@@ -567,3 +567,28 @@ def test_c5_host_allreduce_full_size(device, record_property):
     ref.free()
     for b in ins:
         b.free()
+
+
+def test_collectives_on_many_caller_streams():
+    """A communicator remembers the tail of every caller stream it queued work on (so destroying an aborted one
+    never frees scratch such work may still read); with many short-lived caller streams the drained tails are
+    forgotten instead of growing without bound. 100 streams, each used for one allreduce then destroyed; every
+    result is the P = 1 allreduce's copy, bit-exact; the communicator is then destroyed cleanly."""
+    from fmi_amd import Stream
+    from fmi_amd.comm import Comm, Transport, unique_id
+
+    n = 4099
+    comm = Comm(unique_id(Transport.LOCAL), 1, 0)
+    try:
+        src = Bucket.from_numpy(np.arange(n, dtype=np.float32))
+        for k in range(100):
+            s = Stream()
+            dst = Bucket(n, np.float32)
+            comm.allreduce(Op.SUM, src, dst, stream=s)
+            s.sync()
+            assert np.array_equal(dst.numpy(), np.arange(n, dtype=np.float32)), k
+            dst.free()
+            s.destroy()
+        src.free()
+    finally:
+        comm.destroy()
