@@ -166,6 +166,7 @@ def cpu_baseline(args):
         "c1": c1_host(),
         "c1_reference": c1_reference(),
         "c2_reference": c2_reference(args.bucket_mib, adapter["median_ms"]),
+        "c3": c3_cpu(exe),
     }
 
 
@@ -264,6 +265,45 @@ def c2_reference(bucket_mib: int, port_combine_ms: float, reps: int = 5) -> dict
                     "against the port's (value). Inside the 2-peer allreduce both peers combine at once; "
                     "combine_in_reference_allreduce_ms (allreduce - no-op allreduce) is to be read against "
                     "reference_adapter_combine_2_threads_ms, the same two combines run concurrently outside it"}
+
+
+def c3_cpu(exe: str, reps: int = 5) -> dict:
+    """Config C3 on the host, beside the line's `c3` GPU block (BASELINE.md's CPU-baseline plan): the int64 max
+    combine of two 64 MiB buckets through the port (oracle/cpu_baseline.cpp: the reference's vector adapter around
+    its std::max functor, python/PythonCommunicator.h:137-143, and the bare loop), and the REFERENCE's own scan
+    (PeerToPeer::scan -> scan_no_order, PeerToPeer.cpp:132-184, compiled unmodified in oracle/_ref) of 8 peers'
+    64 MiB f32 buckets, peers as threads, through the vector adapter and std::transform in place."""
+    out = {"config": "C3"}
+    try:
+        runs = {}
+        for mode in ("adapter", "bare"):
+            r = subprocess.run([exe, "--mode", mode, "--dtype", "i64", "--op", "max", "--mib", "64", "--reps",
+                                str(reps)], check=True, capture_output=True, text=True, timeout=300)
+            runs[mode] = json.loads(r.stdout.strip().splitlines()[-1])
+        out["i64_max_pair_64MiB"] = {"kind": "port", "threads": 1, "reps": reps,
+                                     "adapter_ms": round(runs["adapter"]["median_ms"], 3),
+                                     "bare_ms": round(runs["bare"]["median_ms"], 3),
+                                     "adapter_gib_s": round(runs["adapter"]["bucket_gib_s"], 4),
+                                     "bare_gib_s": round(runs["bare"]["bucket_gib_s"], 4)}
+    except Exception as e:  # reported, never required
+        out["i64_max_pair_64MiB"] = {"error": f"{type(e).__name__}: {e}"}
+    try:
+        from oracle import fmi_ref
+
+        if not fmi_ref.available():
+            raise RuntimeError("oracle/_ref not built")
+        n = 64 * MIB // 4
+        ad = fmi_ref.time_scan(8, n, 3, adapter=True)
+        bi = fmi_ref.time_scan(8, n, 3, adapter=False)
+        out["f32_scan_P8_64MiB"] = {
+            "kind": "reference", "peers": 8, "reps": 3,
+            "code": "reference src/comm/PeerToPeer.cpp (scan_no_order), compiled unmodified (oracle/_ref); peers as "
+                    "threads over in-memory FIFOs",
+            "adapter_ms": round(ad, 2), "builtin_inplace_ms": round(bi, 2),
+            "adapter_gib_s_of_outputs": round(8 * 64 / 1024 / (ad * 1e-3), 4)}
+    except Exception as e:  # reported, never required
+        out["f32_scan_P8_64MiB"] = {"error": f"{type(e).__name__}: {e}"}
+    return out
 
 
 _JSON_OUT = None

@@ -223,3 +223,18 @@ def time_allreduce(P: int, n: int, reps: int, adapter) -> float:
     if f(P, n, reps, adapter, ctypes.byref(ms), err, len(err)) != 0:
         raise RefError(err.value.decode())
     return ms.value
+
+
+def time_scan(P: int, n: int, reps: int, adapter: bool) -> float:
+    """Median ms of the reference's own f32 sum-scan (PeerToPeer::scan -> scan_no_order) over P peer threads and
+    the in-memory transport; adapter as for time_allreduce (True: the vector adapter, False: in place)."""
+    lib = _load()
+    f = lib.fmi_ref_time_scan
+    f.restype = ctypes.c_int
+    f.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
+                  ctypes.c_char_p, ctypes.c_size_t]
+    ms = ctypes.c_double(0.0)
+    err = ctypes.create_string_buffer(512)
+    if f(P, n, reps, int(bool(adapter)), ctypes.byref(ms), err, len(err)) != 0:
+        raise RefError(err.value.decode())
+    return ms.value

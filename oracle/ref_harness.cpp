@@ -29,6 +29,7 @@
 //   fmi_ref_expr  symbolic run: each element is a handle to an expression; f.f(a, b) makes "(a+b)" (left operand
 //                 = arg 0 of f.f), so the result is the exact bracketing the reference evaluates.
 //   fmi_ref_time_allreduce  CPU time of the reference's allreduce (bench.py's C1 / C2 rows of the CPU baseline).
+//   fmi_ref_time_scan       CPU time of the reference's scan (bench.py's C3 row of the CPU baseline).
 //   fmi_ref_time_combine    CPU time of the combine alone, on 1 or several concurrent threads (C2 row).
 //   fmi_ref_run_bound / fmi_ref_time_allreduce_bound  the same reference collectives with f.f bound to a
 //                 bucket-reduction C-ABI whose entry points the caller passes by address (INTEGRATION.md §B.2;
@@ -435,7 +436,9 @@ private:
 
 namespace {
 
-int time_allreduce(int P, size_t n, int reps, const raw_func& f, double* median_ms, char* err, size_t errlen) {
+// P peer threads run the reference's allreduce (coll = kAllreduce) or scan (kScan) of n-element f32 buckets.
+int time_collective(int coll, int P, size_t n, int reps, const raw_func& f, double* median_ms, char* err,
+                    size_t errlen) {
     const size_t S = n * sizeof(float);
     std::vector<std::vector<float>> init(P, std::vector<float>(n)), send(P), recv(P, std::vector<float>(n));
     for (int p = 0; p < P; ++p)
@@ -450,7 +453,12 @@ int time_allreduce(int P, size_t n, int reps, const raw_func& f, double* median_
                 send[p] = init[p];
                 bar.wait();
                 const auto t0 = std::chrono::steady_clock::now();
-                ch.allreduce({reinterpret_cast<char*>(send[p].data()), S}, {reinterpret_cast<char*>(recv[p].data()), S}, rf);
+                const channel_data sd{reinterpret_cast<char*>(send[p].data()), S};
+                const channel_data rd{reinterpret_cast<char*>(recv[p].data()), S};
+                if (coll == kScan)
+                    ch.scan(sd, rd, rf);
+                else
+                    ch.allreduce(sd, rd, rf);
                 bar.wait();
                 if (p == 0) ms[r] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
             }
@@ -545,7 +553,7 @@ FMI_REF_API int fmi_ref_time_allreduce_bound(int P, size_t n, int reps, const Re
     }
     RefBinding host_only = *binding;
     host_only.dev_pair = nullptr;
-    return time_allreduce(P, n, reps, bound_combine(host_only, kSum, kF32, n, {}), median_ms, err, errlen);
+    return time_collective(kAllreduce, P, n, reps, bound_combine(host_only, kSum, kF32, n, {}), median_ms, err, errlen);
 }
 
 // CPU timing of the reference's own allreduce (PeerToPeer::allreduce -> allreduce_no_order, f32 sum) over P
@@ -572,5 +580,17 @@ FMI_REF_API int fmi_ref_time_allreduce(int P, size_t n, int reps, int adapter, d
     } else {
         f = make_combine(kSum, kF32, n);
     }
-    return time_allreduce(P, n, reps, f, median_ms, err, errlen);
+    return time_collective(kAllreduce, P, n, reps, f, median_ms, err, errlen);
+}
+
+// The same for the reference's scan (PeerToPeer::scan -> scan_no_order, f32 sum; PeerToPeer.cpp:132-184): bench.py's
+// cpu_baseline reports it beside config C3's peer scan (8 peers x 64 MiB). adapter as for fmi_ref_time_allreduce.
+FMI_REF_API int fmi_ref_time_scan(int P, size_t n, int reps, int adapter, double* median_ms, char* err,
+                                  size_t errlen) {
+    if (P < 1 || reps < 1 || !median_ms) {
+        set_err(err, errlen, "invalid argument");
+        return -1;
+    }
+    const raw_func f = adapter == 1 ? reference_adapter(n) : make_combine(kSum, kF32, n);
+    return time_collective(kScan, P, n, reps, f, median_ms, err, errlen);
 }

@@ -256,6 +256,15 @@ def test_reference_allreduce_timing_runs():
 
 
 @live
+def test_reference_scan_timing_runs():
+    """bench.py's cpu_baseline C3 row: the reference's scan timed over 8 peer threads, through the vector adapter
+    and in place."""
+    ad = ref.time_scan(8, 1 << 14, 3, adapter=True)
+    bi = ref.time_scan(8, 1 << 14, 3, adapter=False)
+    assert ad > 0 and bi > 0
+
+
+@live
 @pytest.mark.parametrize("P", [1, 2, 3, 5, 8, 13, 17])
 def test_live_reference_bcast_and_gather_equal_oracle(P):
     """The binomial bcast and gather the oracle restates (PeerToPeer.cpp:14-27, :186-239; gather carries
@@ -293,7 +302,7 @@ def test_reference_library_is_built_from_the_reference_alone():
                          text=True).stdout
     exported = sorted(line.split()[-1] for line in dyn.splitlines() if " T " in line)
     assert exported == ["fmi_ref_expr", "fmi_ref_run", "fmi_ref_run_bound", "fmi_ref_time_allreduce",
-                        "fmi_ref_time_allreduce_bound", "fmi_ref_time_combine"], exported
+                        "fmi_ref_time_allreduce_bound", "fmi_ref_time_combine", "fmi_ref_time_scan"], exported
     # the product's C-ABI reaches the harness only by address (fmi_ref_run_bound): nothing of it is linked
     needed = subprocess.run(["readelf", "-d", ref.LIB_PATH], check=True, capture_output=True, text=True).stdout
     assert "libfmi_dev" not in needed and "fmi_" not in undefined, (needed, undefined)
