@@ -167,6 +167,7 @@ def cpu_baseline(args):
         "c1_reference": c1_reference(),
         "c2_reference": c2_reference(args.bucket_mib, adapter["median_ms"]),
         "c3": c3_cpu(exe),
+        "c4_reference": c4_reference(),
     }
 
 
@@ -304,6 +305,34 @@ def c3_cpu(exe: str, reps: int = 5) -> dict:
     except Exception as e:  # reported, never required
         out["f32_scan_P8_64MiB"] = {"error": f"{type(e).__name__}: {e}"}
     return out
+
+
+def c4_reference(peers: int = 8, mib: int = 1024) -> dict:
+    """Config C4 through the REFERENCE's own code on the host: its 8-peer f32 sum-allreduce of 1 GiB buckets
+    (PeerToPeer.cpp:96-130: 3 rounds of exchange + combine per peer), peers as threads over in-memory FIFOs, once
+    with std::transform in place and once through the vector adapter (its 6 bucket copies per combine: up to
+    ~72 GiB of host memory at once, so only where MemAvailable holds twice that). One repetition each: the
+    in-place run takes seconds, the adapter run tens of seconds. Beside it: the line's `c4_one_gpu`."""
+    try:
+        from oracle import fmi_ref
+
+        if not fmi_ref.available():
+            return {"error": "oracle/_ref not built"}
+        n = mib * MIB // 4
+        out = {"config": "C4", "kind": "reference", "peers": peers, "bucket_mib": mib, "reps": 1,
+               "code": "reference src/comm/PeerToPeer.cpp (allreduce_no_order), compiled unmodified (oracle/_ref); "
+                       "peers as threads over in-memory FIFOs"}
+        avail = mem_available_bytes()
+        if avail is None or avail < 2 * 3 * peers * n * 4:  # initial, send and recv buckets of every peer
+            return dict(out, error=f"not run: MemAvailable {avail} B is under twice the run's 24 GiB of buckets")
+        out["builtin_inplace_ms"] = round(fmi_ref.time_allreduce(peers, n, 1, adapter=False), 1)
+        if avail >= 2 * (3 + 6) * peers * n * 4:
+            out["adapter_ms"] = round(fmi_ref.time_allreduce(peers, n, 1, adapter=True), 1)
+        else:
+            out["adapter_ms"] = f"not run: MemAvailable {avail} B is under twice the adapter run's ~72 GiB"
+        return out
+    except Exception as e:  # reported, never required
+        return {"error": f"{type(e).__name__}: {e}"}
 
 
 _JSON_OUT = None
