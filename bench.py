@@ -700,6 +700,7 @@ def c3_single(reps: int = 60) -> dict:
     quiet_device()  # the 8 GiB of i64 pairs were just freed
     ms_scan = timed(lambda i: fmi_amd.scan_peers(Op.SUM, Alg.SCAN, outs[i % S], ins[i % S]), 3 * S)
     per_set = [(Event(), Event()) for _ in range(S)]  # diagnostic, untimed: one launch per set, its own events
+    fmi_amd.scan_peers(Op.SUM, Alg.SCAN, outs[S - 1], ins[S - 1])  # after the host wait: the first launch ramps
     for i, (a, b) in enumerate(per_set):
         a.record()
         fmi_amd.scan_peers(Op.SUM, Alg.SCAN, outs[i], ins[i])
