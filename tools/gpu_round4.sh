@@ -19,6 +19,8 @@
 #                                bench line, then the C2 profile (profiles/r04g_*)
 #   bash tools/gpu_round4.sh h   the fused 8-way allreduce kernel against bucket size per peer (64 MiB .. 1 GiB),
 #                                after a quiet second, events over back-to-back launches (profiles/r04_tree8_sizes.jsonl)
+#   bash tools/gpu_round4.sh i   fmi_host_reduce_pair's staging chunk (FMI_TUNE_HOST_CHUNK 4..64 MiB) on pageable 256 MiB
+#                                and 1 MiB pairs, 1 and 2 threads (profiles/r04_host_chunk_sweep.jsonl)
 set -o pipefail
 cd /root/repo
 mkdir -p gpurun_out
@@ -74,6 +76,41 @@ def run(mib, sets, launches=12, peers=8):
     return {"mib_per_peer": mib, "sets": sets, "us": round(ms * 1e3, 2), "frac": round(algo / (ms * 1e-3) / 8e12, 4), "single_launch_us": per}
 for mib, sets in [(1024, 1), (512, 1), (256, 2), (128, 4), (64, 8), (1024, 1)]:
     print(json.dumps(run(mib, sets)), flush=True)
+PY
+    ;;
+i)
+    timeout -k 10 300 python -u - > gpurun_out/r04_host_chunk_sweep.jsonl <<'PY'
+import json, threading, time, sys, os
+sys.path.insert(0, os.getcwd())
+import numpy as np
+import fmi_amd
+from fmi_amd import Op, Tune
+fmi_amd.init(0)
+def run(mib, threads, reps):
+    n = (mib << 20) // 4
+    pairs = [(np.random.default_rng(t).random(n, dtype=np.float32), np.random.default_rng(9 + t).random(n, dtype=np.float32)) for t in range(threads)]
+    want = [a + b for a, b in pairs]
+    bar = threading.Barrier(threads)
+    times = [[0.0] * reps for _ in range(threads)]
+    def body(t):
+        a0, b = pairs[t]
+        for r in range(reps):
+            a = a0.copy()
+            bar.wait()
+            t0 = time.perf_counter()
+            fmi_amd.host_reduce_pair(Op.SUM, a, b)
+            times[t][r] = time.perf_counter() - t0
+            if r == reps - 1 and not np.array_equal(a, want[t]):
+                raise SystemExit("mismatch")
+    th = [threading.Thread(target=body, args=(t,)) for t in range(threads)]
+    [x.start() for x in th]; [x.join() for x in th]
+    per = sorted(max(times[t][r] for t in range(threads)) for r in range(1, reps))
+    return round(per[len(per) // 2] * 1e3, 3)
+for chunk in (4, 8, 16, 32, 64):
+    fmi_amd.tune_set(Tune.HOST_CHUNK, chunk << 20)
+    row = {"chunk_mib": chunk, "pair_256MiB_1thread_ms": run(256, 1, 5), "pair_256MiB_2threads_ms": run(256, 2, 5),
+           "pair_1MiB_1thread_ms": run(1, 1, 21)}
+    print(json.dumps(row), flush=True)
 PY
     ;;
 f)
@@ -169,7 +206,7 @@ for args in [(1, 1024, 64), (8, 1024, 64), (8, 1024, 64, False), (8, 1024, 256)]
 PY
     ;;
 *)
-    echo "usage: bash tools/gpu_round4.sh a|b|c|d|e|f|g|h" >&2
+    echo "usage: bash tools/gpu_round4.sh a|b|c|d|e|f|g|h|i" >&2
     exit 2
     ;;
 esac
