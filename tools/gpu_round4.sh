@@ -21,6 +21,11 @@
 #                                after a quiet second, events over back-to-back launches (profiles/r04_tree8_sizes.jsonl)
 #   bash tools/gpu_round4.sh i   fmi_host_reduce_pair's staging chunk (FMI_TUNE_HOST_CHUNK 4..64 MiB) on pageable 256 MiB
 #                                and 1 MiB pairs, 1 and 2 threads (profiles/r04_host_chunk_sweep.jsonl)
+#   bash tools/gpu_round4.sh j   host memcpy bandwidth, pageable -> page-locked, 1..8 threads (numpy copyto, GIL
+#                                released): could CPU-side staging beat the runtime's pageable copies? (r04_host_memcpy.jsonl)
+#   bash tools/gpu_round4.sh k   the host-staged pageable pipeline (FMI_TUNE_HOST_COPY_THREADS 0 = the runtime's
+#                                pageable copies, 2 / 4 / 8 threads) x staging chunk 4 / 16 / 64 MiB, on 256 MiB and
+#                                1 MiB pairs, 1 and 2 callers (profiles/r04_host_staged_sweep.jsonl)
 set -o pipefail
 cd /root/repo
 mkdir -p gpurun_out
@@ -78,8 +83,10 @@ for mib, sets in [(1024, 1), (512, 1), (256, 2), (128, 4), (64, 8), (1024, 1)]:
     print(json.dumps(run(mib, sets)), flush=True)
 PY
     ;;
-i)
-    timeout -k 10 300 python -u - > gpurun_out/r04_host_chunk_sweep.jsonl <<'PY'
+i | k)
+    out=gpurun_out/r04_host_chunk_sweep.jsonl
+    [ "$1" = k ] && out=gpurun_out/r04_host_staged_sweep.jsonl
+    MODE=$1 timeout -k 10 400 python -u - > "$out" <<'PY'
 import json, threading, time, sys, os
 sys.path.insert(0, os.getcwd())
 import numpy as np
@@ -101,16 +108,78 @@ def run(mib, threads, reps):
             fmi_amd.host_reduce_pair(Op.SUM, a, b)
             times[t][r] = time.perf_counter() - t0
             if r == reps - 1 and not np.array_equal(a, want[t]):
-                raise SystemExit("mismatch")
+                bad.append((mib, threads, t))
+    bad = []
     th = [threading.Thread(target=body, args=(t,)) for t in range(threads)]
     [x.start() for x in th]; [x.join() for x in th]
+    if bad:
+        raise SystemExit(f"result mismatch: {bad}")
     per = sorted(max(times[t][r] for t in range(threads)) for r in range(1, reps))
     return round(per[len(per) // 2] * 1e3, 3)
-for chunk in (4, 8, 16, 32, 64):
-    fmi_amd.tune_set(Tune.HOST_CHUNK, chunk << 20)
-    row = {"chunk_mib": chunk, "pair_256MiB_1thread_ms": run(256, 1, 5), "pair_256MiB_2threads_ms": run(256, 2, 5),
-           "pair_1MiB_1thread_ms": run(1, 1, 21)}
-    print(json.dumps(row), flush=True)
+if os.environ["MODE"] == "i":
+    fmi_amd.tune_set(Tune.HOST_COPY_THREADS, 0)  # the runtime's pageable copies (the path this sweep tuned)
+    for chunk in (4, 8, 16, 32, 64):
+        fmi_amd.tune_set(Tune.HOST_CHUNK, chunk << 20)
+        row = {"chunk_mib": chunk, "pair_256MiB_1thread_ms": run(256, 1, 5), "pair_256MiB_2threads_ms": run(256, 2, 5),
+               "pair_1MiB_1thread_ms": run(1, 1, 21)}
+        print(json.dumps(row), flush=True)
+else:
+    for threads in (0, 2, 4, 8):
+        fmi_amd.tune_set(Tune.HOST_COPY_THREADS, threads)
+        for chunk in ((64,) if threads == 0 else (4, 16, 64)):
+            fmi_amd.tune_set(Tune.HOST_STAGE_CHUNK if threads else Tune.HOST_CHUNK, chunk << 20)
+            row = {"copy_threads": threads, "chunk_mib": chunk, "pair_256MiB_1caller_ms": run(256, 1, 5),
+                   "pair_256MiB_2callers_ms": run(256, 2, 5), "pair_1MiB_1caller_ms": run(1, 1, 21)}
+            print(json.dumps(row), flush=True)
+PY
+    ;;
+j)
+    timeout -k 10 300 python -u - > gpurun_out/r04_host_memcpy.jsonl <<'PY'
+import json, threading, time, sys, os
+sys.path.insert(0, os.getcwd())
+import numpy as np
+import fmi_amd
+from fmi_amd.device import PinnedArray
+fmi_amd.init(0)
+n = (512 << 20) // 4
+src = np.random.default_rng(1).random(n, dtype=np.float32)
+dst = PinnedArray(n, np.float32)
+for threads in (1, 2, 4, 8):
+    parts = np.array_split(np.arange(n), threads)
+    bounds = [(int(p[0]), int(p[-1]) + 1) for p in parts]
+    best = 1e9
+    for rep in range(5):
+        bar = threading.Barrier(threads + 1)
+        def body(lo, hi):
+            bar.wait()
+            np.copyto(dst.array[lo:hi], src[lo:hi])
+        th = [threading.Thread(target=body, args=b) for b in bounds]
+        [x.start() for x in th]
+        bar.wait()
+        t0 = time.perf_counter()
+        [x.join() for x in th]
+        best = min(best, time.perf_counter() - t0)
+    assert np.array_equal(dst.array, src)
+    print(json.dumps({"threads": threads, "MiB": 512, "ms": round(best * 1e3, 2), "GB_s": round(n * 4 / best / 1e9, 1)}), flush=True)
+back = np.empty_like(src)
+for threads in (1, 2, 4, 8):  # and the other way: page-locked -> pageable (the host-staged path's copy-out)
+    parts = np.array_split(np.arange(n), threads)
+    bounds = [(int(p[0]), int(p[-1]) + 1) for p in parts]
+    best = 1e9
+    for rep in range(5):
+        bar = threading.Barrier(threads + 1)
+        def body(lo, hi):
+            bar.wait()
+            np.copyto(back[lo:hi], dst.array[lo:hi])
+        th = [threading.Thread(target=body, args=b) for b in bounds]
+        [x.start() for x in th]
+        bar.wait()
+        t0 = time.perf_counter()
+        [x.join() for x in th]
+        best = min(best, time.perf_counter() - t0)
+    assert np.array_equal(back, src)
+    print(json.dumps({"direction": "page-locked -> pageable", "threads": threads, "MiB": 512, "ms": round(best * 1e3, 2), "GB_s": round(n * 4 / best / 1e9, 1)}), flush=True)
+dst.free()
 PY
     ;;
 f)
@@ -206,7 +275,7 @@ for args in [(1, 1024, 64), (8, 1024, 64), (8, 1024, 64, False), (8, 1024, 256)]
 PY
     ;;
 *)
-    echo "usage: bash tools/gpu_round4.sh a|b|c|d|e|f|g|h|i" >&2
+    echo "usage: bash tools/gpu_round4.sh a|b|c|d|e|f|g|h|i|j|k" >&2
     exit 2
     ;;
 esac
