@@ -1,17 +1,12 @@
 // fmi_dev.hip — C-ABI implementation (include/fmi_dev.h): device state, memory, streams, events, the
 // pairwise hot kernel's launch policy, P-way dispatch, the host-ingress pipeline and synthetic buckets.
-#include <unistd.h>
-
 #include <algorithm>
 #include <atomic>
-#include <condition_variable>
 #include <cstring>
-#include <deque>
 #include <memory>
 #include <mutex>
 #include <shared_mutex>
 #include <string>
-#include <thread>
 #include <vector>
 
 #include "fmi_internal.h"
@@ -50,98 +45,15 @@ struct HostPipe {
     void* stage[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
     size_t stage_bytes = 0;
     hipStream_t pipe[2] = {nullptr, nullptr};
-    // the host-staged path (FMI_TUNE_HOST_COPY_THREADS > 0): two slots of page-locked (a, b) staging and the
-    // event that ends each slot's kernel
-    void* pin[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
-    size_t pin_bytes = 0;
-    hipEvent_t done[2] = {nullptr, nullptr};
     void release() {
         for (int k = 0; k < 2; ++k) {
             if (pipe[k]) (void)hipStreamSynchronize(pipe[k]);
-            for (int j = 0; j < 2; ++j) {
+            for (int j = 0; j < 2; ++j)
                 if (stage[k][j]) (void)hipFree(stage[k][j]);
-                if (pin[k][j]) (void)hipHostFree(pin[k][j]);
-            }
-            if (done[k]) (void)hipEventDestroy(done[k]);
             if (pipe[k]) (void)hipStreamDestroy(pipe[k]);
         }
         *this = HostPipe{};
     }
-};
-
-// Host threads that copy between the caller's pageable buckets and page-locked staging for the host-staged
-// pipeline of fmi_host_reduce_pair. One pool per process, shared by every calling thread (jobs queue FIFO);
-// workers are started on demand and never stopped, the pool is never destroyed (a worker may still be parked on
-// its condition variable while the process exits), and a forked child starts a pool of its own.
-class CopyPool {
-public:
-    static CopyPool& get() {
-        static std::mutex mu;
-        static CopyPool* pool = nullptr;
-        std::lock_guard<std::mutex> lk(mu);
-        if (!pool || pool->pid_ != getpid()) pool = new CopyPool;  // the parent's workers do not exist here
-        return *pool;
-    }
-    // dst[0, bytes) = src[0, bytes) over `parts` threads (the caller's included); returns when all are done.
-    void copy(void* dst, const void* src, size_t bytes, int parts) {
-        constexpr size_t kMinPart = size_t(1) << 20;
-        parts = static_cast<int>(std::min<size_t>(std::max(parts, 1), std::max<size_t>(1, bytes / kMinPart)));
-        if (parts <= 1) {
-            std::memcpy(dst, src, bytes);
-            return;
-        }
-        ensure(parts - 1);
-        Latch latch{parts - 1};
-        const size_t per = (bytes / parts + 4095) & ~size_t(4095);
-        {
-            std::lock_guard<std::mutex> lk(mu_);
-            for (int j = 1; j < parts; ++j) {
-                const size_t lo = std::min(bytes, per * j), hi = std::min(bytes, per * (j + 1));
-                q_.push_back({static_cast<char*>(dst) + lo, static_cast<const char*>(src) + lo, hi - lo, &latch});
-            }
-        }
-        cv_.notify_all();
-        std::memcpy(dst, src, std::min(per, bytes));
-        std::unique_lock<std::mutex> lk(latch.mu);
-        latch.cv.wait(lk, [&] { return latch.left == 0; });
-    }
-
-private:
-    struct Latch {
-        int left;
-        std::mutex mu;
-        std::condition_variable cv;
-    };
-    struct Job {
-        char* dst;
-        const char* src;
-        size_t bytes;
-        Latch* latch;
-    };
-    CopyPool() : pid_(getpid()) {}
-    void ensure(int k) {
-        std::lock_guard<std::mutex> lk(mu_);
-        for (; workers_ < k; ++workers_) std::thread([this] { work(); }).detach();
-    }
-    void work() {
-        for (;;) {
-            Job j;
-            {
-                std::unique_lock<std::mutex> lk(mu_);
-                cv_.wait(lk, [&] { return !q_.empty(); });
-                j = q_.front();
-                q_.pop_front();
-            }
-            std::memcpy(j.dst, j.src, j.bytes);
-            std::lock_guard<std::mutex> lk(j.latch->mu);
-            if (--j.latch->left == 0) j.latch->cv.notify_all();
-        }
-    }
-    const pid_t pid_;
-    std::mutex mu_;
-    std::condition_variable cv_;
-    std::deque<Job> q_;
-    int workers_ = 0;
 };
 std::shared_mutex g_pipes_life;  // shared by every fmi_host_reduce_pair in flight, exclusive in fmi_dev_finalize
 std::atomic<uint64_t> g_pipes_gen{1};
@@ -199,14 +111,13 @@ size_t host_pipe_count(size_t* idle) {
 
 // Defaults from tools/tune_pair.py on MI355X (C2, 256 MiB f32): nontemporal one-shot tiles, 4 × 16 B per
 // operand per thread, 256-thread workgroups — 125 µs = 6.4 TB/s vs 142 µs for plain loads/stores.
-std::atomic<long long> g_tune[16] = {2 /*variant: nontemporal tiles*/, 4 /*unroll*/, 256 /*block*/,
+std::atomic<long long> g_tune[14] = {2 /*variant: nontemporal tiles*/, 4 /*unroll*/, 256 /*block*/,
                                      8 /*grid per CU*/, 64ll << 20 /*host chunk*/, 1 /*host zero-copy*/,
                                      64 /*fused in-flight KiB per CU (tools/ab_fused_cap.py)*/,
                                      1 /*one-pass blocked scan*/, 0 /*ncclAllToAll*/, 0 /*ncclAllGather*/,
                                      0 /*no allreduce pipelining*/, 1 /*fused kernels: buffer ops where measured faster*/,
                                      1 /*pairwise: tiles t % 8 < 1 (one XCD) store sc1 (tools/ab_pair_sc1.py)*/,
-                                     0 /*one-rank communicators copy*/,
-                                     4 /*host copy threads (pageable host combine)*/, 16ll << 20 /*host-staged chunk*/};
+                                     0 /*one-rank communicators copy*/};
 
 int hip_fail(const char* what, hipError_t e) {
     return fail(FMI_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
@@ -1357,82 +1268,6 @@ static int scan_peers_impl(int op, int dtype, int alg, void* const* outs, const 
 // Host-ingress pipeline: chunk c uses slot c % 2 (its own staging pair and its own stream). Stream order
 // keeps a slot's staging from being overwritten before its previous D2H finished, while the other slot's
 // H2D overlaps this slot's kernel + D2H.
-}  // extern "C"
-
-namespace {
-
-// fmi_host_reduce_pair on pageable buckets, host-staged: chunk k is copied by `threads` host threads into the
-// calling thread's page-locked slot k % 2 while the pairwise kernel combines chunk k - 1 in place in the other
-// slot, reading and writing it over PCIe (zero-copy, as for page-locked buckets); then chunk k - 1's result is
-// copied back into the caller's bucket. PCIe carries the same 3 bytes per bucket byte as the zero-copy kernel,
-// and the host copies run beside it (profiles/r04_host_memcpy.jsonl: 4 threads copy at ~89 GB/s). Same kernel,
-// same bits as every other path.
-int host_staged_pair(HostPipe& hp, int op, int dtype, char* hx, const char* hy, size_t n, size_t esz, int threads) {
-    size_t chunk_elems = static_cast<size_t>(std::max<long long>(g_tune[FMI_TUNE_HOST_STAGE_CHUNK].load(), 1 << 16)) / esz;
-    chunk_elems = std::max<size_t>(16, chunk_elems / 16 * 16);
-    const size_t chunk_bytes = chunk_elems * esz;
-    if (hp.pin_bytes < chunk_bytes) {
-        for (int k = 0; k < 2; ++k) FMI_HIP_TRY(hipStreamSynchronize(hp.pipe[k]));
-        for (int k = 0; k < 2; ++k)
-            for (int j = 0; j < 2; ++j) {
-                if (hp.pin[k][j]) FMI_HIP_TRY(hipHostFree(hp.pin[k][j]));
-                hp.pin[k][j] = nullptr;
-            }
-        hp.pin_bytes = 0;
-        for (int k = 0; k < 2; ++k)
-            for (int j = 0; j < 2; ++j) {
-                const hipError_t e = hipHostMalloc(&hp.pin[k][j], chunk_bytes, hipHostMallocDefault);
-                if (e != hipSuccess) return fail(FMI_ERR_ALLOC, std::string("hipHostMalloc (host-staged pipeline): ") + hipGetErrorString(e));
-            }
-        hp.pin_bytes = chunk_bytes;
-    }
-    for (int k = 0; k < 2; ++k)
-        if (!hp.done[k]) FMI_HIP_TRY(hipEventCreateWithFlags(&hp.done[k], hipEventDisableTiming));
-    void* dev[2][2];
-    for (int k = 0; k < 2; ++k)
-        for (int j = 0; j < 2; ++j)
-            if (!host_mapped(hp.pin[k][j], chunk_bytes, &dev[k][j]))
-                return fail(FMI_ERR_HIP, "host-staged pipeline: page-locked staging is not device-mapped");
-    CopyPool& pool = CopyPool::get();
-    const size_t chunks = (n + chunk_elems - 1) / chunk_elems;
-    auto span = [&](size_t k, size_t* off, size_t* cnt) {
-        *off = k * chunk_elems;
-        *cnt = std::min(chunk_elems, n - *off);
-    };
-    int rc = FMI_OK;
-    for (size_t k = 0; k <= chunks && rc == FMI_OK; ++k) {
-        if (k < chunks) {  // chunk k in: its slot's previous chunk (k - 2) was copied out in the last iteration
-            const int slot = static_cast<int>(k & 1);
-            size_t off, cnt;
-            span(k, &off, &cnt);
-            pool.copy(hp.pin[slot][0], hx + off * esz, cnt * esz, threads);
-            pool.copy(hp.pin[slot][1], hy + off * esz, cnt * esz, threads);
-            rc = launch_combine(op, dtype, dev[slot][0], dev[slot][0], dev[slot][1], cnt, hp.pipe[slot]);
-            if (rc != FMI_OK) break;
-            if (const hipError_t e = hipEventRecord(hp.done[slot], hp.pipe[slot]); e != hipSuccess) {
-                rc = hip_fail("host-staged pipeline: event record", e);
-                break;
-            }
-        }
-        if (k >= 1) {  // chunk k - 1 out, while the kernel of chunk k runs
-            const int slot = static_cast<int>((k - 1) & 1);
-            size_t off, cnt;
-            span(k - 1, &off, &cnt);
-            if (const hipError_t e = hipEventSynchronize(hp.done[slot]); e != hipSuccess) {
-                rc = hip_fail("host-staged pipeline: kernel", e);
-                break;
-            }
-            pool.copy(hx + off * esz, hp.pin[slot][0], cnt * esz, threads);
-        }
-    }
-    for (int k = 0; k < 2; ++k) FMI_HIP_TRY(hipStreamSynchronize(hp.pipe[k]));
-    return rc;
-}
-
-}  // namespace
-
-extern "C" {
-
 int fmi_host_reduce_pair(int op, int dtype, void* inout, const void* in, size_t n) {
     if (op < FMI_OP_SUM || op > FMI_OP_MIN) return fail(FMI_ERR_INVALID, "unknown op " + std::to_string(op));
     const size_t esz = dtype_size(dtype);
@@ -1467,8 +1302,6 @@ int fmi_host_reduce_pair(int op, int dtype, void* inout, const void* in, size_t 
             return FMI_OK;
         }
     }
-    if (const int threads = static_cast<int>(g_tune[FMI_TUNE_HOST_COPY_THREADS].load()); threads > 0)
-        return host_staged_pair(hp, op, dtype, static_cast<char*>(inout), static_cast<const char*>(in), n, esz, threads);
     size_t chunk_elems = static_cast<size_t>(std::max<long long>(g_tune[FMI_TUNE_HOST_CHUNK].load(), 1 << 16)) / esz;
     chunk_elems = std::max<size_t>(16, chunk_elems / 16 * 16);
     const size_t chunk_bytes = chunk_elems * esz;
@@ -1601,12 +1434,6 @@ int fmi_tune_set(int key, long long value) {
         case FMI_TUNE_COMM_ONE_RANK_EXCHANGE:
             if (value != 0 && value != 1) return fail(FMI_ERR_INVALID, "one-rank exchange must be 0 or 1");
             break;
-        case FMI_TUNE_HOST_COPY_THREADS:
-            if (value < 0 || value > 64) return fail(FMI_ERR_INVALID, "host copy threads must be in [0, 64]");
-            break;
-        case FMI_TUNE_HOST_STAGE_CHUNK:
-            if (value < (1 << 16)) return fail(FMI_ERR_INVALID, "host-staged chunk must be >= 64 KiB");
-            break;
         default: return fail(FMI_ERR_INVALID, "unknown tuning key");
     }
     g_tune[key].store(value);
@@ -1614,7 +1441,7 @@ int fmi_tune_set(int key, long long value) {
 }
 
 int fmi_tune_get(int key, long long* value) {
-    if (!value || key < 0 || key > FMI_TUNE_HOST_STAGE_CHUNK) return fail(FMI_ERR_INVALID, "bad tuning query");
+    if (!value || key < 0 || key > FMI_TUNE_COMM_ONE_RANK_EXCHANGE) return fail(FMI_ERR_INVALID, "bad tuning query");
     *value = g_tune[key].load();
     return FMI_OK;
 }

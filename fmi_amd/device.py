@@ -63,8 +63,6 @@ class Tune(enum.IntEnum):
     FUSED_POLICY = 11
     PAIR_SC1_OF_8 = 12
     COMM_ONE_RANK_EXCHANGE = 13
-    HOST_COPY_THREADS = 14
-    HOST_STAGE_CHUNK = 15
 
 
 NP_DTYPE = {DType.F32: np.float32, DType.F64: np.float64, DType.I32: np.int32, DType.I64: np.int64,

@@ -387,13 +387,7 @@ typedef enum {
                                     all-to-all, shard kernel, all-gather / gather / all-to-all back, RCCL
                                     reduce-scatter, window mapping, the pipelined split — exchanging with
                                     itself, instead of the reference's P = 1 copy. Same bits; exists so that
-                                    a 1-GPU box runs the RCCL transport's real collectives (tests). Default 0 */,
-    FMI_TUNE_HOST_COPY_THREADS = 14, /* fmi_host_reduce_pair on PAGEABLE buckets: host threads that copy each chunk
-                                    into this thread's page-locked staging (and the result back), while the pairwise
-                                    kernel combines the previous chunk over PCIe from that staging (zero-copy).
-                                    0 = the runtime's pageable copies through device staging instead. Same bits
-                                    always */
-    FMI_TUNE_HOST_STAGE_CHUNK = 15 /* bytes per chunk of that host-staged pipeline (>= 64 KiB) */
+                                    a 1-GPU box runs the RCCL transport's real collectives (tests). Default 0 */
 } fmi_tune_key_t;
 int fmi_tune_set(int key, long long value);
 int fmi_tune_get(int key, long long* value);

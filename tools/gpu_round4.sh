@@ -25,7 +25,8 @@
 #                                released): could CPU-side staging beat the runtime's pageable copies? (r04_host_memcpy.jsonl)
 #   bash tools/gpu_round4.sh k   the host-staged pageable pipeline (FMI_TUNE_HOST_COPY_THREADS 0 = the runtime's
 #                                pageable copies, 2 / 4 / 8 threads) x staging chunk 4 / 16 / 64 MiB, on 256 MiB and
-#                                1 MiB pairs, 1 and 2 callers (profiles/r04_host_staged_sweep.jsonl)
+#                                1 MiB pairs, 1 and 2 callers (profiles/r04_host_staged_sweep.jsonl). Rejected and
+#                                removed: it runs only against the library of commit ba6eddb
 set -o pipefail
 cd /root/repo
 mkdir -p gpurun_out
@@ -117,7 +118,6 @@ def run(mib, threads, reps):
     per = sorted(max(times[t][r] for t in range(threads)) for r in range(1, reps))
     return round(per[len(per) // 2] * 1e3, 3)
 if os.environ["MODE"] == "i":
-    fmi_amd.tune_set(Tune.HOST_COPY_THREADS, 0)  # the runtime's pageable copies (the path this sweep tuned)
     for chunk in (4, 8, 16, 32, 64):
         fmi_amd.tune_set(Tune.HOST_CHUNK, chunk << 20)
         row = {"chunk_mib": chunk, "pair_256MiB_1thread_ms": run(256, 1, 5), "pair_256MiB_2threads_ms": run(256, 2, 5),
