@@ -161,8 +161,9 @@ def cpu_baseline(args):
         "all_threads_loop": {"gib_s": round(omp["bucket_gib_s"], 4), "threads": omp["threads"],
                              "median_ms": round(omp["median_ms"], 3),
                              "note": f"OMP_NUM_THREADS = {os.environ.get('OMP_NUM_THREADS')}: the CPU share the "
-                                     f"box allots one GPU's job; os.cpu_count() = {os.cpu_count()} counts the whole "
-                                     "machine, whose other cores belong to other GPUs' jobs"},
+                                     f"box allots one GPU's job, and so this box's CPU roofline; os.cpu_count() = "
+                                     f"{os.cpu_count()} counts the whole machine, and the same loop on that many "
+                                     "threads ran 52x slower (2.77 GiB/s, profiles/r04_allcores_bench.json)"},
         "c1": c1_host(),
         "c1_reference": c1_reference(),
         "c2_reference": c2_reference(args.bucket_mib, adapter["median_ms"]),
