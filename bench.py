@@ -1275,7 +1275,8 @@ def _fall_back(args, world, rank, watch, dev, numa, ar, err, what) -> bool:
     import torch.distributed as dist
 
     watch.enter(f"agreement on {what}")
-    failed = torch.tensor([0 if err is None else 1], dtype=torch.int32, device=torch.device("cuda", dev))
+    on = torch.device("cuda", dev) if dist.get_backend() == "nccl" else torch.device("cpu")  # gloo: CPU tests
+    failed = torch.tensor([0 if err is None else 1], dtype=torch.int32, device=on)
     dist.all_reduce(failed, op=dist.ReduceOp.MAX)
     if not int(failed.item()):
         return False

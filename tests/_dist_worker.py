@@ -111,3 +111,36 @@ def run_bench(rank, world, port, n, path, outdir):
             json.dump({"step_ms": step_ms, "kernel_ms": kernel_ms, "extra": extra}, f)
     finally:
         dist.destroy_process_group()
+
+
+def run_fall_back(rank, world, port, failing_rank, outdir):
+    """bench._fall_back over gloo: only `failing_rank` saw its step raise (or no rank, failing_rank = -1); every
+    rank must reach the same verdict, and the ranks that fall back hand run_dist_torch_exchange the reason (their
+    own error, or "failed on another rank"). run_dist_torch_exchange itself is recorded, not run (it needs GPUs)."""
+    import json
+    import sys
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench
+
+    calls = []
+    bench.run_dist_torch_exchange = lambda args, w, r, watch, err, numa: calls.append(err)
+
+    class Watch:
+        def enter(self, phase):
+            pass
+
+    class Comm:
+        destroyed = False
+
+        def destroy(self):
+            Comm.destroyed = True
+
+    err = f"RuntimeError: rank {rank} broke" if rank == failing_rank else None
+    fell = bench._fall_back(None, world, rank, Watch(), 0, {}, Comm(), err, "the fmi_comm allreduce")
+    with open(os.path.join(outdir, f"fall{rank}.json"), "w") as f:
+        json.dump({"fell": fell, "calls": calls, "destroyed": Comm.destroyed}, f)
+    dist.destroy_process_group()

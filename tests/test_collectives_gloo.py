@@ -186,3 +186,24 @@ def test_runtime_info_names_the_rccl_and_never_raises(monkeypatch):
     assert info["HIP_VISIBLE_DEVICES"] == "0,1"
     if "rccl_error" not in info:
         assert info["rccl_version"] > 0 and "librccl" in info["rccl_path"] and os.path.isabs(info["rccl_path"])
+
+
+@pytest.mark.parametrize("failing_rank", [-1, 0, 1])
+def test_bench_exchange_fallback_agreement_world2(failing_rank):
+    """bench.py's N > 1 exchange fallback (bench._fall_back), world size 2 over gloo: when one rank's communicator
+    step raised, BOTH ranks fall back (destroying their communicator, naming the reason: their own error or
+    "failed on another rank"); when none did, neither does."""
+    import json
+
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_dist_worker.run_fall_back, args=(world, _free_port(), failing_rank, d), nprocs=world, join=True)
+        res = [json.load(open(os.path.join(d, f"fall{r}.json"))) for r in range(world)]
+    for r, x in enumerate(res):
+        assert x["fell"] == (failing_rank >= 0) and x["destroyed"] == (failing_rank >= 0), (r, x)
+        if failing_rank < 0:
+            assert x["calls"] == []
+        elif r == failing_rank:
+            assert x["calls"] == [f"RuntimeError: rank {r} broke"]
+        else:
+            assert x["calls"] == ["the fmi_comm allreduce failed on another rank"]
