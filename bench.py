@@ -29,7 +29,8 @@ Also reported (one JSON line on rank 0):
   c5            — config C5: N = 1 three self-checked blocks (c5_single: the P = 1 copy, a 1 GiB page-locked
                   pair through fmi_host_reduce_pair, and the whole 8 x 1 GiB workload as 8 LOCAL ranks on
                   this GPU); N > 1 every rank's 1 GiB page-locked bucket through fmi_comm_allreduce_host.
-  cpu_baseline  — (N = 1) oracle/cpu_baseline (a C++ port of the reference's CPU path) on this host.
+  cpu_baseline  — (N = 1) the reference's own CPU combine (oracle/_ref) on this host, its C++ port
+                  (oracle/cpu_baseline) beside it as `port_value`.
   c3            — (N = 1) config C3's kernels: i64 max pair 64 MiB, f32 peer scan 8 x 64 MiB, fraction of peak.
   c4_one_gpu    — (N = 1) config C4's data on one GPU: 8 peers x 1 GiB through the fused 8-way allreduce kernel.
   diagnostics   — (N > 1) the replicated-pair rate (C2 on every GPU, no exchange), the per-phase breakdown
@@ -99,6 +100,11 @@ def parse():
                     help="run the N>1 code path (fmi_comm over RCCL) even at world size 1 — plumbing check; the one "
                          "rank then runs the full exchange with itself (FMI_TUNE_COMM_ONE_RANK_EXCHANGE)")
     ap.add_argument("--cpu-reps", type=int, default=30, help="adapter combines timed (≈10 s of CPU work)")
+    ap.add_argument("--allow-exchange-fallback", action="store_true",
+                    help="N>1: if the fmi_comm communicator fails, report the torch.distributed-exchange rate as `value` "
+                         "and exit 0. Default: that rate goes to `fallback_value`, `value` is null and the run exits 1, "
+                         "so a product failure cannot pass as a scaling point (top-level `exchange` names whose "
+                         "exchange was measured either way)")
     return ap.parse_args()
 
 
@@ -122,13 +128,34 @@ def pmc_traffic(kernel_substr: str, algo_bytes: int):
     return hits[0].get("hbm_bytes_per_launch"), hits[0].get("source", data.get("source"))
 
 
+def reference_combine_ms(n: int, reps: int):
+    """The REFERENCE's own combine on one host thread: oracle/_ref's fmi_ref_time_combine with the vector adapter
+    (include/Communicator.h:180-189 restated, boost being absent; include/utils/Function.h:11-13's by-value
+    operator() compiled from the reference's header) around std::plus<float>, median ms of `reps`. None if
+    oracle/_ref is not built."""
+    try:
+        from oracle import fmi_ref
+
+        if not fmi_ref.available():
+            return None, "oracle/_ref not built"
+        return fmi_ref.time_combine(1, n, reps, adapter=True), None
+    except Exception as e:  # reported, never required
+        return None, f"{type(e).__name__}: {e}"
+
+
 def cpu_baseline(args):
+    """`value` is the reference's own adapter combine (oracle/_ref, "kind": "reference") of the headline pair on one
+    host thread; the port's (oracle/cpu_baseline.cpp) stands beside it as `port_value` with their ratio. Only if
+    oracle/_ref is missing does the port become `value` ("kind": "port")."""
     exe = os.path.join(ROOT, "oracle", "build", "cpu_baseline")
     if not os.path.exists(exe):
         return None
+    n = args.bucket_mib * MIB // 4
+    ref_ms, ref_err = reference_combine_ms(n, args.cpu_reps)
     try:
+        port_reps = max(5, args.cpu_reps // 3) if ref_ms is not None else args.cpu_reps
         out = subprocess.run([exe, "--mode", "adapter", "--dtype", "f32", "--op", "sum", "--mib", str(args.bucket_mib),
-                              "--reps", str(args.cpu_reps)], check=True, capture_output=True, text=True, timeout=600)
+                              "--reps", str(port_reps)], check=True, capture_output=True, text=True, timeout=600)
         adapter = json.loads(out.stdout.strip().splitlines()[-1])
         out = subprocess.run([exe, "--mode", "bare", "--dtype", "f32", "--op", "sum", "--mib", str(args.bucket_mib),
                               "--reps", "9"], check=True, capture_output=True, text=True, timeout=600)
@@ -147,16 +174,33 @@ def cpu_baseline(args):
                 break
     except OSError:
         pass
-    return {
-        "value": round(adapter["bucket_gib_s"], 4),
+    gib = args.bucket_mib / 1024
+    port_gib_s = adapter["bucket_gib_s"]
+    if ref_ms is not None:
+        value, kind = gib / (ref_ms * 1e-3), "reference"
+        sample = (f"the reference's own adapter combine (oracle/_ref: include/utils/Function.h's by-value operator() "
+                  f"compiled from the reference's header, include/Communicator.h:180-189's vector adapter restated) "
+                  f"around std::plus<float>, 1 thread, {args.bucket_mib} MiB f32 pair, median of {args.cpu_reps}: "
+                  f"{ref_ms:.1f} ms/combine; the port (oracle/cpu_baseline.cpp) {adapter['median_ms']:.1f} ms; bare "
+                  f"std::transform 1 thread: {bare['median_ms']:.2f} ms = {bare['bucket_gib_s']:.2f} GiB/s; host "
+                  f"'{model}', {os.cpu_count()} CPUs visible")
+    else:
+        value, kind = port_gib_s, "port"
+        sample = (f"port of the reference's adapter (include/Communicator.h:182-187, 6 bucket copies) around "
+                  f"std::transform(std::plus<float>), 1 thread, {args.bucket_mib} MiB f32 pair, median of "
+                  f"{adapter['reps']} after 1 warm-up: {adapter['median_ms']:.1f} ms/combine ({ref_err}); bare "
+                  f"std::transform 1 thread: {bare['median_ms']:.2f} ms = {bare['bucket_gib_s']:.2f} GiB/s; host "
+                  f"'{model}', {os.cpu_count()} CPUs visible")
+    line = {
+        "value": round(value, 4),
         "unit": "GiB/s",
         "cores": 1,
-        "kind": "port",
-        "sample": (f"reference-faithful adapter (include/Communicator.h:182-187, 6 bucket copies) around "
-                   f"std::transform(std::plus<float>), 1 thread, {args.bucket_mib} MiB f32 pair, median of "
-                   f"{adapter['reps']} after 1 warm-up: {adapter['median_ms']:.1f} ms/combine; bare std::transform "
-                   f"1 thread: {bare['median_ms']:.2f} ms = {bare['bucket_gib_s']:.2f} GiB/s; host '{model}', "
-                   f"{os.cpu_count()} CPUs visible"),
+        "kind": kind,
+        "sample": sample,
+        "port_value": round(port_gib_s, 4),
+        "reference_combine_ms": round(ref_ms, 2) if ref_ms is not None else None,
+        "port_combine_ms": round(adapter["median_ms"], 2),
+        "reference_over_port": round(ref_ms / adapter["median_ms"], 3) if ref_ms is not None else None,
         "bare_loop_gib_s": round(bare["bucket_gib_s"], 4),
         "all_threads_loop": {"gib_s": round(omp["bucket_gib_s"], 4), "threads": omp["threads"],
                              "median_ms": round(omp["median_ms"], 3),
@@ -164,12 +208,17 @@ def cpu_baseline(args):
                                      f"box allots one GPU's job, and so this box's CPU roofline; os.cpu_count() = "
                                      f"{os.cpu_count()} counts the whole machine, and the same loop on that many "
                                      "threads ran 52x slower (2.77 GiB/s, profiles/r04_allcores_bench.json)"},
+    }
+    if ref_err:
+        line["reference_error"] = ref_err
+    line.update({
         "c1": c1_host(),
         "c1_reference": c1_reference(),
-        "c2_reference": c2_reference(args.bucket_mib, adapter["median_ms"]),
+        "c2_reference": c2_reference(args.bucket_mib, adapter["median_ms"], ref_ms),
         "c3": c3_cpu(exe),
         "c4_reference": c4_reference(),
-    }
+    })
+    return line
 
 
 def c1_host():
@@ -221,7 +270,7 @@ def c1_reference(reps: int = 41) -> dict:
     return out
 
 
-def c2_reference(bucket_mib: int, port_combine_ms: float, reps: int = 5) -> dict:
+def c2_reference(bucket_mib: int, port_combine_ms: float, one_thread_ms=None, reps: int = 5) -> dict:
     """The headline size through the REFERENCE's own code: its 2-peer f32 sum-allreduce of `bucket_mib` buckets
     (src/comm/PeerToPeer.cpp:96-130: per peer one exchange, one combine f.f at :119, the result memcpy at :129),
     peers as threads over in-memory FIFOs, with the vector adapter and with std::transform in place. A third
@@ -238,7 +287,7 @@ def c2_reference(bucket_mib: int, port_combine_ms: float, reps: int = 5) -> dict
         ad = fmi_ref.time_allreduce(2, n, reps, adapter=True)
         bi = fmi_ref.time_allreduce(2, n, reps, adapter=False)
         nop = fmi_ref.time_allreduce(2, n, reps, adapter="nop")
-        one = fmi_ref.time_combine(1, n, reps, adapter=True)
+        one = one_thread_ms if one_thread_ms is not None else fmi_ref.time_combine(1, n, reps, adapter=True)
         two = fmi_ref.time_combine(2, n, reps, adapter=True)
     except Exception as e:  # reported, never required
         return {"error": f"{type(e).__name__}: {e}"}
@@ -339,6 +388,11 @@ def c4_reference(peers: int = 8, mib: int = 1024) -> dict:
 _JSON_OUT = None
 _LINE_PRINTED = False  # the one JSON line is out (N > 1: by the emitter, on every rank's view)
 _WATCH = None  # N > 1: the phase watch of this rank (names the phase an error line reports)
+# N > 1: whose exchange the line measures, at top level of every N > 1 line: the product's
+# communicator, or torch.distributed's after the communicator failed (run_dist_torch_exchange)
+EXCHANGE_FMI = "fmi_comm"
+EXCHANGE_TORCH = "torch_fallback"
+_EXCHANGE = EXCHANGE_FMI
 
 
 def json_out():
@@ -418,7 +472,7 @@ def _error_line(world, error, phase, **extra):
         except Exception as e:  # the library itself may be what failed
             runtime = {"error": f"{type(e).__name__}: {e}"}
     line = {"metric": METRIC, "value": None, "unit": "GiB/s", "n_gpus": world, "workload": WORKLOAD_DIST,
-            "higher_is_better": True, "error": error, "phase": phase, "runtime": runtime}
+            "exchange": _EXCHANGE, "higher_is_better": True, "error": error, "phase": phase, "runtime": runtime}
     line.update(extra)
     return line
 
@@ -1157,8 +1211,12 @@ def run_dist(args, world, rank, local_rank):
     watch.enter("process group init")
     if proc:
         dist.init_process_group("gloo")
+        vote = None
     else:
         dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        # the fallback agreement votes on a gloo group of its own: a vote can never pair with an RCCL collective
+        # of the timed loop that another rank is still inside
+        vote = dist.new_group(backend="gloo")
 
     import fmi_amd
     from fmi_amd.collectives import CommAllreduce
@@ -1178,7 +1236,7 @@ def run_dist(args, world, rank, local_rank):
         except Exception as e:  # every rank reaches the agreement below, whether its own init raised or not
             comm_err = f"{type(e).__name__}: {e}"
             print(f"bench: rank {rank}: fmi_comm init failed: {comm_err}", file=sys.stderr, flush=True)
-        if _fall_back(args, world, rank, watch, dev, numa, ar, comm_err, "fmi_comm init"):
+        if _fall_back(args, world, rank, watch, dev, numa, ar, comm_err, "fmi_comm init", group=vote):
             return
     watch.enter("topology check")
     topo = ar.topology()
@@ -1201,7 +1259,7 @@ def run_dist(args, world, rank, local_rank):
         except Exception as e:  # every rank reaches the agreement below
             run_err = f"fmi_comm allreduce failed: {type(e).__name__}: {e}"
             print(f"bench: rank {rank}: {run_err}", file=sys.stderr, flush=True)
-        if _fall_back(args, world, rank, watch, dev, numa, ar, run_err, "the fmi_comm allreduce"):
+        if _fall_back(args, world, rank, watch, dev, numa, ar, run_err, "the fmi_comm allreduce", group=vote):
             return
     out, seed = extra.pop("result")
     value = world * (S / GIB) / (step_ms * 1e-3)
@@ -1229,6 +1287,7 @@ def run_dist(args, world, rank, local_rank):
                      f"(a {args.bucket_mib} MiB device-resident bucket) per GPU, through fmi_comm_allreduce",
                      f"{world} GPUs, one peer per GPU, buckets sharded {world} ways; path {args.path}: "
                      f"{path_desc[args.path]}; transport {args.transport}", n, roof)
+    line["exchange"] = EXCHANGE_FMI
     line["config"]["topology"] = topo
     if one_rank_exchange:
         line["config"]["one_rank_exchange"] = ("FMI_TUNE_COMM_ONE_RANK_EXCHANGE = 1: the one rank runs the full "
@@ -1267,17 +1326,21 @@ def run_dist(args, world, rank, local_rank):
         sys.exit(1)
 
 
-def _fall_back(args, world, rank, watch, dev, numa, ar, err, what) -> bool:
+def _fall_back(args, world, rank, watch, dev, numa, ar, err, what, group=None) -> bool:
     """Every rank calls this at the same point, whether its own step raised (`err`) or not. If the step failed on
     any rank, the communicator is destroyed and the line is measured through torch.distributed's exchange
-    (run_dist_torch_exchange); returns True then."""
+    (run_dist_torch_exchange); returns True then. The vote runs on `group` (a gloo group of its own, CPU tensor)
+    when given, so it cannot pair with an RCCL collective a peer is still inside."""
     import torch
     import torch.distributed as dist
 
     watch.enter(f"agreement on {what}")
-    on = torch.device("cuda", dev) if dist.get_backend() == "nccl" else torch.device("cpu")  # gloo: CPU tests
+    if group is not None:
+        on = torch.device("cpu")
+    else:
+        on = torch.device("cuda", dev) if dist.get_backend() == "nccl" else torch.device("cpu")  # gloo: CPU tests
     failed = torch.tensor([0 if err is None else 1], dtype=torch.int32, device=on)
-    dist.all_reduce(failed, op=dist.ReduceOp.MAX)
+    dist.all_reduce(failed, op=dist.ReduceOp.MAX, group=group)
     if not int(failed.item()):
         return False
     if ar is not None:
@@ -1285,6 +1348,8 @@ def _fall_back(args, world, rank, watch, dev, numa, ar, err, what) -> bool:
             ar.destroy()
         except Exception as e:  # an aborted communicator: its teardown is bounded, the fallback does not need it
             print(f"bench: rank {rank}: destroying the failed communicator: {e}", file=sys.stderr, flush=True)
+    global _EXCHANGE
+    _EXCHANGE = EXCHANGE_TORCH  # every line from here on (the measured one, or an error line) says so
     run_dist_torch_exchange(args, world, rank, watch, err or f"{what} failed on another rank", numa)
     return True
 
@@ -1361,6 +1426,7 @@ def run_dist_torch_exchange(args, world, rank, watch, comm_err, numa):
                      f"(a {args.bucket_mib} MiB device-resident bucket) per GPU",
                      f"{world} GPUs, one peer per GPU, buckets sharded {world} ways; all-to-all + fused tree kernel "
                      f"+ all-gather (bit-exact), exchanges through torch.distributed (RCCL)", n, roof)
+    line["exchange"] = EXCHANGE_TORCH
     line["config"]["topology"] = topo
     line["config"].update({"rotating_sets": args.dist_sets, "numa_binding_rank0": numa, "peers": world,
                            "path": "tree", "transport": "torch.distributed (nccl backend = RCCL)",
@@ -1385,12 +1451,23 @@ def run_dist_torch_exchange(args, world, rank, watch, comm_err, numa):
         except Exception as e:  # reported; the line is still printed
             line["local_equivalent"] = {"error": f"{type(e).__name__}: {e}"}
     line["c4"] = line["c5"] = "not run (needs the fmi_comm communicator)"
+    allowed = bool(getattr(args, "allow_exchange_fallback", False))
+    if not allowed:  # the product failed: the rate measured through torch's exchange is not the headline
+        line["fallback_value"] = line["value"]
+        line["value"] = None
+        line["exchange_fallback_note"] = ("fmi_comm failed (config.exchange_fallback.reason); `fallback_value` is the "
+                                          "same workload through torch.distributed's exchange. Exit status 1; "
+                                          "--allow-exchange-fallback reports it as `value` and exits 0")
     _Emitter(line, rank).emit()
     dist.barrier()
     dist.destroy_process_group()
     if not check["ok"]:
         print("bench: self-check FAILED: the sharded allreduce differs from the single-GPU kernel", file=sys.stderr,
               flush=True)
+        sys.exit(1)
+    if not allowed:
+        print("bench: fmi_comm failed; the line carries the torch.distributed exchange's rate as `fallback_value` "
+              "(--allow-exchange-fallback to report it as `value`)", file=sys.stderr, flush=True)
         sys.exit(1)
 
 

@@ -7,8 +7,10 @@
 //   * Data<Dev::Bucket<A>> (bucket in MI355X HBM) + a built-in Function (Function<T>(Utils::Op::sum)):
 //     every combine the channel algorithm performs is the gfx950 kernel fmi_dev_reduce_pair, on the
 //     buffers where they live — no host round trip, no copies.
-//   * Data<std::vector<A>> + a built-in Function, after use_device(d): each combine streams the two host
-//     buckets through the GPU (fmi_host_reduce_pair: chunked H2D / kernel / D2H).
+//   * Data<std::vector<A>> + a built-in Function, after use_device(d): each combine whose buckets are large
+//     enough to pay (ChannelPolicy::host_combine_on_device, the measured crossover) streams the two host buckets
+//     through the GPU (fmi_host_reduce_pair: zero-copy over PCIe if page-locked, else chunked H2D / kernel /
+//     D2H); smaller ones run in place on the host. use_device(d, true) sends every combine to the GPU.
 //   * Data<std::vector<A>> + a built-in Function without use_device: the combine runs in place on the
 //     host buckets (no bucket copies).
 //   * any user lambda: the reference's adapter, unchanged (include/Communicator.h:180-189 semantics).
@@ -16,6 +18,7 @@
 #ifndef FMI_AMD_COMMUNICATOR_H
 #define FMI_AMD_COMMUNICATOR_H
 
+#include <atomic>
 #include <cstring>
 #include <iostream>
 #include <map>
@@ -141,17 +144,24 @@ public:
     }
 
     void set_channel_policy(std::shared_ptr<Utils::ChannelPolicy> p) { policy = std::move(p); }
+    //! The policy the communicator dispatches through (extension: e.g. to move the host-combine crossover).
+    std::shared_ptr<Utils::ChannelPolicy> channel_policy() const { return policy; }
 
     void hint(Utils::Hint h) {
         channel_hint = h;
         policy->set_hint(h);
     }
 
-    //! MI355X extension: run the combines of built-in Functions on host buckets on GPU `device`.
-    void use_device(int device) {
+    //! MI355X extension: run the combines of built-in Functions on host buckets on GPU `device` where the
+    //! policy's crossover says the GPU pays (ChannelPolicy::host_combine_on_device); `always`: every one.
+    void use_device(int device, bool always = false) {
         Dev::init(device);
         offload_host_ = true;
+        offload_always_ = always;
     }
+
+    //! Where the last built-in combine of host buckets ran (tests, diagnostics): true = the GPU.
+    bool last_host_combine_on_device() const { return last_on_device_->load(); }
 
     Utils::peer_num get_peer_id() const { return peer_id; }
     Utils::peer_num get_num_peers() const { return num_peers; }
@@ -193,9 +203,23 @@ private:
                 const std::size_t count = size_in_bytes / sizeof(A);
                 const device_op dop{static_cast<int>(op), Dev::dtype_of<A>(), count};
                 if (offload_host_) {
-                    auto part = [dop](char* a, char* b, std::size_t off, std::size_t len) {
-                        Dev::check(fmi_host_reduce_pair(dop.op, dop.dtype, a + off, b + off, len / sizeof(A)),
-                                   "fmi_host_reduce_pair");
+                    // per combine: the GPU where it pays, else the host loop (the same op, so the same bits)
+                    auto part = [dop, op, policy = policy, always = offload_always_, last = last_on_device_](
+                                    char* a, char* b, std::size_t off, std::size_t len) {
+                        void* d = nullptr;
+                        const bool pinned = fmi_host_device_ptr(a + off, len, &d) == FMI_OK &&
+                                            fmi_host_device_ptr(b + off, len, &d) == FMI_OK;
+                        if (always || policy->host_combine_on_device(len, pinned)) {
+                            last->store(true);
+                            Dev::check(fmi_host_reduce_pair(dop.op, dop.dtype, a + off, b + off, len / sizeof(A)),
+                                       "fmi_host_reduce_pair");
+                            return;
+                        }
+                        last->store(false);
+                        A* x = reinterpret_cast<A*>(a + off);
+                        const A* y = reinterpret_cast<const A*>(b + off);
+                        for (std::size_t i = 0, m = len / sizeof(A); i < m; ++i)
+                            x[i] = Utils::detail::apply_op<A>(op, x[i], y[i]);
                     };
                     return raw_function{[part, size_in_bytes](char* a, char* b) { part(a, b, 0, size_in_bytes); },
                                         f.associative, f.commutative, dop, part, sizeof(A)};
@@ -242,6 +266,8 @@ private:
     std::string comm_name;
     Utils::Hint channel_hint = Utils::Hint::cheap;
     bool offload_host_ = false;
+    bool offload_always_ = false;
+    std::shared_ptr<std::atomic<bool>> last_on_device_ = std::make_shared<std::atomic<bool>>(false);
 };
 
 }  // namespace FMI

@@ -3,7 +3,8 @@
 // price + FaaS runtime price for Hint::cheap. Channels are compared through their own
 // get_operation_latency / get_operation_price, so an RCCL channel competes on the same terms.
 // Added: channels that cannot carry the operation's buffers (host vs device), or cannot run an opaque user
-// reduction function, are skipped.
+// reduction function, are skipped; and the cost model of a built-in combine of two HOST buckets (after
+// Communicator::use_device): the GPU (fmi_host_reduce_pair) against the host loop in place, by bucket size.
 #ifndef FMI_AMD_UTILS_CHANNELPOLICY_H
 #define FMI_AMD_UTILS_CHANNELPOLICY_H
 
@@ -35,6 +36,25 @@ public:
 
     void set_hint(Hint hint) { hint_ = hint; }
 
+    //! Host-combine crossover: smallest bucket, in bytes, whose built-in combine of two host
+    //! buckets runs faster through the GPU (fmi_host_reduce_pair: the buckets cross PCIe, 2 in and 1 out) than as
+    //! the host loop in place on the calling thread. Measured on MI355X by tools/host_crossover.py
+    //! (profiles/r05_host_crossover.jsonl): page-locked buckets (the zero-copy kernel) pay from 64 MiB; pageable
+    //! buckets (staged H2D / kernel / D2H) not at any size measured, up to 512 MiB; both lose by 14-37x at 64 KiB,
+    //! where the call costs its launch and PCIe latency, not its bytes.
+    static constexpr std::size_t kHostCombinePinnedMinBytes = std::size_t(64) << 20;
+    static constexpr std::size_t kHostCombinePageableMinBytes = std::numeric_limits<std::size_t>::max();
+
+    //! Does a built-in combine of two host buckets of `bucket_bytes` pay on the GPU? (Communicator::use_device
+    //! asks this per combine; use_device(d, true) skips it.)
+    virtual bool host_combine_on_device(std::size_t bucket_bytes, bool page_locked) const {
+        return bucket_bytes >= (page_locked ? host_pinned_min_ : host_pageable_min_);
+    }
+    void set_host_combine_min_bytes(std::size_t pageable, std::size_t page_locked) {
+        host_pageable_min_ = pageable;
+        host_pinned_min_ = page_locked;
+    }
+
 protected:
     std::string pick(const OperationInfo& op_info, bool on_device) {
         std::string best;
@@ -59,6 +79,8 @@ protected:
     peer_num num_peers_;
     double faas_price_;
     Hint hint_;
+    std::size_t host_pageable_min_ = kHostCombinePageableMinBytes;
+    std::size_t host_pinned_min_ = kHostCombinePinnedMinBytes;
 };
 
 }  // namespace FMI::Utils

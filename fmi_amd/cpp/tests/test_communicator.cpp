@@ -660,7 +660,7 @@ GPU_TEST(small_integer_buckets_known_answers) {
         dmax[p] = run(Op::max);
     });
     with_peers(4, [&](Communicator& c, peer_num p) {
-        c.use_device(0);
+        c.use_device(0, true);  // every combine on the GPU, whatever the crossover
         const std::size_t n = 70001;
         Data<std::vector<int8_t>> a(std::vector<int8_t>(n, static_cast<int8_t>(p + 1))), r(n);
         c.allreduce(a, r, Function<std::vector<int8_t>>(Op::sum));
@@ -705,7 +705,7 @@ GPU_TEST(host_offload_matches_host_path) {
         host[p] = r.get();
     });
     with_peers(4, [&](Communicator& c, peer_num p) {
-        c.use_device(0);
+        c.use_device(0, true);  // every combine on the GPU, whatever the crossover
         Data<std::vector<float>> a(synth_f32(n, 7, p)), r(n);
         c.allreduce(a, r, Function<std::vector<float>>(Op::sum));
         off[p] = r.get();
@@ -992,6 +992,50 @@ GPU_TEST(policy_host_ingress_keeps_user_functions_and_small_buckets_on_host) {
     CHECK(policy.get_device_channel({FMI::Utils::allreduce, std::size_t(1) << 20}) == "Rccl");
 }
 
+TEST(policy_host_combine_crossover) {
+    // the built-in combine of two host buckets goes to the GPU only past the measured
+    // crossover (profiles/r05_host_crossover.jsonl); both sides of it, pinned and pageable, and an override
+    std::map<std::string, std::shared_ptr<FMI::Comm::Channel>> chans;
+    FMI::Utils::ChannelPolicy policy(chans, 2, 0.0000166667 / 8, FMI::Utils::fast);
+    using P = FMI::Utils::ChannelPolicy;
+    const std::size_t cross = P::kHostCombinePinnedMinBytes;
+    CHECK(!policy.host_combine_on_device(64 << 10, true));
+    CHECK(!policy.host_combine_on_device(cross - 1, true));
+    CHECK(policy.host_combine_on_device(cross, true));
+    CHECK(policy.host_combine_on_device(std::size_t(1) << 30, true));
+    CHECK(!policy.host_combine_on_device(64 << 10, false));
+    CHECK(!policy.host_combine_on_device(cross, false));  // pageable buckets did not pay at any size measured
+    CHECK(!policy.host_combine_on_device(std::size_t(1) << 30, false));
+    policy.set_host_combine_min_bytes(std::size_t(1) << 20, 0);
+    CHECK(!policy.host_combine_on_device((std::size_t(1) << 20) - 4, false));
+    CHECK(policy.host_combine_on_device(std::size_t(1) << 20, false));
+    CHECK(policy.host_combine_on_device(4, true));
+}
+
+GPU_TEST(host_combine_follows_the_policy_crossover) {
+    // use_device(0): a 1 MiB pageable combine stays on the host (below the crossover); use_device(0, true) and a
+    // policy whose crossover is 0 send it to the GPU; every result is the same, bit for bit
+    const std::size_t n = (1 << 18) + 5;
+    std::vector<float> got[3][2];
+    bool on_device[3][2] = {};
+    for (int mode = 0; mode < 3; ++mode)
+        with_peers(2, [&](Communicator& c, peer_num p) {
+            c.use_device(0, mode == 1);
+            if (mode == 2) c.channel_policy()->set_host_combine_min_bytes(0, 0);
+            Data<std::vector<float>> a(synth_f32(n, 5, p)), r(n);
+            c.allreduce(a, r, Function<std::vector<float>>(Op::sum));
+            got[mode][p] = r.get();
+            on_device[mode][p] = c.last_host_combine_on_device();
+        });
+    for (int p = 0; p < 2; ++p) {
+        CHECK(!on_device[0][p]);
+        CHECK(on_device[1][p]);
+        CHECK(on_device[2][p]);
+        CHECK(std::memcmp(got[0][p].data(), got[1][p].data(), n * 4) == 0);
+        CHECK(std::memcmp(got[0][p].data(), got[2][p].data(), n * 4) == 0);
+    }
+}
+
 GPU_TEST(device_buckets_need_builtin_op) {
     Dev::init(0);
     with_peers(1, [](Communicator& c, peer_num) {
@@ -1025,7 +1069,7 @@ static int dump(const std::string& kind, peer_num P, std::size_t n, const std::s
             }
             run(c, p, a, r, f);
         } else {
-            if (mode == "offload") c.use_device(0);
+            if (mode == "offload") c.use_device(0, true);  // every combine on the GPU
             Data<std::vector<float>> a(synth_f32(n, 42, p)), r(n);
             Function<std::vector<float>> f(Op::sum);
             if (ordered) {

@@ -1112,17 +1112,50 @@ private:
 // ---------------------------------------------------------------------------------------------------
 // communicator
 // ---------------------------------------------------------------------------------------------------
-// Streams and events of the host-ingress pipeline (fmi_comm_allreduce_host), created on first use.
+// The host pipeline's DMA streams: ONE host -> device and ONE device -> host stream per device for the whole
+// process, shared by every communicator's fmi_comm_allreduce_host. The runtime hands its
+// DMA engines to streams: with one stream per direction the two directions run on separate engines, at the
+// link's duplex rate (1 GiB each way in 22.4 ms, 96 GB/s); with a pair per LOCAL rank (8 ranks, 16 copy streams)
+// the directions land on shared engines and serialise, 178-241 ms for 8 GiB each way depending on the streams
+// the runtime had handed out before, against 178.0 ms on one shared pair every time
+// (profiles/r05_pcie_peers.jsonl, tools/microbench_pcie_peers.hip). Per-rank order is kept by each rank's own
+// events; the ranks' chunks interleave on the shared streams in the order their threads issue them, which the
+// LOCAL rendezvous of every chunk keeps rank-major per chunk. Never destroyed (like the library stream).
+static int shared_copy_streams(hipStream_t* h2d, hipStream_t* d2h) {
+    static std::mutex mu;
+    static auto* by_device = new std::map<int, std::pair<hipStream_t, hipStream_t>>;
+    int device = -1;
+    FMI_COMM_HIP(hipGetDevice(&device));
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = by_device->find(device);
+    if (it == by_device->end()) {
+        hipStream_t a = nullptr, b = nullptr;
+        FMI_COMM_HIP(hipStreamCreateWithFlags(&a, hipStreamNonBlocking));
+        const hipError_t e = hipStreamCreateWithFlags(&b, hipStreamNonBlocking);
+        if (e != hipSuccess) {
+            (void)hipStreamDestroy(a);
+            return fail(FMI_ERR_HIP, std::string("hipStreamCreateWithFlags (shared D2H stream): ") + hipGetErrorString(e));
+        }
+        it = by_device->emplace(device, std::make_pair(a, b)).first;
+    }
+    *h2d = it->second.first;
+    *d2h = it->second.second;
+    return FMI_OK;
+}
+
+// Streams and events of the host-ingress pipeline (fmi_comm_allreduce_host), created on first use: the chunk's
+// sharded allreduce runs on the communicator's own stream, the copies on the device's shared pair.
 struct HostPipe {
-    hipStream_t cs = nullptr;   // the chunk's sharded allreduce
-    hipStream_t h2d = nullptr;  // host -> device loads
-    hipStream_t d2h = nullptr;  // device -> host results
+    hipStream_t cs = nullptr;   // the chunk's sharded allreduce (this communicator's own)
+    hipStream_t h2d = nullptr;  // host -> device loads (shared_copy_streams: not owned)
+    hipStream_t d2h = nullptr;  // device -> host results (shared_copy_streams: not owned)
     hipEvent_t loaded[2] = {}, reduced[2] = {}, drained[2] = {};
     bool ready = false;
 
     int init() {
         if (ready) return FMI_OK;
-        for (hipStream_t* st : {&cs, &h2d, &d2h}) FMI_COMM_HIP(hipStreamCreateWithFlags(st, hipStreamNonBlocking));
+        FMI_COMM_RC(shared_copy_streams(&h2d, &d2h));
+        FMI_COMM_HIP(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
         for (int k = 0; k < 2; ++k)
             for (hipEvent_t* ev : {&loaded[k], &reduced[k], &drained[k]})
                 FMI_COMM_HIP(hipEventCreateWithFlags(ev, hipEventDisableTiming));
@@ -1130,8 +1163,7 @@ struct HostPipe {
         return FMI_OK;
     }
     ~HostPipe() {
-        for (hipStream_t st : {cs, h2d, d2h})
-            if (st) (void)hipStreamDestroy(st);
+        if (cs) (void)hipStreamDestroy(cs);
         for (int k = 0; k < 2; ++k)
             for (hipEvent_t ev : {loaded[k], reduced[k], drained[k]})
                 if (ev) (void)hipEventDestroy(ev);
@@ -1256,11 +1288,16 @@ struct Comm {
             // be referenced by work that never drained: free only if everything drained within a bound,
             // otherwise leak it (and the streams) rather than free memory a kernel may still touch.
             bool drained = Transport::drain(library_stream(), 10.0);
-            for (hipStream_t st : {pipe.cs, pipe.h2d, pipe.d2h, chunks.gs})
+            for (hipStream_t st : {pipe.cs, chunks.gs})
                 if (st) drained = Transport::drain(st, 10.0) && drained;
+            // the shared copy streams carry other communicators' chunks too: only this one's copies are waited for
+            for (int k = 0; k < 2; ++k)
+                for (hipEvent_t ev : {pipe.loaded[k], pipe.drained[k]})
+                    if (ev) drained = Transport::drain_event(ev, 10.0) && drained;
             for (auto& [st, ev] : user_tail) drained = Transport::drain_event(ev, 10.0) && drained;
             if (!drained) {
-                pipe.cs = pipe.h2d = pipe.d2h = chunks.gs = nullptr;
+                pipe.cs = chunks.gs = nullptr;
+                for (int k = 0; k < 2; ++k) pipe.loaded[k] = pipe.reduced[k] = pipe.drained[k] = nullptr;
                 for (void*& b : buf) b = nullptr;
                 windows.clear();
                 return;
@@ -1276,6 +1313,9 @@ struct Comm {
             return;
         }
         if (pipe.cs) (void)hipStreamSynchronize(pipe.cs);
+        for (int k = 0; k < 2; ++k)
+            for (hipEvent_t ev : {pipe.loaded[k], pipe.drained[k]})
+                if (ev) (void)hipEventSynchronize(ev);
         if (chunks.gs) (void)hipStreamSynchronize(chunks.gs);
         for (auto& [st, ev] : user_tail) {
             (void)hipEventSynchronize(ev);
@@ -1832,7 +1872,7 @@ static int comm_allreduce_impl(fmi_comm_t comm, int op, int dtype, int alg, int 
 }
 
 // Three-stage pipeline over two chunk slots: while chunk k is allreduced on pipe.cs, chunk k+1 loads on
-// pipe.h2d and chunk k-1 drains on pipe.d2h. Slot reuse is ordered by events: a load into slot j waits
+// pipe.h2d and chunk k-1 drains on pipe.d2h (the device's shared copy streams, shared_copy_streams). Slot reuse is ordered by events: a load into slot j waits
 // until the allreduce that read it has finished (reduced), an allreduce into slot j waits until the
 // previous result in it has drained to the host.
 static int comm_allreduce_host_impl(fmi_comm_t comm, int op, int dtype, int alg, int path, const void* send, void* recv,
@@ -1887,7 +1927,8 @@ static int comm_allreduce_host_impl(fmi_comm_t comm, int op, int dtype, int alg,
         FMI_COMM_HIP(hipMemcpyAsync(dst + k * chunk * esz, out[j], span(k) * esz, hipMemcpyDefault, p.d2h));
         FMI_COMM_HIP(hipEventRecord(p.drained[j], p.d2h));
     }
-    FMI_COMM_RC(c->t->wait_stream(p.d2h, "fmi_comm_allreduce_host"));
+    // this communicator's last result copy (the shared D2H stream may already carry other ranks' later chunks)
+    FMI_COMM_RC(c->t->wait_event(p.drained[(nchunks - 1) & 1], p.d2h, "fmi_comm_allreduce_host"));
     return c->t->wait_stream(p.cs, "fmi_comm_allreduce_host");
 }
 

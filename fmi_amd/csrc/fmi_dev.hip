@@ -2,6 +2,7 @@
 // pairwise hot kernel's launch policy, P-way dispatch, the host-ingress pipeline and synthetic buckets.
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -33,13 +34,17 @@ struct DeviceState {
 std::mutex g_mu;
 DeviceState g_state;  // one process drives one device (one process per GPU, as FMI runs one peer per process)
 
-// Host-ingress pipeline of fmi_host_reduce_pair: two slots of (a, b) device staging and two streams, one set PER
-// CALLING THREAD. The reference's peers combine concurrently when they are threads of one process (its
-// allreduce's peers each call f.f at once), and one shared pipeline serialised them: 2 / 4 threads took exactly
-// 2 / 4 x one combine (profiles/r04_host_pair_threads_shared.jsonl). A thread leases a set on its first call and
-// hands it back to the idle pool when it exits, so short-lived peer threads reuse sets instead of growing
-// device memory: at most one set per thread alive at once. fmi_dev_finalize frees every set; a lease is trusted
-// only for the generation it was taken in.
+// Host-ingress pipeline of fmi_host_reduce_pair: two slots of (a, b) device staging and two streams per SET. The
+// reference's peers combine concurrently when they are threads of one process (its allreduce's peers each call
+// f.f at once), and one shared set serialised them: 2 / 4 threads took exactly 2 / 4 x one combine
+// (profiles/r04_host_pair_threads_shared.jsonl). So a call leases a set from a per-process pool for its own
+// duration and hands it back when it returns (no per-thread state: the reference spawns threads per collective).
+// Bounded: at most kMaxHostPipes sets per device exist; a caller past the cap waits until a set comes
+// back (the PCIe link is saturated well before that many concurrent combines). A set's staging grows to the
+// largest chunk it has served, rounded up to a power of two and capped at the host chunk (FMI_TUNE_HOST_CHUNK):
+// small combines keep small staging. fmi_dev_finalize frees every set; it holds g_pipes_life exclusively, which
+// every call holds shared for its whole duration, so no lease is outstanding then.
+constexpr size_t kMaxHostPipes = 8;
 struct HostPipe {
     int device = -1;
     void* stage[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
@@ -55,12 +60,12 @@ struct HostPipe {
         *this = HostPipe{};
     }
 };
-std::shared_mutex g_pipes_life;  // shared by every fmi_host_reduce_pair in flight, exclusive in fmi_dev_finalize
-std::atomic<uint64_t> g_pipes_gen{1};
+std::shared_mutex g_pipes_life;  // shared by every fmi_host_reduce_pair in flight, exclusive in init / finalize
 struct PipeRegistry {
     std::mutex mu;
-    std::vector<std::unique_ptr<HostPipe>> all;  // every set of this generation (owning)
-    std::vector<HostPipe*> idle;                 // sets whose thread has exited
+    std::condition_variable back;                // a set came back to the pool
+    std::vector<std::unique_ptr<HostPipe>> all;  // every set (owning)
+    std::vector<HostPipe*> idle;                 // sets no call holds; most recently returned last
 };
 // Never destroyed: a thread still running while the process exits may hand its set back after static
 // destruction has begun.
@@ -69,43 +74,50 @@ PipeRegistry& pipes() {
     return *r;
 }
 
+// One call's set: leased on construction (waiting while the device's kMaxHostPipes sets are all in use), returned
+// to the pool on destruction. No HIP call on return: the call synchronised the set's streams before returning.
 struct PipeLease {
     HostPipe* p = nullptr;
-    uint64_t gen = 0;
-    ~PipeLease() {  // thread exit: no HIP call here, the set's work was synchronised before its last call returned
-        if (!p) return;
-        std::lock_guard<std::mutex> lk(pipes().mu);
-        if (gen == g_pipes_gen.load()) pipes().idle.push_back(p);
-    }
-};
-thread_local PipeLease t_lease;
-
-HostPipe* my_host_pipe() {
-    const uint64_t gen = g_pipes_gen.load();
-    if (t_lease.p && t_lease.gen == gen && t_lease.p->device == g_state.device) return t_lease.p;
-    PipeRegistry& reg = pipes();
-    std::lock_guard<std::mutex> lk(reg.mu);
-    if (t_lease.p && t_lease.gen == gen) reg.idle.push_back(t_lease.p);  // another device's set: back to the pool
-    HostPipe* got = nullptr;
-    for (size_t i = 0; i < reg.idle.size(); ++i)
-        if (reg.idle[i]->device == g_state.device) {
-            got = reg.idle[i];
-            reg.idle.erase(reg.idle.begin() + static_cast<std::ptrdiff_t>(i));
-            break;
+    explicit PipeLease(int device) {
+        PipeRegistry& reg = pipes();
+        std::unique_lock<std::mutex> lk(reg.mu);
+        for (;;) {
+            for (size_t i = reg.idle.size(); i-- > 0;)
+                if (reg.idle[i]->device == device) {
+                    p = reg.idle[i];
+                    reg.idle.erase(reg.idle.begin() + static_cast<std::ptrdiff_t>(i));
+                    return;
+                }
+            size_t mine = 0;
+            for (auto& q : reg.all) mine += q->device == device;
+            if (mine < kMaxHostPipes) {
+                reg.all.push_back(std::make_unique<HostPipe>());
+                p = reg.all.back().get();
+                p->device = device;
+                return;
+            }
+            reg.back.wait(lk);
         }
-    if (!got) {
-        reg.all.push_back(std::make_unique<HostPipe>());
-        got = reg.all.back().get();
-        got->device = g_state.device;
     }
-    t_lease.p = got;
-    t_lease.gen = gen;
-    return got;
-}
+    ~PipeLease() {
+        PipeRegistry& reg = pipes();
+        {
+            std::lock_guard<std::mutex> lk(reg.mu);
+            reg.idle.push_back(p);
+        }
+        reg.back.notify_one();
+    }
+    PipeLease(const PipeLease&) = delete;
+    PipeLease& operator=(const PipeLease&) = delete;
+};
 
-size_t host_pipe_count(size_t* idle) {
+size_t host_pipe_count(size_t* idle, size_t* staging_bytes) {
     std::lock_guard<std::mutex> lk(pipes().mu);
     if (idle) *idle = pipes().idle.size();
+    if (staging_bytes) {
+        *staging_bytes = 0;
+        for (auto& p : pipes().all) *staging_bytes += 4 * p->stage_bytes;
+    }
     return pipes().all.size();
 }
 
@@ -879,6 +891,7 @@ int fmi_dev_init(int device) {
     FMI_HIP_TRY(hipSetDevice(device));
     hipStream_t s = nullptr;
     FMI_HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    std::unique_lock<std::shared_mutex> life(g_pipes_life);  // fmi_host_reduce_pair reads g_state under it, shared
     g_state.device = device;
     g_state.num_cus = prop.multiProcessorCount;
     g_state.lds_per_cu = prop.maxSharedMemoryPerMultiProcessor;
@@ -892,13 +905,14 @@ int fmi_dev_finalize(void) {
     if (g_state.device < 0) return FMI_OK;
     (void)hipSetDevice(g_state.device);
     (void)hipDeviceSynchronize();
+    // exclusive: no fmi_host_reduce_pair is in flight (each holds it shared throughout), and none starts until
+    // g_state says there is no device
+    std::unique_lock<std::shared_mutex> life(g_pipes_life);
     {
-        std::unique_lock<std::shared_mutex> life(g_pipes_life);
         std::lock_guard<std::mutex> lk(pipes().mu);
         for (auto& p : pipes().all) p->release();
         pipes().all.clear();
         pipes().idle.clear();
-        g_pipes_gen.fetch_add(1);
     }
     if (g_state.arena) (void)hipFree(g_state.arena);
     if (g_state.arena_free) (void)hipEventDestroy(g_state.arena_free);
@@ -920,9 +934,10 @@ int fmi_dev_describe(char* buf, size_t len) {
     FMI_HIP_TRY(hipGetDeviceProperties(&prop, g_state.device));
     std::string d = std::string(prop.name) + " " + prop.gcnArchName + " CUs=" + std::to_string(prop.multiProcessorCount) +
                     " HBM=" + std::to_string(prop.totalGlobalMem >> 20) + "MiB";
-    size_t idle = 0;
-    const size_t pipes = host_pipe_count(&idle);  // fmi_host_reduce_pair's per-thread staging sets
-    d += " host_pipelines=" + std::to_string(pipes) + " idle=" + std::to_string(idle);
+    size_t idle = 0, staging = 0;
+    const size_t pipes = host_pipe_count(&idle, &staging);  // fmi_host_reduce_pair's pooled staging sets
+    d += " host_pipelines=" + std::to_string(pipes) + " idle=" + std::to_string(idle) +
+         " host_staging_bytes=" + std::to_string(staging) + " host_pipelines_max=" + std::to_string(kMaxHostPipes);
     std::snprintf(buf, len, "%s", d.c_str());
     return FMI_OK;
 }
@@ -1286,7 +1301,10 @@ int fmi_host_reduce_pair(int op, int dtype, void* inout, const void* in, size_t 
                                          "(pin or register the whole bucket, or none of it)");
     }
     std::shared_lock<std::shared_mutex> life(g_pipes_life);
-    HostPipe& hp = *my_host_pipe();  // this thread's streams and staging: concurrent callers do not serialise
+    const int device = g_state.device;  // read under the lock: a finalize between require_device() and here
+    if (device < 0) return fail(FMI_ERR_NO_DEVICE, "fmi_dev_finalize ran before this fmi_host_reduce_pair started");
+    PipeLease lease(device);  // this call's streams and staging: concurrent callers do not serialise (up to the cap)
+    HostPipe& hp = *lease.p;
     for (int k = 0; k < 2; ++k)
         if (!hp.pipe[k]) FMI_HIP_TRY(hipStreamCreateWithFlags(&hp.pipe[k], hipStreamNonBlocking));
     if (g_tune[FMI_TUNE_HOST_ZERO_COPY].load()) {
@@ -1305,7 +1323,11 @@ int fmi_host_reduce_pair(int op, int dtype, void* inout, const void* in, size_t 
     size_t chunk_elems = static_cast<size_t>(std::max<long long>(g_tune[FMI_TUNE_HOST_CHUNK].load(), 1 << 16)) / esz;
     chunk_elems = std::max<size_t>(16, chunk_elems / 16 * 16);
     const size_t chunk_bytes = chunk_elems * esz;
-    if (hp.stage_bytes < chunk_bytes) {
+    // this call's largest chunk, rounded up to a power of two (>= 64 KiB), never above the tuned chunk
+    size_t need = 64 << 10;
+    while (need < std::min(chunk_bytes, n * esz)) need <<= 1;
+    need = std::min(need, chunk_bytes);
+    if (hp.stage_bytes < need) {
         for (int k = 0; k < 2; ++k) FMI_HIP_TRY(hipStreamSynchronize(hp.pipe[k]));
         for (int k = 0; k < 2; ++k)
             for (int j = 0; j < 2; ++j) {
@@ -1314,13 +1336,13 @@ int fmi_host_reduce_pair(int op, int dtype, void* inout, const void* in, size_t 
             }
         for (int k = 0; k < 2; ++k)
             for (int j = 0; j < 2; ++j) {
-                const hipError_t e = hipMalloc(&hp.stage[k][j], chunk_bytes);
+                const hipError_t e = hipMalloc(&hp.stage[k][j], need);
                 if (e != hipSuccess) {
                     hp.stage_bytes = 0;
                     return fail(FMI_ERR_ALLOC, std::string("hipMalloc (host pipeline staging): ") + hipGetErrorString(e));
                 }
             }
-        hp.stage_bytes = chunk_bytes;
+        hp.stage_bytes = need;
     }
     char* hx = static_cast<char*>(inout);
     const char* hy = static_cast<const char*>(in);

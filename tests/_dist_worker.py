@@ -140,7 +140,8 @@ def run_fall_back(rank, world, port, failing_rank, outdir):
             Comm.destroyed = True
 
     err = f"RuntimeError: rank {rank} broke" if rank == failing_rank else None
-    fell = bench._fall_back(None, world, rank, Watch(), 0, {}, Comm(), err, "the fmi_comm allreduce")
+    vote = dist.new_group(backend="gloo")  # bench.run_dist votes on a gloo group of its own
+    fell = bench._fall_back(None, world, rank, Watch(), 0, {}, Comm(), err, "the fmi_comm allreduce", group=vote)
     with open(os.path.join(outdir, f"fall{rank}.json"), "w") as f:
         json.dump({"fell": fell, "calls": calls, "destroyed": Comm.destroyed}, f)
     dist.destroy_process_group()

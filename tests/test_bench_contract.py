@@ -340,3 +340,38 @@ def test_c5_size_follows_mem_available():
     assert bench.c5_size_mib(8, 1024, 32 * G) == 1024  # 16 + 16 fits exactly
     assert bench.c5_size_mib(8, 1024, 31 * G) == 512
     assert bench.c5_size_mib(8, 1024, 20 * G) == 256
+
+
+def _light_cpu_baseline(monkeypatch):
+    for name in ("c1_host", "c1_reference", "c3_cpu", "c4_reference"):
+        monkeypatch.setattr(bench, name, lambda *a, **k: None)
+    monkeypatch.setattr(bench, "c2_reference", lambda *a, **k: None)
+    import argparse
+
+    return argparse.Namespace(bucket_mib=4, cpu_reps=3)
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(ROOT, "oracle", "build", "cpu_baseline")),
+                    reason="oracle/build/cpu_baseline not built (__graft_entry__.build())")
+def test_cpu_baseline_value_is_the_reference_combine(monkeypatch):
+    """the stated CPU baseline is the reference's own adapter combine (oracle/_ref), the
+    port beside it as port_value; value = bucket / reference ms."""
+    from oracle import fmi_ref
+
+    if not fmi_ref.available():
+        pytest.skip("oracle/_ref not built")
+    got = bench.cpu_baseline(_light_cpu_baseline(monkeypatch))
+    assert got["kind"] == "reference" and got["cores"] == 1 and got["unit"] == "GiB/s"
+    assert got["value"] == pytest.approx(4 / 1024 / (got["reference_combine_ms"] * 1e-3), rel=1e-3)
+    assert got["port_value"] > 0 and got["port_combine_ms"] > 0
+    assert got["reference_over_port"] == pytest.approx(got["reference_combine_ms"] / got["port_combine_ms"], rel=1e-2)
+    assert "reference's own adapter combine" in got["sample"]
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(ROOT, "oracle", "build", "cpu_baseline")),
+                    reason="oracle/build/cpu_baseline not built (__graft_entry__.build())")
+def test_cpu_baseline_falls_back_to_the_port_only_without_oracle_ref(monkeypatch):
+    monkeypatch.setattr(bench, "reference_combine_ms", lambda n, reps: (None, "oracle/_ref not built"))
+    got = bench.cpu_baseline(_light_cpu_baseline(monkeypatch))
+    assert got["kind"] == "port" and got["value"] == got["port_value"] and got["reference_combine_ms"] is None
+    assert got["reference_error"] == "oracle/_ref not built"

@@ -54,3 +54,15 @@ def test_cited_paths_exist(doc):
             continue
         missing.append(p)
     assert not missing, f"{doc} cites paths that do not exist: {sorted(set(missing))}"
+
+
+DRIVER = re.compile(r"(?<![\w/.])((?:BENCH|GPUTEST|SCALE|MULTICHIP)_r\d\d\.json)")
+
+
+@pytest.mark.parametrize("doc", DOCS)
+def test_cited_driver_records_exist(doc):
+    """every driver record a document cites (BENCH_r0N.json, GPUTEST_r0N.json, SCALE_…,
+    MULTICHIP_…) is in the tree; a result quoted from a record that is not there cannot be checked."""
+    text = open(os.path.join(ROOT, doc), encoding="utf-8").read()
+    missing = sorted({r for r in DRIVER.findall(text) if not os.path.exists(os.path.join(ROOT, r))})
+    assert not missing, f"{doc} cites driver records that do not exist: {missing}"

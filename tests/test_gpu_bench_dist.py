@@ -88,6 +88,7 @@ def test_bench_py_proc_transport(world):
 
 def _check_topology_and_anchor(line, world, transport):
     assert line["workload"] == "sharded_allreduce", line.get("workload")
+    assert line["exchange"] == "fmi_comm", line.get("exchange")  # whose exchange `value` measured
     topo = line["config"]["topology"]
     assert topo["ok"] and topo["transport"] == transport and len(topo["ranks"]) == world, topo
     rt = topo["runtime"]  # the librccl and visibility environment the run used
@@ -178,28 +179,38 @@ def test_bench_py_error_line_names_the_runtime():
     assert len(lines) == 1, r.stdout + r.stderr[-3000:]
     line = json.loads(lines[0])
     assert line["value"] is None and line["workload"] == "sharded_allreduce", line
+    assert line["exchange"] == "fmi_comm", line
     assert line["phase"] == "topology check" and "injected failure" in line["error"], line
     rt = line["runtime"]
     assert rt["rccl_version"] > 0 and "librccl" in rt["rccl_path"] and "HIP_VISIBLE_DEVICES" in rt, rt
 
 
-@pytest.mark.parametrize("phase", ["fmi_comm init", "warm-up and timed allreduces"])
-def test_bench_py_falls_back_to_torch_exchange_when_fmi_comm_fails(phase):
+@pytest.mark.parametrize("phase,allow", [("fmi_comm init", False), ("warm-up and timed allreduces", True)])
+def test_bench_py_falls_back_to_torch_exchange_when_fmi_comm_fails(phase, allow):
     """If the product communicator cannot be built over RCCL, or fails in its first allreduces
-    (FMI_BENCH_TEST_RAISE_IN injects the failure in that phase, on every rank), bench.py still measures the same sharded allreduce — the fused tree kernel of
-    libfmi_dev.so on every shard, the two exchanges through torch.distributed's own RCCL group — self-checks it
-    bit-exact, and names the reason in config.exchange_fallback. World size 1 with --force-dist: the exchange
-    runs with itself."""
+    (FMI_BENCH_TEST_RAISE_IN injects the failure in that phase, on every rank), bench.py still measures the same
+    sharded allreduce — the fused tree kernel of libfmi_dev.so on every shard, the two exchanges through
+    torch.distributed's own RCCL group — self-checks it bit-exact, and names the reason in config.exchange_fallback
+    and `exchange: torch_fallback` at top level. By default the product failed, so `value` is null, the rate is
+    `fallback_value` and the run exits 1; --allow-exchange-fallback reports it as `value` and exits 0.
+    World size 1 with --force-dist: the exchange runs with itself."""
     env = dict(os.environ, OMP_NUM_THREADS="1", FMI_BENCH_TEST_RAISE_IN=phase)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--force-dist",
            "--steps", "4", "--warmup", "1", "--dist-sets", "2", "--bucket-mib", "8", "--no-diagnostics"]
+    if allow:
+        cmd.append("--allow-exchange-fallback")
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=240, env=env)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert (r.returncode == 0) == allow, r.stdout[-3000:] + r.stderr[-3000:]
     lines = r.stdout.strip().splitlines()
     assert len(lines) == 1, r.stdout
     line = json.loads(lines[0])
-    assert line["value"] > 0 and line["workload"] == "sharded_allreduce", line
+    assert line["exchange"] == "torch_fallback", line
+    if allow:
+        assert line["value"] > 0 and "fallback_value" not in line, line
+    else:
+        assert line["value"] is None and line["fallback_value"] > 0, line
+    assert line["workload"] == "sharded_allreduce", line
     fb = line["config"]["exchange_fallback"]
     assert "injected failure" in fb["reason"] and "torch.distributed" in fb["exchange"], fb
     chk = line["self_check"]

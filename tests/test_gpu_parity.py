@@ -770,10 +770,18 @@ def _host_pipelines():
     return int(m.group(1)), int(m.group(2))
 
 
+def _host_staging():
+    import re
+
+    m = re.search(r"host_staging_bytes=(\d+) host_pipelines_max=(\d+)", fmi_amd.describe())
+    assert m, fmi_amd.describe()
+    return int(m.group(1)), int(m.group(2))
+
+
 def test_host_reduce_pair_short_lived_threads_reuse_staging(device):
-    """The reference spawns a thread per peer for every collective; each calling thread leases a staging set,
-    and an exited thread's set returns to the pool: 40 waves of 4 short-lived threads leave at most the sets
-    that were alive at once (not 160), and every combine is bit-exact."""
+    """The reference spawns a thread per peer for every collective; each call leases a staging set and returns it
+    to the pool: 40 waves of 4 short-lived threads leave at most the pool's cap of sets (not 160), and every
+    combine is bit-exact."""
     import threading
 
     old = fmi_amd.tune_get(Tune.HOST_CHUNK)
@@ -791,12 +799,60 @@ def test_host_reduce_pair_short_lived_threads_reuse_staging(device):
         assert not errors, errors
         import time
 
-        time.sleep(0.5)  # Thread.join returns before the OS thread runs its C++ thread_local destructors
         after, idle = _host_pipelines()
-        # 4 alive at once, plus the sets of a wave whose OS threads had not quite exited when the next started
-        assert after - before <= 12 and idle >= 1, (before, after, idle)
+        _, cap = _host_staging()
+        assert after <= cap and after - before <= 4 and idle == after, (before, after, idle, cap)
     finally:
         fmi_amd.tune_set(Tune.HOST_CHUNK, old)
+
+
+_MANY_SMALL_SCRIPT = """
+import sys, threading, re
+sys.path.insert(0, {root!r})
+import numpy as np
+import fmi_amd
+from fmi_amd import Op
+fmi_amd.init(0)
+n = (256 << 10) // 4  # 256 KiB pageable buckets: staged, one chunk each
+T = 48
+start = threading.Barrier(T)
+bad = []
+def body(t):
+    rng = np.random.default_rng(t)
+    a, b = rng.random(n, dtype=np.float32), rng.random(n, dtype=np.float32)
+    start.wait()
+    for r in range(5):
+        got = a.copy()
+        fmi_amd.host_reduce_pair(Op.SUM, got, b)
+        if not np.array_equal(got, a + b):
+            bad.append((t, r))
+ts = [threading.Thread(target=body, args=(t,)) for t in range(T)]
+[x.start() for x in ts]
+[x.join(timeout=120) for x in ts]
+assert not any(x.is_alive() for x in ts), "a caller did not finish"
+assert not bad, bad
+d = fmi_amd.describe()
+sets = int(re.search(r"host_pipelines=(\\d+)", d).group(1))
+staging = int(re.search(r"host_staging_bytes=(\\d+)", d).group(1))
+cap = int(re.search(r"host_pipelines_max=(\\d+)", d).group(1))
+print("sets", sets, "staging", staging, "cap", cap)
+assert 1 <= sets <= cap, d
+assert staging <= sets * 4 * (256 << 10), d  # each set's 4 buffers sized to the 256 KiB bucket, not the 64 MiB chunk
+print("ok")
+"""
+
+
+def test_host_reduce_pair_pool_is_bounded_for_many_small_callers(device):
+    """48 threads making small pageable combines at once (the reference's peers as threads) share at
+    most the pool's cap of staging sets, each sized to the bucket rather than the 64 MiB host chunk, and every
+    combine is bit-exact. In a child process, so the set count starts from zero."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", _MANY_SMALL_SCRIPT.format(root=root)], capture_output=True, text=True,
+                       timeout=240, cwd=root)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout[-2000:] + r.stderr[-4000:]
 
 
 _REINIT_SCRIPT = """
@@ -818,9 +874,8 @@ print("ok")
 
 
 def test_host_reduce_pair_pipelines_survive_reinit(device):
-    """fmi_dev_finalize frees every thread's pipeline; a thread that combined before it gets a fresh one after
-    fmi_dev_init (its cached pointer belongs to the old generation). In a child process, so the session's
-    device state is left alone."""
+    """fmi_dev_finalize frees every pooled pipeline; calls after fmi_dev_init lease fresh ones. In a child process,
+    so the session's device state is left alone."""
     import subprocess
     import sys
 

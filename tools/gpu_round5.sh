@@ -1,0 +1,57 @@
+# Round 5's GPU calls, by step (profiles/INDEX.md names the files each made):
+#   bash tools/gpu_round5.sh a   C5's co-resident DMA ceiling by issue shape (tools/microbench_pcie_peers.hip: own vs
+#                                shared streams, SDMA vs kernel copies, 1 / 2 / 8 peers), the host-combine crossover
+#                                (tools/host_crossover.py), the counters this rocprofv3 offers, and the fused 8-way
+#                                allreduce at 256 / 512 / 1024 MiB per peer under a kernel trace (tools/tree8_shapes.py)
+#   bash tools/gpu_round5.sh b   the same three tree shapes under seven separate --pmc passes (read / write request
+#                                levels and DRAM credit stalls, translation, TA / SQ stalls, FETCH_SIZE, WRITE_SIZE)
+#   bash tools/gpu_round5.sh c   the pooled fmi_host_reduce_pair staging and the shared per-device copy streams of
+#                                fmi_comm_allreduce_host: the whole GPU suite, C5's p1_copy + local_peers blocks, and the
+#                                host-combine crossover to 512 MiB (profiles/r05_c_*, r05_c5_blocks.json)
+set -o pipefail
+cd /root/repo
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+case "$1" in
+a)
+    timeout -k 10 240 build/mbpciepeers 3 0 > gpurun_out/r05_pcie_peers.jsonl 2> gpurun_out/r05_pcie_peers.err &&
+    timeout -k 10 240 build/mbpciepeers 3 6 >> gpurun_out/r05_pcie_peers.jsonl 2>> gpurun_out/r05_pcie_peers.err &&
+    timeout -k 10 200 python -u tools/host_crossover.py > gpurun_out/r05_host_crossover.jsonl 2> gpurun_out/r05_host_crossover.err &&
+    timeout -k 10 120 rocprofv3 -L > gpurun_out/r05_rocprofv3_counters.txt 2>&1 &&
+    timeout -k 10 200 python -u tools/tree8_shapes.py --mib 256,512,1024,512,256 > gpurun_out/r05_tree8_events.jsonl &&
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r05_tree8_trace -o run -- \
+        python3 tools/tree8_shapes.py --mib 256,512,1024 > gpurun_out/r05_tree8_under_trace.jsonl 2> gpurun_out/r05_tree8_trace.err
+    ;;
+b)
+    # one --pmc pass per counter group (MI355X_MICROARCH.md: separate passes, <= 4 TCC / 4 TCP / 2 TA / 2 GRBM / 8 SQ)
+    R=$PWD
+    cd /tmp
+    k=0
+    for pmc in "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_LEVEL_sum TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum TCC_TAG_STALL_sum GRBM_GUI_ACTIVE" \
+               "TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_LEVEL_sum TCC_EA0_WRREQ_DRAM_CREDIT_STALL_sum TCC_EA0_WRREQ_STALL_sum GRBM_GUI_ACTIVE" \
+               "TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_UTCL1_STALL_MULTI_MISS_sum TCP_PENDING_STALL_CYCLES_sum GRBM_UTCL2_BUSY GRBM_GUI_ACTIVE" \
+               "TA_DATA_STALLED_BY_TC_CYCLES_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAVES GRBM_GUI_ACTIVE" \
+               "FETCH_SIZE" "WRITE_SIZE" "TCC_EA0_RDREQ_DRAM_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_64B_sum TCC_BUSY_sum"; do
+        k=$((k + 1))
+        timeout -s KILL 120 rocprofv3 --pmc $pmc --kernel-trace --output-format csv -d $R/gpurun_out/r05_tree8_pmc$k -o run -- \
+            python3 $R/tools/tree8_shapes.py --mib 256,512,1024 > $R/gpurun_out/r05_tree8_pmc$k.jsonl 2> $R/gpurun_out/r05_tree8_pmc$k.err || exit 1
+    done
+    ;;
+c)
+    # the pooled host-combine staging and the shared per-device copy streams: their GPU tests, C5's blocks, the
+    # crossover sweep to 512 MiB
+    timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider \
+        > gpurun_out/r05_c_full_gpu.log 2>&1 &&
+    timeout -k 10 300 python -u -c "
+import json, bench, fmi_amd
+fmi_amd.init(0)
+bench.quiet_device()
+print(json.dumps({'p1_copy': bench.c5_p1_copy(1024), 'local_peers': bench.c5_local_peers(8, 1024)}))
+" > gpurun_out/r05_c5_blocks.json 2> gpurun_out/r05_c5_blocks.err &&
+    timeout -k 10 300 python -u tools/host_crossover.py > gpurun_out/r05_host_crossover_512.jsonl 2> gpurun_out/r05_host_crossover_512.err
+    ;;
+*)
+    echo "usage: bash tools/gpu_round5.sh a|b|c" >&2
+    exit 2
+    ;;
+esac
