@@ -477,6 +477,18 @@ def _error_line(world, error, phase, **extra):
     return line
 
 
+def placement() -> str:
+    """How the line's device buckets are placed: fmi_dev_alloc's rotating 4 KiB slots, or plain."""
+    try:
+        import fmi_amd
+
+        on = fmi_amd.tune_get(fmi_amd.Tune.ALLOC_SLOTS)
+    except Exception as e:  # reported, never required
+        return f"unknown ({type(e).__name__}: {e})"
+    return ("fmi_dev_alloc: every bucket of >= 1 MiB in the next of 16 rotating 4 KiB slots (mod 64 KiB) of its own "
+            "hipMalloc (FMI_TUNE_ALLOC_SLOTS = 1)" if on else "fmi_dev_alloc: plain hipMalloc (FMI_TUNE_ALLOC_SLOTS = 0)")
+
+
 def _headline(args, value, step_ms, workload, parallelism, n, roofline):
     return {
         "metric": METRIC,
@@ -493,7 +505,7 @@ def _headline(args, value, step_ms, workload, parallelism, n, roofline):
         "dtype": "f32",
         "data": "synthetic (splitmix64 counter generator, SURVEY.md §8d), device-resident in HBM",
         "config": {"workload": workload, "bucket_mib": args.bucket_mib, "elements": n, "parallelism": parallelism,
-                   "rotating_sets": args.sets},
+                   "rotating_sets": args.sets, "placement": placement()},
         "roofline": roofline,
     }
 
@@ -1049,7 +1061,7 @@ def c5_size_mib(peers: int, mib: int, avail) -> int:
     return size
 
 
-def c5_local_peers(peers: int, mib: int, iters: int = 2) -> dict:
+def c5_local_peers(peers: int, mib: int, iters: int = 2, chunk_mib: int = 64) -> dict:
     """C5's workload on ONE GPU: `peers` LOCAL ranks (threads of this process), each with a page-locked f32
     bucket of `mib` (1 GiB: 8 GiB in, 8 GiB out over this GPU's one PCIe link), fmi_comm_allreduce_host with
     64 MiB chunks. Per iteration every rank starts at a barrier; the iteration's time is the slowest rank's;
@@ -1085,7 +1097,7 @@ def c5_local_peers(peers: int, mib: int, iters: int = 2) -> dict:
                     for k in range(iters + 1):
                         bar.wait(timeout=300)
                         t0 = time.perf_counter()
-                        c.allreduce_host(Op.SUM, send[r].array, recv[r].array, chunk=64 * MIB // 4)
+                        c.allreduce_host(Op.SUM, send[r].array, recv[r].array, chunk=chunk_mib * MIB // 4)
                         times[r][k] = time.perf_counter() - t0
                 finally:
                     c.destroy()
@@ -1120,8 +1132,8 @@ def c5_local_peers(peers: int, mib: int, iters: int = 2) -> dict:
     ms = statistics.median(per_iter) * 1e3
     S = n * 4
     return {"workload": f"C5 on one GPU: {peers} LOCAL ranks x {size} MiB f32 page-locked host buckets, "
-                        "fmi_comm_allreduce_host (H2D + sharded allreduce + D2H pipelined, 64 MiB chunks)",
-            "peers": peers, "bucket_mib": size, "requested_bucket_mib": mib,
+                        f"fmi_comm_allreduce_host (H2D + sharded allreduce + D2H pipelined, {chunk_mib} MiB chunks)",
+            "peers": peers, "chunk_mib": chunk_mib, "bucket_mib": size, "requested_bucket_mib": mib,
             "mem_available_gib": round(avail / GIB, 1) if avail else None,
             "ms": round(ms, 2), "host_buckets_GiB_s": round(peers * S / GIB / (ms * 1e-3), 2),
             "pcie_GB_s_both_directions": round(2 * peers * S / (ms * 1e-3) / 1e9, 1), "iters": iters,
@@ -1434,6 +1446,9 @@ def run_dist_torch_exchange(args, world, rank, watch, comm_err, numa):
                            "shard_elems": shard})
     line["config"]["exchange_fallback"] = {
         "reason": comm_err,
+        "parity": ("unpinned at N > 1: this fallback's self-check (check_windows, every rank, bit-exact against the "
+                   "single-GPU kernel) has run on hardware only at world size 1 (--force-dist); no multi-GPU run of it "
+                   "exists yet") if world > 1 else "self-checked at world size 1",
         "exchange": "torch.distributed all_to_all_single + all_gather_into_tensor on torch's RCCL process group "
                     "(fmi_amd.collectives.ShardedAllreduce); the shard kernel is libfmi_dev.so's fused tree kernel"}
     line["self_check"] = check

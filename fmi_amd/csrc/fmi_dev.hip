@@ -4,6 +4,7 @@
 #include <atomic>
 #include <condition_variable>
 #include <cstring>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <shared_mutex>
@@ -32,7 +33,21 @@ struct DeviceState {
 };
 
 std::mutex g_mu;
-DeviceState g_state;  // one process drives one device (one process per GPU, as FMI runs one peer per process)
+DeviceState g_state;
+
+// Bucket placement (fmi_dev_alloc, round 5). A fused kernel reads its P buckets at the same offset at the same time.
+// Separate hipMallocs of large buckets start on 2 MiB boundaries, so those P streams sit at the same offset modulo
+// every HBM interleave period below 2 MiB, and they collide: the 8-way tree at 512 MiB per peer ran 0.71 of peak on
+// separate allocations, 0.62 with the buckets packed back to back, and 0.83 with bucket j shifted by j x 4 KiB
+// (profiles/r05_skew_sweep.jsonl, tools/skew_sweep.py; the C3 scan 0.75 -> 0.80, the N = 8 shard shape 0.73 ->
+// 0.79; the pair and copy kernels, 2-3 streams, within 1 %). Shifts of 16, 32 or 64 KiB collide again: what counts
+// is a distinct 4 KiB slot modulo 64 KiB for each stream. So every allocation of >= 1 MiB is placed at the next of
+// 16 such slots inside a hipMalloc 64 KiB larger: any 16 buckets allocated one after another (a fused kernel's
+// inputs and outputs, up to 8 in + 8 out) sit in distinct slots. FMI_TUNE_ALLOC_SLOTS = 0 turns it off.
+constexpr size_t kSlotBytes = 4096, kSlots = 16, kSlotSpan = kSlotBytes * kSlots, kSlotMinBytes = size_t(1) << 20;
+std::mutex g_slots_mu;
+size_t g_next_slot = 0;
+std::map<void*, void*> g_slotted;  // pointer handed out -> its hipMalloc base  // one process drives one device (one process per GPU, as FMI runs one peer per process)
 
 // Host-ingress pipeline of fmi_host_reduce_pair: two slots of (a, b) device staging and two streams per SET. The
 // reference's peers combine concurrently when they are threads of one process (its allreduce's peers each call
@@ -123,13 +138,14 @@ size_t host_pipe_count(size_t* idle, size_t* staging_bytes) {
 
 // Defaults from tools/tune_pair.py on MI355X (C2, 256 MiB f32): nontemporal one-shot tiles, 4 × 16 B per
 // operand per thread, 256-thread workgroups — 125 µs = 6.4 TB/s vs 142 µs for plain loads/stores.
-std::atomic<long long> g_tune[14] = {2 /*variant: nontemporal tiles*/, 4 /*unroll*/, 256 /*block*/,
+std::atomic<long long> g_tune[15] = {2 /*variant: nontemporal tiles*/, 4 /*unroll*/, 256 /*block*/,
                                      8 /*grid per CU*/, 64ll << 20 /*host chunk*/, 1 /*host zero-copy*/,
                                      64 /*fused in-flight KiB per CU (tools/ab_fused_cap.py)*/,
                                      1 /*one-pass blocked scan*/, 0 /*ncclAllToAll*/, 0 /*ncclAllGather*/,
                                      0 /*no allreduce pipelining*/, 1 /*fused kernels: buffer ops where measured faster*/,
                                      1 /*pairwise: tiles t % 8 < 1 (one XCD) store sc1 (tools/ab_pair_sc1.py)*/,
-                                     0 /*one-rank communicators copy*/};
+                                     0 /*one-rank communicators copy*/,
+                                     1 /*bucket allocations rotate over 16 4-KiB slots (profiles/r05_skew_sweep.jsonl)*/};
 
 int hip_fail(const char* what, hipError_t e) {
     return fail(FMI_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
@@ -957,15 +973,34 @@ int fmi_dev_pci_bus_id(int device, char* buf, size_t len) {
 int fmi_dev_alloc(void** ptr, size_t bytes) {
     if (!ptr) return fail(FMI_ERR_INVALID, "ptr is null");
     if (int rc = require_device()) return rc;
-    const hipError_t e = hipMalloc(ptr, std::max<size_t>(bytes, 1));
+    const bool slotted = bytes >= kSlotMinBytes && g_tune[FMI_TUNE_ALLOC_SLOTS].load() != 0;
+    void* base = nullptr;
+    const hipError_t e = hipMalloc(&base, std::max<size_t>(bytes, 1) + (slotted ? kSlotSpan : 0));
     if (e != hipSuccess) return fail(FMI_ERR_ALLOC, "hipMalloc(" + std::to_string(bytes) + "): " + hipGetErrorString(e));
+    if (!slotted) {
+        *ptr = base;
+        return FMI_OK;
+    }
+    std::lock_guard<std::mutex> lk(g_slots_mu);
+    char* p = static_cast<char*>(base) + (g_next_slot++ % kSlots) * kSlotBytes;
+    g_slotted[p] = base;
+    *ptr = p;
     return FMI_OK;
 }
 
 int fmi_dev_free(void* ptr) {
     if (!ptr) return FMI_OK;
     if (int rc = require_device()) return rc;
-    FMI_HIP_TRY(hipFree(ptr));
+    void* base = ptr;
+    {
+        std::lock_guard<std::mutex> lk(g_slots_mu);
+        auto it = g_slotted.find(ptr);
+        if (it != g_slotted.end()) {
+            base = it->second;
+            g_slotted.erase(it);
+        }
+    }
+    FMI_HIP_TRY(hipFree(base));
     return FMI_OK;
 }
 
@@ -1456,6 +1491,9 @@ int fmi_tune_set(int key, long long value) {
         case FMI_TUNE_COMM_ONE_RANK_EXCHANGE:
             if (value != 0 && value != 1) return fail(FMI_ERR_INVALID, "one-rank exchange must be 0 or 1");
             break;
+        case FMI_TUNE_ALLOC_SLOTS:
+            if (value != 0 && value != 1) return fail(FMI_ERR_INVALID, "allocation slots must be 0 or 1");
+            break;
         default: return fail(FMI_ERR_INVALID, "unknown tuning key");
     }
     g_tune[key].store(value);
@@ -1463,7 +1501,7 @@ int fmi_tune_set(int key, long long value) {
 }
 
 int fmi_tune_get(int key, long long* value) {
-    if (!value || key < 0 || key > FMI_TUNE_COMM_ONE_RANK_EXCHANGE) return fail(FMI_ERR_INVALID, "bad tuning query");
+    if (!value || key < 0 || key > FMI_TUNE_ALLOC_SLOTS) return fail(FMI_ERR_INVALID, "bad tuning query");
     *value = g_tune[key].load();
     return FMI_OK;
 }

@@ -102,7 +102,10 @@ int fmi_dev_describe(char* buf, size_t len);
  * fmi_comm_query, lets the ranks of a communicator show they sit on distinct GPUs. */
 int fmi_dev_pci_bus_id(int device, char* buf, size_t len);
 
-/* ---- memory (replaces the reference's new[]/std::vector bucket storage, include/comm/Data.h:50-97) */
+/* ---- memory (replaces the reference's new[]/std::vector bucket storage, include/comm/Data.h:50-97)
+ * fmi_dev_alloc: device memory, 4 KiB aligned. Buckets of >= 1 MiB are placed in rotating 4 KiB slots
+ * (FMI_TUNE_ALLOC_SLOTS) so that the buckets one fused kernel streams together do not collide in HBM; free with
+ * fmi_dev_free only (the pointer may lie inside its hipMalloc). */
 int fmi_dev_alloc(void** ptr, size_t bytes);
 int fmi_dev_free(void* ptr);
 int fmi_host_pin_alloc(void** ptr, size_t bytes);  /* page-locked host memory for recv buffers */
@@ -383,11 +386,15 @@ typedef enum {
                                     workgroups are dispatched to different XCDs, so k of the 8 XCDs store sc1.
                                     Default 1 (tools/ab_pair_sc1.py, measured with no MALL re-use). Same bits
                                     always */
-    FMI_TUNE_COMM_ONE_RANK_EXCHANGE = 13 /* 1: a ONE-rank communicator runs the full sharded schedule —
+    FMI_TUNE_COMM_ONE_RANK_EXCHANGE = 13, /* 1: a ONE-rank communicator runs the full sharded schedule —
                                     all-to-all, shard kernel, all-gather / gather / all-to-all back, RCCL
                                     reduce-scatter, window mapping, the pipelined split — exchanging with
                                     itself, instead of the reference's P = 1 copy. Same bits; exists so that
                                     a 1-GPU box runs the RCCL transport's real collectives (tests). Default 0 */
+    FMI_TUNE_ALLOC_SLOTS = 14     /* fmi_dev_alloc of >= 1 MiB: 1 (default) = place successive buckets in
+                                    successive of 16 4-KiB slots (modulo 64 KiB) of a hipMalloc 64 KiB larger,
+                                    so the buckets a fused kernel streams at one offset do not collide in HBM
+                                    (DESIGN §4); 0 = plain hipMalloc. fmi_dev_free takes either. Same bits */
 } fmi_tune_key_t;
 int fmi_tune_set(int key, long long value);
 int fmi_tune_get(int key, long long* value);

@@ -1000,3 +1000,38 @@ def test_beyond_2pow32_elements_64bit_indexing(device):
         assert_bit_equal(ins[0].view(lo, m).numpy(), host(0, lo, m) + host(1, lo, m), f"pair window {lo}")
     for b in ins[:2]:
         b.free()
+
+
+def test_dev_alloc_places_buckets_in_rotating_slots(device):
+    """fmi_dev_alloc: 16 buckets of >= 1 MiB allocated one after another sit in 16 distinct 4 KiB slots
+    modulo 64 KiB (the buckets a fused kernel streams at one offset must not collide in HBM), are 4 KiB aligned,
+    usable to their last byte and freed through fmi_dev_free; small buckets and FMI_TUNE_ALLOC_SLOTS = 0 are plain
+    hipMallocs; a fused kernel over slotted buckets gives the same bits as over plain ones."""
+    n = (1 << 20) // 4 + 7
+    bs = [Bucket(n, np.float32) for _ in range(16)]
+    slots = {(b.ptr % 65536) // 4096 for b in bs}
+    assert len(slots) == 16 and all(b.ptr % 4096 == 0 for b in bs), [hex(b.ptr) for b in bs]
+    for k, b in enumerate(bs):
+        b.fill_synthetic(3, k)
+    xs = [b.numpy() for b in bs[:8]]
+    for k, b in enumerate(bs):
+        tail = b.view(n - 5, 5).numpy()
+        assert np.array_equal(tail.view(np.uint32), orc.synthetic(np.float32, n, 3, k)[-5:].view(np.uint32))
+    out_slotted = Bucket(n, np.float32)
+    fmi_amd.reduce_tree(Op.SUM, Alg.ALLREDUCE, out_slotted, bs[:8])
+    old = fmi_amd.tune_get(Tune.ALLOC_SLOTS)
+    try:
+        fmi_amd.tune_set(Tune.ALLOC_SLOTS, 0)
+        plain = [Bucket.from_numpy(x) for x in xs]
+        out_plain = Bucket(n, np.float32)
+        fmi_amd.reduce_tree(Op.SUM, Alg.ALLREDUCE, out_plain, plain)
+        assert out_plain.numpy().tobytes() == out_slotted.numpy().tobytes()
+        for b in plain + [out_plain]:
+            b.free()
+    finally:
+        fmi_amd.tune_set(Tune.ALLOC_SLOTS, old)
+    small = [Bucket(1000, np.float32) for _ in range(4)]  # < 1 MiB: plain allocations
+    for b in bs + small + [out_slotted]:
+        b.free()
+    with pytest.raises(fmi_amd.FmiError):
+        fmi_amd.tune_set(Tune.ALLOC_SLOTS, 2)

@@ -8,6 +8,14 @@
 #   bash tools/gpu_round5.sh c   the pooled fmi_host_reduce_pair staging and the shared per-device copy streams of
 #                                fmi_comm_allreduce_host: the whole GPU suite, C5's p1_copy + local_peers blocks, and the
 #                                host-combine crossover to 512 MiB (profiles/r05_c_*, r05_c5_blocks.json)
+#   bash tools/gpu_round5.sh d   the tree shapes by placement (inputs carved from one allocation at stride bucket + K
+#                                KiB) and with the bucket launched in slices (profiles/r05_tree8_skew.jsonl, _slices)
+#   bash tools/gpu_round5.sh e   C5's local_peers block (8 LOCAL ranks x 1 GiB) at 8 / 16 / 32 / 64 MiB pipeline chunks
+#                                per rank (profiles/r05_c5_chunks.jsonl)
+#   bash tools/gpu_round5.sh f   placement sweep: pair (C2), tree8 (32 / 512 MiB), scan8 (C3), copy, each with its
+#                                buckets carved from one allocation at stride bucket + K KiB (profiles/r05_skew_sweep.jsonl)
+#   bash tools/gpu_round5.sh g   the slotted fmi_dev_alloc: the whole GPU suite, separate allocations with slots off /
+#                                on twice (profiles/r05_alloc_slots_ab.jsonl), the default bench line (r05_g_*)
 set -o pipefail
 cd /root/repo
 mkdir -p gpurun_out
@@ -50,8 +58,41 @@ print(json.dumps({'p1_copy': bench.c5_p1_copy(1024), 'local_peers': bench.c5_loc
 " > gpurun_out/r05_c5_blocks.json 2> gpurun_out/r05_c5_blocks.err &&
     timeout -k 10 300 python -u tools/host_crossover.py > gpurun_out/r05_host_crossover_512.jsonl 2> gpurun_out/r05_host_crossover_512.err
     ;;
+d)
+    # placement: the tree shapes with the 8 inputs + output carved from ONE allocation at stride bucket + K KiB
+    # (K = -1: separate allocations), and the 1 GiB bucket launched as 4 slices of 256 MiB
+    timeout -k 10 300 python -u tools/tree8_shapes.py --mib 256,512,1024 --skew-kib=-1,0,4,64,2052 \
+        > gpurun_out/r05_tree8_skew.jsonl 2> gpurun_out/r05_tree8_skew.err &&
+    timeout -k 10 200 python -u tools/tree8_shapes.py --mib 512,1024 --slices 1,2,4 \
+        > gpurun_out/r05_tree8_slices.jsonl 2> gpurun_out/r05_tree8_slices.err
+    ;;
+e)
+    # C5's co-resident block by pipeline chunk per rank (the shared copy streams' fill and drain shrink with it)
+    timeout -k 10 400 python -u -c "
+import json, bench, fmi_amd
+fmi_amd.init(0)
+for chunk in (8, 16, 32, 64, 16):
+    bench.quiet_device()
+    r = bench.c5_local_peers(8, 1024, chunk_mib=chunk)
+    print(json.dumps({'chunk_mib': chunk, 'ms': r['ms'], 'pcie_GB_s': r['pcie_GB_s_both_directions'], 'ok': r['self_check']['ok']}), flush=True)
+" > gpurun_out/r05_c5_chunks.jsonl 2> gpurun_out/r05_c5_chunks.err
+    ;;
+f)
+    # placement sweep over every kernel shape of the line (tools/skew_sweep.py)
+    timeout -k 10 600 python -u tools/skew_sweep.py --skew-kib=-1,0,1,2,4,8,16,32,2052 --tree-mib 32,512 \
+        > gpurun_out/r05_skew_sweep.jsonl 2> gpurun_out/r05_skew_sweep.err
+    ;;
+g)
+    # the slotted allocator: the whole GPU suite, the sweep's separate-allocation rows with slots off / on, the
+    # default line
+    timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider \
+        > gpurun_out/r05_g_full_gpu.log 2>&1 &&
+    timeout -k 10 400 python -u tools/skew_sweep.py --skew-kib=-1 --alloc-slots 0,1,0,1 --tree-mib 32,128,512,1024 \
+        > gpurun_out/r05_alloc_slots_ab.jsonl 2> gpurun_out/r05_alloc_slots_ab.err &&
+    timeout -k 10 600 python bench.py > gpurun_out/r05_g_bench.json 2> gpurun_out/r05_g_bench.err
+    ;;
 *)
-    echo "usage: bash tools/gpu_round5.sh a|b|c" >&2
+    echo "usage: bash tools/gpu_round5.sh a|b|c|d|e|f|g" >&2
     exit 2
     ;;
 esac

@@ -4,10 +4,13 @@ bucket sizes per peer, for the counter-led experiment of VERDICT r04 item 2 (DES
 one output, allocated in the order given, filled, a quiet second, then `launches` back-to-back launches between two
 HIP events on the library stream. Prints one JSON line per shape (events) to stdout.
 
-  python tools/tree8_shapes.py [--mib 256,512,1024] [--launches 8] [--slices S]
+  python tools/tree8_shapes.py [--mib 256,512,1024] [--launches 8] [--slices S] [--skew-kib K,...]
 
 --slices S launches each allreduce as S consecutive slices of the buckets (same program per element, so the
 same bits), the shape change VERDICT r04 item 2 names as the first candidate.
+--skew-kib K,...: instead of one hipMalloc per bucket, carve the 8 inputs and the output out of ONE allocation,
+bucket j at j x (bucket + K KiB): whether the buckets' relative placement (address aliasing between the streams
+read at the same offset) is what separates the shapes. -1 = separate allocations (the default layout).
 """
 import argparse
 import json
@@ -24,10 +27,17 @@ from bench import eval_bracketing  # noqa: E402
 from fmi_amd import Alg, Bucket, Event, Op  # noqa: E402
 
 
-def run(mib: int, launches: int, slices: int, peers: int = 8) -> dict:
+def run(mib: int, launches: int, slices: int, skew_kib: int = -1, peers: int = 8) -> dict:
     n = mib * (1 << 20) // 4
-    ins = [Bucket(n, np.float32).fill_synthetic(11, p) for p in range(peers)]
-    out = Bucket(n, np.float32)
+    owner = None
+    if skew_kib < 0:
+        ins = [Bucket(n, np.float32).fill_synthetic(11, p) for p in range(peers)]
+        out = Bucket(n, np.float32)
+    else:
+        stride = n + skew_kib * 256  # elements
+        owner = Bucket(stride * (peers + 1), np.float32)
+        ins = [owner.view(p * stride, n).fill_synthetic(11, p) for p in range(peers)]
+        out = owner.view(peers * stride, n)
     bases = [b.ptr for b in ins] + [out.ptr]
     step = -(-n // slices)
     step = -(-step // 64) * 64
@@ -51,10 +61,10 @@ def run(mib: int, launches: int, slices: int, peers: int = 8) -> dict:
     xs = [b.view(0, 1 << 16).numpy() for b in ins]
     want = eval_bracketing(fmi_amd.schedule_expr(Alg.ALLREDUCE, peers, 0), xs)
     ok = bool(np.array_equal(got.view(np.uint32), want.view(np.uint32)))
-    for b in [out] + ins:
+    for b in [out] + ins + ([owner] if owner is not None else []):
         b.free()
     algo = (peers + 1) * n * 4
-    return {"mib_per_peer": mib, "slices": slices, "launches": launches, "us": round(us, 2),
+    return {"mib_per_peer": mib, "slices": slices, "skew_kib": skew_kib, "launches": launches, "us": round(us, 2),
             "frac": round(algo / (us * 1e-6) / 8e12, 4), "window_bit_exact": ok,
             "bases": [hex(b) for b in bases]}
 
@@ -64,11 +74,13 @@ def main() -> None:
     ap.add_argument("--mib", default="256,512,1024")
     ap.add_argument("--launches", type=int, default=8)
     ap.add_argument("--slices", default="1")
+    ap.add_argument("--skew-kib", default="-1")
     a = ap.parse_args()
     fmi_amd.init(0)
-    for s in [int(x) for x in a.slices.split(",")]:
-        for mib in [int(x) for x in a.mib.split(",")]:
-            print(json.dumps(run(mib, a.launches, s)), flush=True)
+    for k in [int(x) for x in a.skew_kib.split(",")]:
+        for s in [int(x) for x in a.slices.split(",")]:
+            for mib in [int(x) for x in a.mib.split(",")]:
+                print(json.dumps(run(mib, a.launches, s, k)), flush=True)
 
 
 if __name__ == "__main__":
