@@ -39,10 +39,11 @@ public:
     //! Host-combine crossover: smallest bucket, in bytes, whose built-in combine of two host
     //! buckets runs faster through the GPU (fmi_host_reduce_pair: the buckets cross PCIe, 2 in and 1 out) than as
     //! the host loop in place on the calling thread. Measured on MI355X by tools/host_crossover.py
-    //! (profiles/r05_host_crossover.jsonl): page-locked buckets (the zero-copy kernel) pay from 64 MiB; pageable
-    //! buckets (staged H2D / kernel / D2H) not at any size measured, up to 512 MiB; both lose by 14-37x at 64 KiB,
-    //! where the call costs its launch and PCIe latency, not its bytes.
-    static constexpr std::size_t kHostCombinePinnedMinBytes = std::size_t(64) << 20;
+    //! (profiles/r05_host_crossover_512.jsonl): page-locked buckets (the zero-copy kernel) pay from 32 MiB (GPU /
+    //! host 0.98 at 32 MiB, 0.89 at 64 MiB, 0.77-0.81 from 128 MiB; 1.02 at 16 MiB); pageable buckets (staged H2D /
+    //! kernel / D2H) at no size measured, up to 512 MiB (1.11-1.22); both lose by 15-40x at 64 KiB, where the call
+    //! costs its launch and PCIe latency, not its bytes.
+    static constexpr std::size_t kHostCombinePinnedMinBytes = std::size_t(32) << 20;
     static constexpr std::size_t kHostCombinePageableMinBytes = std::numeric_limits<std::size_t>::max();
 
     //! Does a built-in combine of two host buckets of `bucket_bytes` pay on the GPU? (Communicator::use_device

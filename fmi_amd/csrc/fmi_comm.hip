@@ -1146,17 +1146,21 @@ static int shared_copy_streams(hipStream_t* h2d, hipStream_t* d2h) {
 // Streams and events of the host-ingress pipeline (fmi_comm_allreduce_host), created on first use: the chunk's
 // sharded allreduce runs on the communicator's own stream, the copies on the device's shared pair.
 struct HostPipe {
+    // chunk slots in flight: the load of chunk k waits for the allreduce of chunk k - kDepth, so with 3 slots that
+    // wait is on work long finished when the load is queued, and no wait on a shared copy stream holds up the
+    // other ranks' copies behind it
+    static constexpr int kDepth = 3;
     hipStream_t cs = nullptr;   // the chunk's sharded allreduce (this communicator's own)
     hipStream_t h2d = nullptr;  // host -> device loads (shared_copy_streams: not owned)
     hipStream_t d2h = nullptr;  // device -> host results (shared_copy_streams: not owned)
-    hipEvent_t loaded[2] = {}, reduced[2] = {}, drained[2] = {};
+    hipEvent_t loaded[kDepth] = {}, reduced[kDepth] = {}, drained[kDepth] = {};
     bool ready = false;
 
     int init() {
         if (ready) return FMI_OK;
         FMI_COMM_RC(shared_copy_streams(&h2d, &d2h));
         FMI_COMM_HIP(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
-        for (int k = 0; k < 2; ++k)
+        for (int k = 0; k < kDepth; ++k)
             for (hipEvent_t* ev : {&loaded[k], &reduced[k], &drained[k]})
                 FMI_COMM_HIP(hipEventCreateWithFlags(ev, hipEventDisableTiming));
         ready = true;
@@ -1164,7 +1168,7 @@ struct HostPipe {
     }
     ~HostPipe() {
         if (cs) (void)hipStreamDestroy(cs);
-        for (int k = 0; k < 2; ++k)
+        for (int k = 0; k < kDepth; ++k)
             for (hipEvent_t ev : {loaded[k], reduced[k], drained[k]})
                 if (ev) (void)hipEventDestroy(ev);
     }
@@ -1248,8 +1252,9 @@ struct KernelTiming {
 };
 
 struct Comm {
-    // 0-3: collective scratch; 4-7: host-pipeline chunk slots; 8-15: pipelined-allreduce slots (2 x 4)
-    static constexpr int kSlots = 16;
+    // 0-3: collective scratch; 4-7 and 16-17: host-pipeline chunk slots (in / out x HostPipe::kDepth);
+    // 8-15: pipelined-allreduce slots (2 x 4)
+    static constexpr int kSlots = 18;
     std::unique_ptr<Transport> t;
     std::mutex mu;
     KernelTiming timing;
@@ -1291,13 +1296,13 @@ struct Comm {
             for (hipStream_t st : {pipe.cs, chunks.gs})
                 if (st) drained = Transport::drain(st, 10.0) && drained;
             // the shared copy streams carry other communicators' chunks too: only this one's copies are waited for
-            for (int k = 0; k < 2; ++k)
+            for (int k = 0; k < HostPipe::kDepth; ++k)
                 for (hipEvent_t ev : {pipe.loaded[k], pipe.drained[k]})
                     if (ev) drained = Transport::drain_event(ev, 10.0) && drained;
             for (auto& [st, ev] : user_tail) drained = Transport::drain_event(ev, 10.0) && drained;
             if (!drained) {
                 pipe.cs = chunks.gs = nullptr;
-                for (int k = 0; k < 2; ++k) pipe.loaded[k] = pipe.reduced[k] = pipe.drained[k] = nullptr;
+                for (int k = 0; k < HostPipe::kDepth; ++k) pipe.loaded[k] = pipe.reduced[k] = pipe.drained[k] = nullptr;
                 for (void*& b : buf) b = nullptr;
                 windows.clear();
                 return;
@@ -1313,7 +1318,7 @@ struct Comm {
             return;
         }
         if (pipe.cs) (void)hipStreamSynchronize(pipe.cs);
-        for (int k = 0; k < 2; ++k)
+        for (int k = 0; k < HostPipe::kDepth; ++k)
             for (hipEvent_t ev : {pipe.loaded[k], pipe.drained[k]})
                 if (ev) (void)hipEventSynchronize(ev);
         if (chunks.gs) (void)hipStreamSynchronize(chunks.gs);
@@ -1871,10 +1876,10 @@ static int comm_allreduce_impl(fmi_comm_t comm, int op, int dtype, int alg, int 
     return allreduce_device(c, op, dtype, alg, path, send, recv, n, resolve_stream(stream));
 }
 
-// Three-stage pipeline over two chunk slots: while chunk k is allreduced on pipe.cs, chunk k+1 loads on
-// pipe.h2d and chunk k-1 drains on pipe.d2h (the device's shared copy streams, shared_copy_streams). Slot reuse is ordered by events: a load into slot j waits
-// until the allreduce that read it has finished (reduced), an allreduce into slot j waits until the
-// previous result in it has drained to the host.
+// Three-stage pipeline over HostPipe::kDepth chunk slots: while chunk k is allreduced on pipe.cs, chunk k+1 loads on
+// pipe.h2d and chunk k-1 drains on pipe.d2h (the device's shared copy streams, shared_copy_streams). Slot reuse is
+// ordered by events: a load into slot j waits until the allreduce that read it (chunk k - kDepth) has finished
+// (reduced), an allreduce into slot j waits until the previous result in it has drained to the host.
 static int comm_allreduce_host_impl(fmi_comm_t comm, int op, int dtype, int alg, int path, const void* send, void* recv,
                             size_t n, size_t chunk) {
     FMI_COMM_RC(check_common(comm, op, dtype));
@@ -1885,6 +1890,7 @@ static int comm_allreduce_host_impl(fmi_comm_t comm, int op, int dtype, int alg,
     std::lock_guard<std::mutex> lk(c->mu);
     HostPipe& p = c->pipe;
     FMI_COMM_RC(p.init());
+    constexpr int D = HostPipe::kDepth;
     const size_t esz = dtype_size(dtype);
     if (chunk == 0) {
         long long bytes = 0;
@@ -1893,18 +1899,19 @@ static int comm_allreduce_host_impl(fmi_comm_t comm, int op, int dtype, int alg,
     }
     chunk = std::min(chunk, n);
     const size_t nchunks = (n + chunk - 1) / chunk;
-    char* in[2] = {};
-    char* out[2] = {};
-    for (int j = 0; j < 2; ++j) {
-        FMI_COMM_RC(c->scratch(4 + j, chunk * esz, p.cs, &in[j]));
-        FMI_COMM_RC(c->scratch(6 + j, chunk * esz, p.cs, &out[j]));
+    static constexpr int kIn[D] = {4, 5, 16}, kOut[D] = {6, 7, 17};
+    char* in[D] = {};
+    char* out[D] = {};
+    for (int j = 0; j < D && static_cast<size_t>(j) < nchunks; ++j) {
+        FMI_COMM_RC(c->scratch(kIn[j], chunk * esz, p.cs, &in[j]));
+        FMI_COMM_RC(c->scratch(kOut[j], chunk * esz, p.cs, &out[j]));
     }
     const char* src = static_cast<const char*>(send);
     char* dst = static_cast<char*>(recv);
     auto span = [&](size_t k) { return std::min(chunk, n - k * chunk); };
     auto load = [&](size_t k) -> int {
-        const int j = static_cast<int>(k & 1);
-        if (k >= 2) FMI_COMM_HIP(hipStreamWaitEvent(p.h2d, p.reduced[j], 0));
+        const int j = static_cast<int>(k % D);
+        if (k >= static_cast<size_t>(D)) FMI_COMM_HIP(hipStreamWaitEvent(p.h2d, p.reduced[j], 0));
         FMI_COMM_HIP(hipMemcpyAsync(in[j], src + k * chunk * esz, span(k) * esz, hipMemcpyDefault, p.h2d));
         FMI_COMM_HIP(hipEventRecord(p.loaded[j], p.h2d));
         return FMI_OK;
@@ -1912,10 +1919,10 @@ static int comm_allreduce_host_impl(fmi_comm_t comm, int op, int dtype, int alg,
     FMI_COMM_RC(load(0));
     for (size_t k = 0; k < nchunks; ++k) {
         if (k + 1 < nchunks) FMI_COMM_RC(load(k + 1));
-        const int j = static_cast<int>(k & 1);
+        const int j = static_cast<int>(k % D);
         FMI_COMM_HIP(hipStreamWaitEvent(p.cs, p.loaded[j], 0));
-        if (k >= 2) {
-            // Host-side too: chunk k - 2 has drained before chunk k is queued. The device would wait for it anyway
+        if (k >= static_cast<size_t>(D)) {
+            // Host-side too: chunk k - D has drained before chunk k is queued. The device would wait for it anyway
             // (the stream wait above); waiting here as well gives the communicator's timeout a fresh deadline per
             // chunk, so it bounds the progress of one chunk, never the whole bucket's transfer time.
             FMI_COMM_HIP(hipStreamWaitEvent(p.cs, p.drained[j], 0));
@@ -1928,7 +1935,7 @@ static int comm_allreduce_host_impl(fmi_comm_t comm, int op, int dtype, int alg,
         FMI_COMM_HIP(hipEventRecord(p.drained[j], p.d2h));
     }
     // this communicator's last result copy (the shared D2H stream may already carry other ranks' later chunks)
-    FMI_COMM_RC(c->t->wait_event(p.drained[(nchunks - 1) & 1], p.d2h, "fmi_comm_allreduce_host"));
+    FMI_COMM_RC(c->t->wait_event(p.drained[(nchunks - 1) % D], p.d2h, "fmi_comm_allreduce_host"));
     return c->t->wait_stream(p.cs, "fmi_comm_allreduce_host");
 }
 
