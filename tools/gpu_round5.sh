@@ -17,7 +17,8 @@
 #   bash tools/gpu_round5.sh g   the slotted fmi_dev_alloc: the whole GPU suite, separate allocations with slots off /
 #                                on twice (profiles/r05_alloc_slots_ab.jsonl), the default bench line (r05_g_*)
 #   bash tools/gpu_round5.sh h   the pair kernel, slots off / on x 4 (r05_pair_slots_ab.jsonl); C5's co-resident block
-#                                with the 3-slot host pipeline at 16 / 32 / 64 MiB chunks (r05_c5_chunks_depth3.jsonl)
+#                                with the 3-slot host pipeline at 32 / 64 MiB chunks, tapered or not, twice
+#                                (r05_c5_chunks_depth3.jsonl)
 set -o pipefail
 cd /root/repo
 mkdir -p gpurun_out
@@ -95,16 +96,18 @@ g)
     ;;
 h)
     # the pair kernel (C2) on separate allocations, slots off / on interleaved 4 times; then C5's co-resident block
-    # with the 3-slot host pipeline at 16 / 32 / 64 MiB chunks, twice each
+    # with the 3-slot host pipeline at 32 / 64 MiB chunks, tapered and not, twice each
     timeout -k 10 300 python -u tools/skew_sweep.py --kernels pair --skew-kib=-1 --alloc-slots 0,1,0,1,0,1,0,1 \
         --launches 96 > gpurun_out/r05_pair_slots_ab.jsonl 2> gpurun_out/r05_pair_slots_ab.err &&
     timeout -k 10 500 python -u -c "
 import json, bench, fmi_amd
 fmi_amd.init(0)
-for chunk in (16, 32, 64, 16, 32, 64):
-    bench.quiet_device()
-    r = bench.c5_local_peers(8, 1024, chunk_mib=chunk)
-    print(json.dumps({'chunk_mib': chunk, 'depth': 3, 'ms': r['ms'], 'pcie_GB_s': r['pcie_GB_s_both_directions'], 'ok': r['self_check']['ok']}), flush=True)
+for taper in (1, 0, 1, 0):
+    fmi_amd.tune_set(fmi_amd.Tune.HOST_TAPER, taper)
+    for chunk in (32, 64):
+        bench.quiet_device()
+        r = bench.c5_local_peers(8, 1024, chunk_mib=chunk)
+        print(json.dumps({'chunk_mib': chunk, 'depth': 3, 'taper': taper, 'ms': r['ms'], 'pcie_GB_s': r['pcie_GB_s_both_directions'], 'ok': r['self_check']['ok']}), flush=True)
 " > gpurun_out/r05_c5_chunks_depth3.jsonl 2> gpurun_out/r05_c5_chunks_depth3.err
     ;;
 *)
