@@ -1898,30 +1898,7 @@ static int comm_allreduce_host_impl(fmi_comm_t comm, int op, int dtype, int alg,
         chunk = std::max<size_t>(static_cast<size_t>(bytes) / esz, kShardAlign);
     }
     chunk = std::min(chunk, n);
-    // Chunk spans (offset, length). Tapered (FMI_TUNE_HOST_TAPER, default on) where the bucket holds >= 4 chunks:
-    // the first chunks grow c/8, c/8, c/4, c/2 and the last ones shrink the same way, so the pipeline's fill (loads
-    // before the first result can drain) and drain (results left after the last load) cost a small chunk each
-    // instead of a whole one. Every rank derives the same spans from (n, chunk); the bits do not depend on them.
-    std::vector<std::pair<size_t, size_t>> spans;
-    {
-        const size_t a = kShardAlign;
-        const size_t c8 = chunk / 8 / a * a, c4 = chunk / 4 / a * a, c2 = chunk / 2 / a * a;
-        const size_t ramp = 2 * c8 + c4 + c2;
-        size_t off = 0;
-        auto add = [&](size_t len) {
-            spans.emplace_back(off, len);
-            off += len;
-        };
-        if (tune(FMI_TUNE_HOST_TAPER) && c8 > 0 && n >= 4 * chunk) {
-            for (size_t len : {c8, c8, c4, c2}) add(len);
-            const size_t mid_end = n - ramp;
-            while (off < mid_end) add(std::min(chunk, mid_end - off));
-            for (size_t len : {c2, c4, c8, c8}) add(len);
-        } else {
-            while (off < n) add(std::min(chunk, n - off));
-        }
-    }
-    const size_t nchunks = spans.size();
+    const size_t nchunks = (n + chunk - 1) / chunk;
     static constexpr int kIn[D] = {4, 5, 16}, kOut[D] = {6, 7, 17};
     char* in[D] = {};
     char* out[D] = {};
@@ -1931,11 +1908,11 @@ static int comm_allreduce_host_impl(fmi_comm_t comm, int op, int dtype, int alg,
     }
     const char* src = static_cast<const char*>(send);
     char* dst = static_cast<char*>(recv);
-    auto span = [&](size_t k) { return spans[k].second; };
+    auto span = [&](size_t k) { return std::min(chunk, n - k * chunk); };
     auto load = [&](size_t k) -> int {
         const int j = static_cast<int>(k % D);
         if (k >= static_cast<size_t>(D)) FMI_COMM_HIP(hipStreamWaitEvent(p.h2d, p.reduced[j], 0));
-        FMI_COMM_HIP(hipMemcpyAsync(in[j], src + spans[k].first * esz, span(k) * esz, hipMemcpyDefault, p.h2d));
+        FMI_COMM_HIP(hipMemcpyAsync(in[j], src + k * chunk * esz, span(k) * esz, hipMemcpyDefault, p.h2d));
         FMI_COMM_HIP(hipEventRecord(p.loaded[j], p.h2d));
         return FMI_OK;
     };
@@ -1954,7 +1931,7 @@ static int comm_allreduce_host_impl(fmi_comm_t comm, int op, int dtype, int alg,
         FMI_COMM_RC(allreduce_device(c, op, dtype, alg, path, in[j], out[j], span(k), p.cs));
         FMI_COMM_HIP(hipEventRecord(p.reduced[j], p.cs));
         FMI_COMM_HIP(hipStreamWaitEvent(p.d2h, p.reduced[j], 0));
-        FMI_COMM_HIP(hipMemcpyAsync(dst + spans[k].first * esz, out[j], span(k) * esz, hipMemcpyDefault, p.d2h));
+        FMI_COMM_HIP(hipMemcpyAsync(dst + k * chunk * esz, out[j], span(k) * esz, hipMemcpyDefault, p.d2h));
         FMI_COMM_HIP(hipEventRecord(p.drained[j], p.d2h));
     }
     // this communicator's last result copy (the shared D2H stream may already carry other ranks' later chunks)

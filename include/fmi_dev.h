@@ -391,14 +391,10 @@ typedef enum {
                                     reduce-scatter, window mapping, the pipelined split — exchanging with
                                     itself, instead of the reference's P = 1 copy. Same bits; exists so that
                                     a 1-GPU box runs the RCCL transport's real collectives (tests). Default 0 */
-    FMI_TUNE_ALLOC_SLOTS = 14,    /* fmi_dev_alloc of >= 1 MiB: 1 (default) = place successive buckets in
+    FMI_TUNE_ALLOC_SLOTS = 14     /* fmi_dev_alloc of >= 1 MiB: 1 (default) = place successive buckets in
                                     successive of 16 4-KiB slots (modulo 64 KiB) of a hipMalloc 64 KiB larger,
                                     so the buckets a fused kernel streams at one offset do not collide in HBM
                                     (DESIGN §4); 0 = plain hipMalloc. fmi_dev_free takes either. Same bits */
-    FMI_TUNE_HOST_TAPER = 15      /* fmi_comm_allreduce_host of >= 4 chunks: 1 (default) = the first chunks grow
-                                    c/8, c/8, c/4, c/2 and the last ones shrink the same way (short pipeline fill
-                                    and drain); 0 = equal chunks. EVERY rank must set the same value (the chunks
-                                    are collectives). Same bits */
 } fmi_tune_key_t;
 int fmi_tune_set(int key, long long value);
 int fmi_tune_get(int key, long long* value);

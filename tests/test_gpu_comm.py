@@ -11,7 +11,7 @@ import numpy as np
 import pytest
 
 import fmi_amd
-from fmi_amd import Bucket, Op, PinnedArray, Tune
+from fmi_amd import Bucket, Op, PinnedArray
 from fmi_amd.comm import Comm, Path, Transport, unique_id
 from oracle import fmi_oracle as orc
 from tests.test_gpu_parity import OPNAME, assert_bit_equal, inputs
@@ -305,26 +305,6 @@ def test_comm_allreduce_host_pipeline(device, N, pinned):
         for r in range(N):
             assert_bit_equal(res[r][0], want[r], f"N={N} {op.name} ordered={ordered} rank {r}")
             assert_bit_equal(res[r][1], xs[r], "send bucket untouched")
-
-
-@pytest.mark.parametrize("N", [2, 8])
-@pytest.mark.parametrize("taper", [1, 0])
-def test_comm_allreduce_host_tapered_chunks(device, N, taper):
-    """FMI_TUNE_HOST_TAPER: a bucket of >= 4 chunks streams its first chunks at c/8, c/8, c/4, c/2 and its last
-    ones the same way in reverse (a ragged chunk in the middle); page-locked and pageable buckets, both settings,
-    every rank's result equals the oracle's bit for bit."""
-    n, chunk = 9 * 4096 + 17, 4096
-    old = fmi_amd.tune_get(Tune.HOST_TAPER)
-    try:
-        fmi_amd.tune_set(Tune.HOST_TAPER, taper)
-        for pinned in (True, False):
-            xs = [inputs(np.float32, n, r, seed=31) for r in range(N)]
-            res = run_ranks(N, lambda c, r: _host_allreduce(c, r, xs[r], Op.SUM, False, pinned, chunk))
-            want, _ = orc.allreduce(xs, orc.OPS["sum"])
-            for r in range(N):
-                assert_bit_equal(res[r][0], want[r], f"N={N} taper={taper} pinned={pinned} rank {r}")
-    finally:
-        fmi_amd.tune_set(Tune.HOST_TAPER, old)
 
 
 def test_comm_allreduce_host_default_chunk_matches_device(device):

@@ -19,6 +19,8 @@
 #   bash tools/gpu_round5.sh h   the pair kernel, slots off / on x 4 (r05_pair_slots_ab.jsonl); C5's co-resident block
 #                                with the 3-slot host pipeline at 32 / 64 MiB chunks, tapered or not, twice
 #                                (r05_c5_chunks_depth3.jsonl)
+#   bash tools/gpu_round5.sh z   the round-end sequence: GPU suite, smoke(), default line, C2 profile (r05z_*;
+#                                then tools/pmc_summarize.py --tag r05z_c2 --merge)
 set -o pipefail
 cd /root/repo
 mkdir -p gpurun_out
@@ -102,16 +104,26 @@ h)
     timeout -k 10 500 python -u -c "
 import json, bench, fmi_amd
 fmi_amd.init(0)
-for taper in (1, 0, 1, 0):
-    fmi_amd.tune_set(fmi_amd.Tune.HOST_TAPER, taper)
+for taper in (1, 0, 1, 0):  # as run: against fad2b1e's FMI_TUNE_HOST_TAPER (removed after: no gain)
+    if hasattr(fmi_amd.Tune, 'HOST_TAPER'):
+        fmi_amd.tune_set(fmi_amd.Tune.HOST_TAPER, taper)
     for chunk in (32, 64):
         bench.quiet_device()
         r = bench.c5_local_peers(8, 1024, chunk_mib=chunk)
         print(json.dumps({'chunk_mib': chunk, 'depth': 3, 'taper': taper, 'ms': r['ms'], 'pcie_GB_s': r['pcie_GB_s_both_directions'], 'ok': r['self_check']['ok']}), flush=True)
 " > gpurun_out/r05_c5_chunks_depth3.jsonl 2> gpurun_out/r05_c5_chunks_depth3.err
     ;;
+z)
+    # the round-end sequence on the final library and bench: the whole GPU suite, smoke(), the default line, then
+    # the C2 profile (kernel trace + stats, separate FETCH_SIZE / WRITE_SIZE passes, an unprofiled line)
+    timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+        -p no:cacheprovider > gpurun_out/r05z_full_gpu.log 2>&1 &&
+    timeout -k 10 300 python -u -c 'import __graft_entry__ as g; g.smoke()' > gpurun_out/r05z_smoke.log 2>&1 &&
+    timeout -k 10 600 python bench.py > gpurun_out/r05z_bench.json 2> gpurun_out/r05z_bench.err &&
+    bash tools/c2_profile.sh
+    ;;
 *)
-    echo "usage: bash tools/gpu_round5.sh a|b|c|d|e|f|g|h" >&2
+    echo "usage: bash tools/gpu_round5.sh a|b|c|d|e|f|g|h|z" >&2
     exit 2
     ;;
 esac
