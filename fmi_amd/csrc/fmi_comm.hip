@@ -279,6 +279,9 @@ public:
     // shards short or empty), so a bucket needs no zero padding. all_to_all_ragged: recv[j * shard ...] = rank
     // j's shard `rank` (span(rank) bytes); all_gather_ragged: recv[j * shard ...] = rank j's send (span(j)).
     virtual bool ragged() const { return false; }
+    // Several ranks of this communicator drive the same device from this process (their host pipelines share the
+    // device's copy streams, shared_copy_streams).
+    virtual bool co_resident() const { return false; }
     virtual int all_to_all_ragged(const char*, char*, size_t, size_t, hipStream_t) {
         return fail(FMI_ERR_UNSUPPORTED, "transport has no ragged exchanges");
     }
@@ -640,6 +643,8 @@ constexpr char kLocalMagic[8] = {'F', 'M', 'I', 'L', 'O', 'C', 'A', 'L'};
 class LocalTransport final : public Transport {
 public:
     LocalTransport(std::shared_ptr<Hub> hub, int n, int rank) : Transport(n, rank), hub_(std::move(hub)) {}
+
+    bool co_resident() const override { return n_ > 1; }  // the ranks are threads sharing this device
 
     // Every exchange below runs the RCCL transport's own plan (fmi_exchange_plan.h): each receive copies
     // from the matching send of the peer's plan (same peer order, same length, or the call fails), so the
@@ -1146,10 +1151,14 @@ static int shared_copy_streams(hipStream_t* h2d, hipStream_t* d2h) {
 // Streams and events of the host-ingress pipeline (fmi_comm_allreduce_host), created on first use: the chunk's
 // sharded allreduce runs on the communicator's own stream, the copies on the device's shared pair.
 struct HostPipe {
-    // chunk slots in flight: the load of chunk k waits for the allreduce of chunk k - kDepth, so with 3 slots that
-    // wait is on work long finished when the load is queued, and no wait on a shared copy stream holds up the
-    // other ranks' copies behind it
-    static constexpr int kDepth = 3;
+    // Chunk slots in flight: the load of chunk k waits for the allreduce of chunk k - depth. One rank per device
+    // (every communicator across GPUs): 2 — the wait paces the loads to the results draining, and the two
+    // directions stay overlapped (a 1 GiB one-rank pipeline 23.2-24.3 ms at 2, 32.7-33.0 ms at 3). Co-resident
+    // ranks sharing the device's copy streams (LOCAL): 3 — one rank's load waiting for its allreduce of chunk
+    // k - 2 would hold every other rank's loads behind it on the shared stream, and at depth 3 that wait is long
+    // finished when the load is queued (8 ranks x 1 GiB: 203-204 ms at 3, 217-240 ms at 2).
+    // profiles/r05_depth_ab.jsonl (build/ab_d2: make -C fmi_amd/csrc ab_depth2, FMI_HOST_PIPE_DEPTH=2 forces 2).
+    static constexpr int kDepth = 3;  // slots allocated
     hipStream_t cs = nullptr;   // the chunk's sharded allreduce (this communicator's own)
     hipStream_t h2d = nullptr;  // host -> device loads (shared_copy_streams: not owned)
     hipStream_t d2h = nullptr;  // device -> host results (shared_copy_streams: not owned)
@@ -1890,7 +1899,11 @@ static int comm_allreduce_host_impl(fmi_comm_t comm, int op, int dtype, int alg,
     std::lock_guard<std::mutex> lk(c->mu);
     HostPipe& p = c->pipe;
     FMI_COMM_RC(p.init());
-    constexpr int D = HostPipe::kDepth;
+#ifdef FMI_HOST_PIPE_DEPTH
+    const int D = FMI_HOST_PIPE_DEPTH;
+#else
+    const int D = c->t->co_resident() ? HostPipe::kDepth : 2;
+#endif
     const size_t esz = dtype_size(dtype);
     if (chunk == 0) {
         long long bytes = 0;
@@ -1899,9 +1912,9 @@ static int comm_allreduce_host_impl(fmi_comm_t comm, int op, int dtype, int alg,
     }
     chunk = std::min(chunk, n);
     const size_t nchunks = (n + chunk - 1) / chunk;
-    static constexpr int kIn[D] = {4, 5, 16}, kOut[D] = {6, 7, 17};
-    char* in[D] = {};
-    char* out[D] = {};
+    static constexpr int kIn[3] = {4, 5, 16}, kOut[3] = {6, 7, 17};
+    char* in[HostPipe::kDepth] = {};
+    char* out[HostPipe::kDepth] = {};
     for (int j = 0; j < D && static_cast<size_t>(j) < nchunks; ++j) {
         FMI_COMM_RC(c->scratch(kIn[j], chunk * esz, p.cs, &in[j]));
         FMI_COMM_RC(c->scratch(kOut[j], chunk * esz, p.cs, &out[j]));

@@ -19,6 +19,11 @@
 #   bash tools/gpu_round5.sh h   the pair kernel, slots off / on x 4 (r05_pair_slots_ab.jsonl); C5's co-resident block
 #                                with the 3-slot host pipeline at 32 / 64 MiB chunks, tapered or not, twice
 #                                (r05_c5_chunks_depth3.jsonl)
+#   bash tools/gpu_round5.sh i   FMI_TUNE_FUSED_INFLIGHT_KIB x FMI_TUNE_FUSED_POLICY on slotted buckets: tree8 1 GiB /
+#                                32 MiB, scan8 64 MiB, two interleaved rounds (r05_fused_retune.jsonl); then the 8-peer
+#                                shared-stream DMA with and without a concurrent HBM copy loop (r05_pcie_busy.jsonl)
+#   bash tools/gpu_round5.sh j   host pipeline 3 vs 2 chunk slots (build/ab_d2), C5 p1_copy + local_peers, 3 x
+#                                interleaved processes (r05_depth_ab.jsonl)
 #   bash tools/gpu_round5.sh z   the round-end sequence: GPU suite, smoke(), default line, C2 profile (r05z_*;
 #                                then tools/pmc_summarize.py --tag r05z_c2 --merge)
 set -o pipefail
@@ -113,6 +118,31 @@ for taper in (1, 0, 1, 0):  # as run: against fad2b1e's FMI_TUNE_HOST_TAPER (rem
         print(json.dumps({'chunk_mib': chunk, 'depth': 3, 'taper': taper, 'ms': r['ms'], 'pcie_GB_s': r['pcie_GB_s_both_directions'], 'ok': r['self_check']['ok']}), flush=True)
 " > gpurun_out/r05_c5_chunks_depth3.jsonl 2> gpurun_out/r05_c5_chunks_depth3.err
     ;;
+i)
+    # the fused kernels' in-flight cap and access policy re-tuned on slotted buckets (tools/fused_retune.py)
+    timeout -k 10 400 python -u tools/fused_retune.py --rounds 2 > gpurun_out/r05_fused_retune.jsonl \
+        2> gpurun_out/r05_fused_retune.err &&
+    timeout -k 10 200 build/mbpciepeers 3 0 1 > gpurun_out/r05_pcie_busy.jsonl 2> gpurun_out/r05_pcie_busy.err
+    ;;
+j)
+    # the host pipeline depth of the library (2, or 3 for co-resident LOCAL ranks) vs always 2 (build/ab_d2, make -C
+    # fmi_amd/csrc ab_depth2; first run: the library at 3 for every communicator), separate processes,
+    # interleaved three times: C5's p1_copy and local_peers blocks
+    for k in 1 2 3; do
+        for lib in fmi_amd/lib/libfmi_dev.so build/ab_d2/libfmi_dev.so; do
+            FMI_DEV_LIB=$PWD/$lib timeout -k 10 200 python -u -c "
+import json, os, bench, fmi_amd
+fmi_amd.init(0)
+bench.quiet_device()
+p1 = bench.c5_p1_copy(1024)
+bench.quiet_device()
+lp = bench.c5_local_peers(8, 1024)
+print(json.dumps({'lib': os.environ['FMI_DEV_LIB'].split('/repo/')[-1], 'p1_copy_ms': p1['ms'], 'p1_ok': p1['self_check']['ok'],
+                  'local_peers_ms': lp['ms'], 'local_peers_GB_s': lp['pcie_GB_s_both_directions'], 'lp_ok': lp['self_check']['ok']}))
+" >> gpurun_out/r05_depth_ab.jsonl 2>> gpurun_out/r05_depth_ab.err || exit 1
+        done
+    done
+    ;;
 z)
     # the round-end sequence on the final library and bench: the whole GPU suite, smoke(), the default line, then
     # the C2 profile (kernel trace + stats, separate FETCH_SIZE / WRITE_SIZE passes, an unprofiled line)
@@ -123,7 +153,7 @@ z)
     bash tools/c2_profile.sh
     ;;
 *)
-    echo "usage: bash tools/gpu_round5.sh a|b|c|d|e|f|g|h|z" >&2
+    echo "usage: bash tools/gpu_round5.sh a|b|c|d|e|f|g|h|i|j|z" >&2
     exit 2
     ;;
 esac

@@ -9,9 +9,12 @@
 // Each peer's chunks are issued by its own host thread (as the LOCAL ranks do), except the shared variants,
 // which one thread feeds. Wall time from host clocks around issue .. last stream drained; 1 GiB = 2^30 B.
 // "streams_before" opens that many idle streams first (where the runtime hands out its DMA engines by stream).
+// "busy" (third argument 1): the shared-stream variants again while a third stream keeps HBM busy with device
+// copies of 256 MiB (the co-resident ranks' exchange copies and kernels, as fmi_comm_allreduce_host runs them
+// beside its DMA): does the link's duplex rate hold when the chip is also streaming HBM?
 //
 // Build: hipcc -std=c++20 -O3 --offload-arch=gfx950 tools/microbench_pcie_peers.hip -o build/mbpciepeers
-// Run:   build/mbpciepeers [rounds, default 3]
+// Run:   build/mbpciepeers [rounds, default 3] [streams_before, default 0] [busy, default 0]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -72,9 +75,15 @@ static void enqueue(Peer& p, size_t off, bool kernel, hipMemcpyKind hk, hipMemcp
     }
 }
 
+__global__ void __launch_bounds__(256) hbm_copy(u32x4* __restrict__ dst, const u32x4* __restrict__ src, size_t n16) {
+    for (size_t i = blockIdx.x * size_t(256) + threadIdx.x; i < n16; i += size_t(gridDim.x) * 256)
+        __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
+}
+
 int main(int argc, char** argv) {
     const int rounds = argc > 1 ? std::atoi(argv[1]) : 3;
     const int streams_before = argc > 2 ? std::atoi(argv[2]) : 0;
+    const bool busy = argc > 3 && std::atoi(argv[3]) != 0;
     std::vector<hipStream_t> idle(streams_before);
     for (auto& s : idle) CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     constexpr int kMaxPeers = 8;
@@ -104,7 +113,14 @@ int main(int argc, char** argv) {
         int grid;
     };
     std::vector<V> vs;
+    if (busy) {
+        vs.push_back({"shared-sdma+hbm-busy", 8, true, false, false, 0});
+        vs.push_back({"shared-sdma", 8, true, false, false, 0});
+        vs.push_back({"shared-sdma+hbm-busy", 8, true, false, false, 0});
+        vs.push_back({"shared-sdma", 8, true, false, false, 0});
+    }
     for (int P : {1, 2, 8}) {
+        if (busy) break;
         vs.push_back({"own-sdma", P, false, false, false, 0});
         vs.push_back({"own-sdma-def", P, false, false, true, 0});
         vs.push_back({"shared-sdma", P, true, false, false, 0});
@@ -114,12 +130,37 @@ int main(int argc, char** argv) {
             vs.push_back({"shared-kernel", P, true, true, false, g});
         }
     }
+    // the busy stream's buffers: 2 x 256 MiB in HBM
+    constexpr size_t kBusyBytes = size_t(256) << 20;
+    u32x4 *busy_a = nullptr, *busy_b = nullptr;
+    hipStream_t busy_s = nullptr;
+    if (busy) {
+        CHECK(hipMalloc(&busy_a, kBusyBytes));
+        CHECK(hipMalloc(&busy_b, kBusyBytes));
+        CHECK(hipMemset(busy_a, 1, kBusyBytes));
+        CHECK(hipStreamCreateWithFlags(&busy_s, hipStreamNonBlocking));
+    }
     for (auto& v : vs) {
         std::vector<double> ms;
+        const bool keep_busy = v.name.find("hbm-busy") != std::string::npos;
         for (int rep = 0; rep < rounds + 1; ++rep) {
             CHECK(hipDeviceSynchronize());
             const hipMemcpyKind hk = v.deflt ? hipMemcpyDefault : hipMemcpyHostToDevice;
             const hipMemcpyKind dk = v.deflt ? hipMemcpyDefault : hipMemcpyDeviceToHost;
+            std::atomic<bool> stop{false};
+            std::thread feeder;
+            if (keep_busy)  // keep 2 copies queued at a time until the DMA is done (~0.1 ms each)
+                feeder = std::thread([&] {
+                    hipEvent_t done[2];
+                    for (auto& ev : done) CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+                    for (int k = 0; !stop.load(); ++k) {
+                        if (k >= 2) CHECK(hipEventSynchronize(done[k & 1]));
+                        hbm_copy<<<2048, 256, 0, busy_s>>>(busy_b, busy_a, kBusyBytes / 16);
+                        CHECK(hipEventRecord(done[k & 1], busy_s));
+                    }
+                    CHECK(hipStreamSynchronize(busy_s));
+                    for (auto& ev : done) CHECK(hipEventDestroy(ev));
+                });
             const auto t0 = std::chrono::steady_clock::now();
             if (v.shared) {
                 for (size_t off = 0; off < kBytes; off += kChunk)
@@ -140,6 +181,8 @@ int main(int argc, char** argv) {
                 for (auto& t : th) t.join();
             }
             const double t = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+            stop.store(true);
+            if (feeder.joinable()) feeder.join();
             if (rep > 0) ms.push_back(t);  // the first is a warm-up
         }
         // byte-exact: every peer's device copy of its source, and its host copy of the device bucket
