@@ -973,7 +973,7 @@ int fmi_dev_pci_bus_id(int device, char* buf, size_t len) {
 int fmi_dev_alloc(void** ptr, size_t bytes) {
     if (!ptr) return fail(FMI_ERR_INVALID, "ptr is null");
     if (int rc = require_device()) return rc;
-    const bool slotted = bytes >= kSlotMinBytes && g_tune[FMI_TUNE_ALLOC_SLOTS].load() != 0;
+    const bool slotted = bytes >= kSlotMinBytes && bytes <= SIZE_MAX - kSlotSpan && g_tune[FMI_TUNE_ALLOC_SLOTS].load() != 0;
     void* base = nullptr;
     const hipError_t e = hipMalloc(&base, std::max<size_t>(bytes, 1) + (slotted ? kSlotSpan : 0));
     if (e != hipSuccess) return fail(FMI_ERR_ALLOC, "hipMalloc(" + std::to_string(bytes) + "): " + hipGetErrorString(e));

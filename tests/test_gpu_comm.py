@@ -307,6 +307,40 @@ def test_comm_allreduce_host_pipeline(device, N, pinned):
             assert_bit_equal(res[r][1], xs[r], "send bucket untouched")
 
 
+def test_comm_allreduce_host_concurrent_communicators_share_copy_streams(device):
+    """Every communicator's host pipeline issues its copies on the device's ONE H2D and ONE D2H stream
+    (shared_copy_streams): three independent LOCAL communicators (1, 2 and 4 ranks: pipeline depth 2, 3 and 3)
+    run host allreduces at the same time, several calls each with different chunkings, so their chunks interleave
+    on the shared streams. Every rank's result equals the oracle's bit for bit."""
+    sizes = {1: 9 * 4096 + 3, 2: 7 * 4096 + 5, 4: 11 * 4096 + 7}
+    results, errors = {}, []
+
+    def comm_job(N):
+        n = sizes[N]
+        xs = [[inputs(np.float32, n, r, seed=60 + N + k) for r in range(N)] for k in range(3)]
+
+        def body(c, r):
+            return [_host_allreduce(c, r, xs[k][r], Op.SUM, False, (r + k) % 2 == 0, 4096 * (k + 1))[0]
+                    for k in range(3)]
+
+        try:
+            results[N] = (xs, run_ranks(N, body))
+        except BaseException as e:  # noqa: BLE001 - reported below
+            errors.append(f"N={N}: {e!r}")
+
+    jobs = [threading.Thread(target=comm_job, args=(N,)) for N in sizes]
+    for t in jobs:
+        t.start()
+    for t in jobs:
+        t.join(timeout=300)
+    assert not errors and not any(t.is_alive() for t in jobs), errors
+    for N, (xs, res) in results.items():
+        for k in range(3):
+            want, _ = orc.allreduce(xs[k], orc.OPS["sum"])
+            for r in range(N):
+                assert_bit_equal(res[r][k], want[r], f"communicator N={N} call {k} rank {r}")
+
+
 def test_comm_allreduce_host_default_chunk_matches_device(device):
     """Default chunking (FMI_TUNE_HOST_CHUNK) over a 40 MiB bucket per rank: bit-identical to the device
     allreduce of the whole bucket."""
