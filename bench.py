@@ -1227,8 +1227,16 @@ def run_dist(args, world, rank, local_rank):
     else:
         dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
         # the fallback agreement votes on a gloo group of its own: a vote can never pair with an RCCL collective
-        # of the timed loop that another rank is still inside
-        vote = dist.new_group(backend="gloo")
+        # of the timed loop that another rank is still inside. If gloo cannot connect here, the vote
+        # runs on the RCCL group as before (every rank fails the same way: the group is made collectively).
+        try:
+            import datetime
+
+            vote = dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=120))
+        except Exception as e:  # noqa: BLE001 - the vote still happens, on the world group
+            print(f"bench: rank {rank}: no gloo group for the fallback vote ({type(e).__name__}: {e}); voting over "
+                  "the RCCL group", file=sys.stderr, flush=True)
+            vote = None
 
     import fmi_amd
     from fmi_amd.collectives import CommAllreduce
