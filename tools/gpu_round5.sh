@@ -24,6 +24,8 @@
 #                                shared-stream DMA with and without a concurrent HBM copy loop (r05_pcie_busy.jsonl)
 #   bash tools/gpu_round5.sh j   host pipeline 3 vs 2 chunk slots (build/ab_d2), C5 p1_copy + local_peers, 3 x
 #                                interleaved processes (r05_depth_ab.jsonl)
+#   bash tools/gpu_round5.sh k   8-in / 1-out tree shape, U = 1 / 2 / 4 lane groups per thread x a cap of 2 / 4 / 8 / no
+#                                workgroups per CU, slotted buckets, 1 GiB and 32 MiB per peer (tools/microbench_tree_u.hip)
 #   bash tools/gpu_round5.sh z   the round-end sequence: GPU suite, smoke(), default line, C2 profile (r05z_*;
 #                                then tools/pmc_summarize.py --tag r05z_c2 --merge)
 set -o pipefail
@@ -143,17 +145,21 @@ print(json.dumps({'lib': os.environ['FMI_DEV_LIB'].split('/repo/')[-1], 'p1_copy
         done
     done
     ;;
+k)
+    # the 8-way tree's lane groups per thread (U) x workgroups-per-CU cap on slotted buckets (build/mbtreeu)
+    timeout -k 10 300 build/mbtreeu 3 > gpurun_out/r05_tree_u.jsonl 2> gpurun_out/r05_tree_u.err
+    ;;
 z)
     # the round-end sequence on the final library and bench: the whole GPU suite, smoke(), the default line, then
     # the C2 profile (kernel trace + stats, separate FETCH_SIZE / WRITE_SIZE passes, an unprofiled line)
     timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
-        -p no:cacheprovider > gpurun_out/r05z_full_gpu.log 2>&1 &&
-    timeout -k 10 300 python -u -c 'import __graft_entry__ as g; g.smoke()' > gpurun_out/r05z_smoke.log 2>&1 &&
-    timeout -k 10 600 python bench.py > gpurun_out/r05z_bench.json 2> gpurun_out/r05z_bench.err &&
+        -p no:cacheprovider > gpurun_out/${TAG:-r05z}_full_gpu.log 2>&1 &&
+    timeout -k 10 300 python -u -c 'import __graft_entry__ as g; g.smoke()' > gpurun_out/${TAG:-r05z}_smoke.log 2>&1 &&
+    timeout -k 10 600 python bench.py > gpurun_out/${TAG:-r05z}_bench.json 2> gpurun_out/${TAG:-r05z}_bench.err &&
     bash tools/c2_profile.sh
     ;;
 *)
-    echo "usage: bash tools/gpu_round5.sh a|b|c|d|e|f|g|h|i|j|z" >&2
+    echo "usage: bash tools/gpu_round5.sh a|b|c|d|e|f|g|h|i|j|k|z" >&2
     exit 2
     ;;
 esac
