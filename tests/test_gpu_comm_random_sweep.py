@@ -2,14 +2,16 @@
 random rank count, collective, order (commutative or left-to-right), op, dtype and bucket length — the
 shard grid, its zero padding, the all-to-all, the fused (or blocked) shard program and the gather /
 all-to-all back — every rank's result bit-exact against the oracle's simulation of the reference
-collective. Deterministic: the case list is a function of the seed."""
+collective. Since round 5 also the host-ingress allreduce (fmi_comm_allreduce_host: page-locked or pageable
+host buckets, a random chunk giving 1-12 chunks, through the device's shared copy streams, two or three chunk
+slots deep). Deterministic: the case list is a function of the seed."""
 import os
 
 import numpy as np
 import pytest
 
 import fmi_amd
-from fmi_amd import Bucket
+from fmi_amd import Bucket, PinnedArray
 from fmi_amd.comm import Path
 from oracle import fmi_oracle as orc
 from tests.test_gpu_comm import run_ranks
@@ -33,19 +35,20 @@ def _cases(seed):
     rng = np.random.default_rng(seed)
     for k in range(CASES):
         N = int(rng.choice([1, 2, 3, 4, 5, 7, 8, 11, 16, 19]))
-        kind = str(rng.choice(["allreduce", "allreduce_direct", "reduce", "reduce_sendbuf", "scan"]))
+        kind = str(rng.choice(["allreduce", "allreduce_direct", "allreduce_host", "reduce", "reduce_sendbuf", "scan"]))
         ordered = bool(rng.integers(0, 2))
         op = OPS[int(rng.integers(0, 4))]
         dtype = ALL_DTYPES[int(rng.integers(0, len(ALL_DTYPES)))]
         n = int(rng.choice([1, 5, 64, 255, 1000, 4099, 65536 + 7]))
         root = int(rng.integers(0, N))
-        yield k, N, kind, ordered, op, dtype, n, root
+        chunk = max(1, n // int(rng.integers(1, 13)))  # allreduce_host: 1-12 chunks (rounded by the library)
+        yield k, N, kind, ordered, op, dtype, n, root, chunk
 
 
 @pytest.mark.parametrize("seed", _seeds([11, 12]))
 def test_random_comm_cases(device, seed):
     done = 0
-    for k, N, kind, ordered, op, dtype, n, root in _cases(seed):
+    for k, N, kind, ordered, op, dtype, n, root, chunk in _cases(seed):
         xs = [inputs(dtype, n, r, seed=500 * seed + k) for r in range(N)]
 
         def body(c, r):
@@ -59,6 +62,18 @@ def test_random_comm_cases(device, seed):
                 fmi_amd.sync()
                 got = out.numpy()
                 c.window_free(w)
+                return got
+            elif kind == "allreduce_host":  # even ranks page-locked buckets, odd ranks pageable
+                if r % 2 == 0:
+                    hs, ho = PinnedArray(n, dtype), PinnedArray(n, dtype)
+                    hs.array[:] = xs[r]
+                    c.allreduce_host(op, hs.array, ho.array, ordered=ordered, chunk=chunk)
+                    got = ho.array.copy()
+                    hs.free()
+                    ho.free()
+                    return got
+                got = np.zeros(n, dtype)
+                c.allreduce_host(op, xs[r].copy(), got, ordered=ordered, chunk=chunk)
                 return got
             elif kind == "reduce":
                 c.reduce(op, s, out if r == root else None, root, ordered=ordered)
