@@ -26,6 +26,7 @@
 #                                interleaved processes (r05_depth_ab.jsonl)
 #   bash tools/gpu_round5.sh k   8-in / 1-out tree shape, U = 1 / 2 / 4 lane groups per thread x a cap of 2 / 4 / 8 / no
 #                                workgroups per CU, slotted buckets, 1 GiB and 32 MiB per peer (tools/microbench_tree_u.hip)
+#   bash tools/gpu_round5.sh l   C5 local_peers at GPU_MAX_HW_QUEUES 4 / 8 / 16, twice (r05_c5_hwq.jsonl)
 #   bash tools/gpu_round5.sh z   the round-end sequence: GPU suite, smoke(), default line, C2 profile (r05z_*;
 #                                then tools/pmc_summarize.py --tag r05z_c2 --merge)
 set -o pipefail
@@ -149,6 +150,18 @@ k)
     # the 8-way tree's lane groups per thread (U) x workgroups-per-CU cap on slotted buckets (build/mbtreeu)
     timeout -k 10 300 build/mbtreeu 3 > gpurun_out/r05_tree_u.jsonl 2> gpurun_out/r05_tree_u.err
     ;;
+l)
+    # C5's co-resident block against the process's hardware-queue count (GPU_MAX_HW_QUEUES 4 / 8 / 16), twice
+    for q in 4 8 16 4 8 16; do
+        GPU_MAX_HW_QUEUES=$q timeout -k 10 200 python -u -c "
+import json, os, bench, fmi_amd
+fmi_amd.init(0)
+bench.quiet_device()
+lp = bench.c5_local_peers(8, 1024)
+print(json.dumps({'GPU_MAX_HW_QUEUES': int(os.environ['GPU_MAX_HW_QUEUES']), 'ms': lp['ms'], 'pcie_GB_s': lp['pcie_GB_s_both_directions'], 'ok': lp['self_check']['ok']}))
+" >> gpurun_out/r05_c5_hwq.jsonl 2>> gpurun_out/r05_c5_hwq.err || exit 1
+    done
+    ;;
 z)
     # the round-end sequence on the final library and bench: the whole GPU suite, smoke(), the default line, then
     # the C2 profile (kernel trace + stats, separate FETCH_SIZE / WRITE_SIZE passes, an unprofiled line)
@@ -159,7 +172,7 @@ z)
     bash tools/c2_profile.sh
     ;;
 *)
-    echo "usage: bash tools/gpu_round5.sh a|b|c|d|e|f|g|h|i|j|k|z" >&2
+    echo "usage: bash tools/gpu_round5.sh a|b|c|d|e|f|g|h|i|j|k|l|z" >&2
     exit 2
     ;;
 esac
