@@ -105,7 +105,8 @@ int fmi_dev_pci_bus_id(int device, char* buf, size_t len);
 /* ---- memory (replaces the reference's new[]/std::vector bucket storage, include/comm/Data.h:50-97)
  * fmi_dev_alloc: device memory, 4 KiB aligned. Buckets of >= 1 MiB are placed in rotating 4 KiB slots
  * (FMI_TUNE_ALLOC_SLOTS) so that the buckets one fused kernel streams together do not collide in HBM; free with
- * fmi_dev_free only (the pointer may lie inside its hipMalloc). */
+ * fmi_dev_free only (the pointer may lie inside its hipMalloc, up to 60 KiB past its base, so it is not a
+ * hipIpcGetMemHandle base either: memory shared across processes comes from fmi_comm_window_alloc). */
 int fmi_dev_alloc(void** ptr, size_t bytes);
 int fmi_dev_free(void* ptr);
 int fmi_host_pin_alloc(void** ptr, size_t bytes);  /* page-locked host memory for recv buffers */
