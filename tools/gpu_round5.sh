@@ -148,7 +148,7 @@ print(json.dumps({'lib': os.environ['FMI_DEV_LIB'].split('/repo/')[-1], 'p1_copy
     ;;
 k)
     # the 8-way tree's lane groups per thread (U) x workgroups-per-CU cap on slotted buckets (build/mbtreeu)
-    timeout -k 10 300 build/mbtreeu 3 > gpurun_out/r05_tree_u.jsonl 2> gpurun_out/r05_tree_u.err
+    timeout -k 10 300 build/mbtreeu 3 > gpurun_out/${OUT:-r05_tree_u}.jsonl 2> gpurun_out/${OUT:-r05_tree_u}.err
     ;;
 l)
     # C5's co-resident block against the process's hardware-queue count (GPU_MAX_HW_QUEUES 4 / 8 / 16), twice

@@ -5,7 +5,8 @@
 // f32 sum of the same access pattern (buffer loads nt, buffer stores sc1, 256-thread workgroups, one tile per
 // workgroup) for U = 1, 2, 4 and caps of 2, 4 or 8 workgroups per CU (none = registers decide), interleaved in one
 // process over rotating sets of slotted buckets. Wall time per launch from events around `launches` launches;
-// every variant's output checked against a host sum on one window.
+// every variant's output checked against a host sum on one window. Also U = 1 / 2 at 2 per CU with each XCD taking a
+// contiguous eighth of the tiles instead of every eighth tile.
 //
 // Build: hipcc -std=c++20 -O3 --offload-arch=gfx950 tools/microbench_tree_u.hip -o build/mbtreeu
 // Run:   build/mbtreeu [rounds, default 3]
@@ -41,9 +42,12 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 1 << 30, 0x00020000);
 }
 
-template <int U>
+// XCD: 0 = tile = workgroup index (consecutive tiles on consecutive XCDs, the library's order); 1 = each XCD takes
+// a contiguous eighth of the tiles (workgroup w runs on XCD w % 8)
+template <int U, int XCD>
 __global__ void __launch_bounds__(256) tree8(Ptrs p, size_t n16) {
-    const size_t tile = blockIdx.x;
+    const size_t per_xcd = gridDim.x / 8;
+    const size_t tile = XCD ? (blockIdx.x % 8) * per_xcd + blockIdx.x / 8 : blockIdx.x;
     const size_t first = tile * U * 256;
     if (first + U * 256 > n16) return;  // whole tiles only (sizes here are multiples)
     const size_t tile_byte = first * 16;
@@ -100,12 +104,13 @@ int main(int argc, char** argv) {
             }
         }
         struct V {
-            int u, cap;
+            int u, cap, xcd;
             std::vector<double> us;
         };
         std::vector<V> vs;
         for (int u : {1, 2, 4})
-            for (int cap : {2, 4, 8, 0}) vs.push_back({u, cap, {}});
+            for (int cap : {2, 4, 8, 0}) vs.push_back({u, cap, 0, {}});
+        for (int u : {1, 2}) vs.push_back({u, 2, 1, {}});
         hipEvent_t e0, e1;
         CHECK(hipEventCreate(&e0));
         CHECK(hipEventCreate(&e1));
@@ -114,9 +119,14 @@ int main(int argc, char** argv) {
                 const size_t lds = v.cap ? (lds_cu / v.cap) & ~size_t(255) : 0;
                 const unsigned grid = static_cast<unsigned>(n16 / (v.u * 256));
                 auto launch = [&](int s) {
-                    if (v.u == 1) tree8<1><<<grid, 256, lds>>>(sets[s].p, n16);
-                    if (v.u == 2) tree8<2><<<grid, 256, lds>>>(sets[s].p, n16);
-                    if (v.u == 4) tree8<4><<<grid, 256, lds>>>(sets[s].p, n16);
+                    if (v.xcd) {
+                        if (v.u == 1) tree8<1, 1><<<grid, 256, lds>>>(sets[s].p, n16);
+                        if (v.u == 2) tree8<2, 1><<<grid, 256, lds>>>(sets[s].p, n16);
+                        return;
+                    }
+                    if (v.u == 1) tree8<1, 0><<<grid, 256, lds>>>(sets[s].p, n16);
+                    if (v.u == 2) tree8<2, 0><<<grid, 256, lds>>>(sets[s].p, n16);
+                    if (v.u == 4) tree8<4, 0><<<grid, 256, lds>>>(sets[s].p, n16);
                 };
                 for (int s = 0; s < sh.sets; ++s) launch(s);
                 CHECK(hipEventRecord(e0));
@@ -144,9 +154,9 @@ int main(int argc, char** argv) {
         for (auto& v : vs) {
             std::sort(v.us.begin(), v.us.end());
             const double med = v.us[v.us.size() / 2];
-            std::printf("{\"mib_per_peer\": %zu, \"U\": %d, \"wg_per_cu_cap\": %d, \"median_us\": %.2f, \"min_us\": %.2f, "
-                        "\"frac\": %.4f, \"bits_ok\": %s}\n",
-                        sh.mib, v.u, v.cap, med, v.us.front(), 9.0 * bytes / (med * 1e-6) / 8e12, ok ? "true" : "false");
+            std::printf("{\"mib_per_peer\": %zu, \"U\": %d, \"wg_per_cu_cap\": %d, \"xcd_contiguous\": %d, \"median_us\": %.2f, "
+                        "\"min_us\": %.2f, \"frac\": %.4f, \"bits_ok\": %s}\n",
+                        sh.mib, v.u, v.cap, v.xcd, med, v.us.front(), 9.0 * bytes / (med * 1e-6) / 8e12, ok ? "true" : "false");
         }
         std::fflush(stdout);
         for (auto& s : sets)
