@@ -27,6 +27,7 @@
 #   bash tools/gpu_round5.sh k   8-in / 1-out tree shape, U = 1 / 2 / 4 lane groups per thread x a cap of 2 / 4 / 8 / no
 #                                workgroups per CU, slotted buckets, 1 GiB and 32 MiB per peer (tools/microbench_tree_u.hip)
 #   bash tools/gpu_round5.sh l   C5 local_peers at GPU_MAX_HW_QUEUES 4 / 8 / 16, twice (r05_c5_hwq.jsonl)
+#   bash tools/gpu_round5.sh m   C5 local_peers under rocprofv3 --kernel-trace --memory-copy-trace (r05_c5_trace*)
 #   bash tools/gpu_round5.sh z   the round-end sequence: GPU suite, smoke(), default line, C2 profile (r05z_*;
 #                                then tools/pmc_summarize.py --tag r05z_c2 --merge)
 set -o pipefail
@@ -162,6 +163,21 @@ print(json.dumps({'GPU_MAX_HW_QUEUES': int(os.environ['GPU_MAX_HW_QUEUES']), 'ms
 " >> gpurun_out/r05_c5_hwq.jsonl 2>> gpurun_out/r05_c5_hwq.err || exit 1
     done
     ;;
+m)
+    # C5's co-resident block under a kernel + memory-copy trace: where the 25 ms above the copy ceiling go
+    R=$PWD
+    cd /tmp
+    timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d $R/gpurun_out/r05_c5_trace \
+        -o run -- python3 -c "
+import sys, json
+sys.path.insert(0, '$R')
+import bench, fmi_amd
+fmi_amd.init(0)
+bench.quiet_device()
+lp = bench.c5_local_peers(8, 1024, iters=1)
+print(json.dumps({'ms': lp['ms'], 'ok': lp['self_check']['ok']}))
+" > $R/gpurun_out/r05_c5_trace.json 2> $R/gpurun_out/r05_c5_trace.err
+    ;;
 z)
     # the round-end sequence on the final library and bench: the whole GPU suite, smoke(), the default line, then
     # the C2 profile (kernel trace + stats, separate FETCH_SIZE / WRITE_SIZE passes, an unprofiled line)
@@ -172,7 +188,7 @@ z)
     bash tools/c2_profile.sh
     ;;
 *)
-    echo "usage: bash tools/gpu_round5.sh a|b|c|d|e|f|g|h|i|j|k|l|z" >&2
+    echo "usage: bash tools/gpu_round5.sh a|b|c|d|e|f|g|h|i|j|k|l|m|z" >&2
     exit 2
     ;;
 esac
