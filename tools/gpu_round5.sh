@@ -28,6 +28,8 @@
 #                                workgroups per CU, slotted buckets, 1 GiB and 32 MiB per peer (tools/microbench_tree_u.hip)
 #   bash tools/gpu_round5.sh l   C5 local_peers at GPU_MAX_HW_QUEUES 4 / 8 / 16, twice (r05_c5_hwq.jsonl)
 #   bash tools/gpu_round5.sh m   C5 local_peers under rocprofv3 --kernel-trace --memory-copy-trace (r05_c5_trace*)
+#   bash tools/gpu_round5.sh n   co-resident ranks' chunk-major first loads + small first chunks vs the build before
+#                                (build/ab_prev), 3 x interleaved (r05_c5_start_ab.jsonl); then step m on the library
 #   bash tools/gpu_round5.sh z   the round-end sequence: GPU suite, smoke(), default line, C2 profile (r05z_*;
 #                                then tools/pmc_summarize.py --tag r05z_c2 --merge)
 set -o pipefail
@@ -178,6 +180,25 @@ lp = bench.c5_local_peers(8, 1024, iters=1)
 print(json.dumps({'ms': lp['ms'], 'ok': lp['self_check']['ok']}))
 " > $R/gpurun_out/r05_c5_trace.json 2> $R/gpurun_out/r05_c5_trace.err
     ;;
+n)
+    # the library against the previous build (build/ab_prev: before the co-resident ranks' chunk-major first loads
+    # and small first chunks), separate processes interleaved three times; then the library under the copy trace
+    for k in 1 2 3; do
+        for lib in fmi_amd/lib/libfmi_dev.so build/ab_prev/libfmi_dev.so; do
+            FMI_DEV_LIB=$PWD/$lib timeout -k 10 200 python -u -c "
+import json, os, bench, fmi_amd
+fmi_amd.init(0)
+bench.quiet_device()
+p1 = bench.c5_p1_copy(1024)
+bench.quiet_device()
+lp = bench.c5_local_peers(8, 1024)
+print(json.dumps({'lib': os.environ['FMI_DEV_LIB'].split('/repo/')[-1], 'p1_copy_ms': p1['ms'], 'p1_ok': p1['self_check']['ok'],
+                  'local_peers_ms': lp['ms'], 'local_peers_GB_s': lp['pcie_GB_s_both_directions'], 'lp_ok': lp['self_check']['ok']}))
+" >> gpurun_out/r05_c5_start_ab.jsonl 2>> gpurun_out/r05_c5_start_ab.err || exit 1
+        done
+    done
+    rm -rf gpurun_out/r05_c5_trace && bash tools/gpu_round5.sh m
+    ;;
 z)
     # the round-end sequence on the final library and bench: the whole GPU suite, smoke(), the default line, then
     # the C2 profile (kernel trace + stats, separate FETCH_SIZE / WRITE_SIZE passes, an unprofiled line)
@@ -188,7 +209,7 @@ z)
     bash tools/c2_profile.sh
     ;;
 *)
-    echo "usage: bash tools/gpu_round5.sh a|b|c|d|e|f|g|h|i|j|k|l|m|z" >&2
+    echo "usage: bash tools/gpu_round5.sh a|b|c|d|e|f|g|h|i|j|k|l|m|n|z" >&2
     exit 2
     ;;
 esac
