@@ -1911,23 +1911,7 @@ static int comm_allreduce_host_impl(fmi_comm_t comm, int op, int dtype, int alg,
         chunk = std::max<size_t>(static_cast<size_t>(bytes) / esz, kShardAlign);
     }
     chunk = std::min(chunk, n);
-    // Chunk spans (offset, length). Co-resident ranks of a bucket of >= 4 chunks start small (c/8, c/4, c/2, then
-    // c): their first results can drain only once EVERY rank's first chunk has loaded through the one shared H2D
-    // stream, so the first chunk sets how long the D2H direction idles at the start (a memory-copy trace of 8 ranks
-    // x 1 GiB at 64 MiB chunks: 20 ms before the first D2H, profiles/r05_c5_trace_summary.json). Every rank of the
-    // communicator derives the same spans from (n, chunk); the bits do not depend on them.
-    std::vector<std::pair<size_t, size_t>> spans;
-    {
-        const size_t a = kShardAlign;
-        size_t off = 0;
-        if (c->t->co_resident() && n >= 4 * chunk && chunk / 8 >= a)
-            for (size_t len : {chunk / 8 / a * a, chunk / 4 / a * a, chunk / 2 / a * a}) {
-                spans.emplace_back(off, len);
-                off += len;
-            }
-        for (; off < n; off += chunk) spans.emplace_back(off, std::min(chunk, n - off));
-    }
-    const size_t nchunks = spans.size();
+    const size_t nchunks = (n + chunk - 1) / chunk;
     static constexpr int kIn[3] = {4, 5, 16}, kOut[3] = {6, 7, 17};
     char* in[HostPipe::kDepth] = {};
     char* out[HostPipe::kDepth] = {};
@@ -1937,18 +1921,15 @@ static int comm_allreduce_host_impl(fmi_comm_t comm, int op, int dtype, int alg,
     }
     const char* src = static_cast<const char*>(send);
     char* dst = static_cast<char*>(recv);
-    auto span = [&](size_t k) { return spans[k].second; };
+    auto span = [&](size_t k) { return std::min(chunk, n - k * chunk); };
     auto load = [&](size_t k) -> int {
         const int j = static_cast<int>(k % D);
         if (k >= static_cast<size_t>(D)) FMI_COMM_HIP(hipStreamWaitEvent(p.h2d, p.reduced[j], 0));
-        FMI_COMM_HIP(hipMemcpyAsync(in[j], src + spans[k].first * esz, span(k) * esz, hipMemcpyDefault, p.h2d));
+        FMI_COMM_HIP(hipMemcpyAsync(in[j], src + k * chunk * esz, span(k) * esz, hipMemcpyDefault, p.h2d));
         FMI_COMM_HIP(hipEventRecord(p.loaded[j], p.h2d));
         return FMI_OK;
     };
     FMI_COMM_RC(load(0));
-    // Co-resident ranks: every rank's first load is queued on the shared H2D stream before any rank's second (a
-    // host-only barrier: this rank's allreduce stream holds no work yet), so chunk 0 of all ranks lands first.
-    if (c->t->co_resident()) FMI_COMM_RC(c->t->barrier(p.cs));
     for (size_t k = 0; k < nchunks; ++k) {
         if (k + 1 < nchunks) FMI_COMM_RC(load(k + 1));
         const int j = static_cast<int>(k % D);
@@ -1963,7 +1944,7 @@ static int comm_allreduce_host_impl(fmi_comm_t comm, int op, int dtype, int alg,
         FMI_COMM_RC(allreduce_device(c, op, dtype, alg, path, in[j], out[j], span(k), p.cs));
         FMI_COMM_HIP(hipEventRecord(p.reduced[j], p.cs));
         FMI_COMM_HIP(hipStreamWaitEvent(p.d2h, p.reduced[j], 0));
-        FMI_COMM_HIP(hipMemcpyAsync(dst + spans[k].first * esz, out[j], span(k) * esz, hipMemcpyDefault, p.d2h));
+        FMI_COMM_HIP(hipMemcpyAsync(dst + k * chunk * esz, out[j], span(k) * esz, hipMemcpyDefault, p.d2h));
         FMI_COMM_HIP(hipEventRecord(p.drained[j], p.d2h));
     }
     // this communicator's last result copy (the shared D2H stream may already carry other ranks' later chunks)
