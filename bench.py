@@ -1137,6 +1137,9 @@ def c5_local_peers(peers: int, mib: int, iters: int = 2, chunk_mib: int = 64) ->
             "mem_available_gib": round(avail / GIB, 1) if avail else None,
             "ms": round(ms, 2), "host_buckets_GiB_s": round(peers * S / GIB / (ms * 1e-3), 2),
             "pcie_GB_s_both_directions": round(2 * peers * S / (ms * 1e-3) / 1e9, 1), "iters": iters,
+            "ceiling": ("the copies alone, issued the same way (8 x 1 GiB each way on the device's one H2D + one D2H "
+                        "stream, no compute): 177.97 ms = 96.5 GB/s, profiles/r05_pcie_peers.jsonl "
+                        "(tools/microbench_pcie_peers.hip); DESIGN.md section 8"),
             "self_check": {"ok": bad == 0, "mismatches": bad, "elements_checked": len(offs) * win * peers,
                            "against": "numpy float32 evaluation of each rank's allreduce_no_order bracketing "
                                       "(fmi_schedule_expr) over the peers' windows, three windows, bit-exact"}}
