@@ -30,6 +30,7 @@
 #   bash tools/gpu_round5.sh m   C5 local_peers under rocprofv3 --kernel-trace --memory-copy-trace (r05_c5_trace*)
 #   bash tools/gpu_round5.sh n   co-resident ranks' chunk-major first loads + small first chunks vs the build before
 #                                (build/ab_prev), 3 x interleaved (r05_c5_start_ab.jsonl); then step m on the library
+#   bash tools/gpu_round5.sh o   the pair kernel's sc1 tiles re-checked on slotted buckets (r05_ab_pair_sc1.jsonl)
 #   bash tools/gpu_round5.sh z   the round-end sequence: GPU suite, smoke(), default line, C2 profile (r05z_*;
 #                                then tools/pmc_summarize.py --tag r05z_c2 --merge)
 set -o pipefail
@@ -199,6 +200,14 @@ print(json.dumps({'lib': os.environ['FMI_DEV_LIB'].split('/repo/')[-1], 'p1_copy
     done
     rm -rf gpurun_out/r05_c5_trace && bash tools/gpu_round5.sh m
     ;;
+o)
+    # the pair kernel's sc1 tiles (FMI_TUNE_PAIR_SC1_OF_8 0 / 1 / 2 / 4) re-checked on slotted buckets: C2 (256 MiB,
+    # 16 sets) and C3's i64 shape (64 MiB, 64 sets)
+    timeout -k 10 300 python -u tools/ab_pair_sc1.py --rounds 5 --mib 256 --sets 16 --budgets 0,1,2,4 \
+        > gpurun_out/r05_ab_pair_sc1.jsonl 2> gpurun_out/r05_ab_pair_sc1.err &&
+    timeout -k 10 300 python -u tools/ab_pair_sc1.py --rounds 5 --mib 64 --sets 64 --dtype i64 --budgets 0,1,2,4 \
+        >> gpurun_out/r05_ab_pair_sc1.jsonl 2>> gpurun_out/r05_ab_pair_sc1.err
+    ;;
 z)
     # the round-end sequence on the final library and bench: the whole GPU suite, smoke(), the default line, then
     # the C2 profile (kernel trace + stats, separate FETCH_SIZE / WRITE_SIZE passes, an unprofiled line)
@@ -209,7 +218,7 @@ z)
     bash tools/c2_profile.sh
     ;;
 *)
-    echo "usage: bash tools/gpu_round5.sh a|b|c|d|e|f|g|h|i|j|k|l|m|n|z" >&2
+    echo "usage: bash tools/gpu_round5.sh a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|z" >&2
     exit 2
     ;;
 esac
