@@ -375,3 +375,19 @@ def test_cpu_baseline_falls_back_to_the_port_only_without_oracle_ref(monkeypatch
     got = bench.cpu_baseline(_light_cpu_baseline(monkeypatch))
     assert got["kind"] == "port" and got["value"] == got["port_value"] and got["reference_combine_ms"] is None
     assert got["reference_error"] == "oracle/_ref not built"
+
+
+def test_line_names_the_bucket_placement():
+    """The N = 1 / N > 1 line's config.placement says how the device buckets were placed: the
+    allocator's rotating 4 KiB slots by default, plain hipMalloc when FMI_TUNE_ALLOC_SLOTS = 0."""
+    import fmi_amd
+
+    old = fmi_amd.tune_get(fmi_amd.Tune.ALLOC_SLOTS)
+    try:
+        assert old == 1 and "FMI_TUNE_ALLOC_SLOTS = 1" in bench.placement()
+        fmi_amd.tune_set(fmi_amd.Tune.ALLOC_SLOTS, 0)
+        assert "plain hipMalloc" in bench.placement()
+        with pytest.raises(fmi_amd.FmiError):
+            fmi_amd.tune_set(fmi_amd.Tune.ALLOC_SLOTS, 3)
+    finally:
+        fmi_amd.tune_set(fmi_amd.Tune.ALLOC_SLOTS, old)
