@@ -31,6 +31,7 @@
 #   bash tools/gpu_round5.sh n   co-resident ranks' chunk-major first loads + small first chunks vs the build before
 #                                (build/ab_prev), 3 x interleaved (r05_c5_start_ab.jsonl); then step m on the library
 #   bash tools/gpu_round5.sh o   the pair kernel's sc1 tiles re-checked on slotted buckets (r05_ab_pair_sc1.jsonl)
+#   bash tools/gpu_round5.sh p   bench.py --force-dist at world 1 over RCCL with C5 at 1 GiB (r05_force_dist_c5.json)
 #   bash tools/gpu_round5.sh z   the round-end sequence: GPU suite, smoke(), default line, C2 profile (r05z_*;
 #                                then tools/pmc_summarize.py --tag r05z_c2 --merge)
 set -o pipefail
@@ -208,6 +209,13 @@ o)
     timeout -k 10 300 python -u tools/ab_pair_sc1.py --rounds 5 --mib 64 --sets 64 --dtype i64 --budgets 0,1,2,4 \
         >> gpurun_out/r05_ab_pair_sc1.jsonl 2>> gpurun_out/r05_ab_pair_sc1.err
     ;;
+p)
+    # the N > 1 code path at world size 1 over RCCL with the full exchange (--force-dist): C5's per-GPU pipeline with
+    # the real RCCL calls per chunk, 1 GiB (the closest one-GPU form of C5 as BASELINE states it)
+    timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node=1 --master-addr 127.0.0.1 \
+        --master-port 29533 bench.py --force-dist --steps 20 --warmup 5 --c5-mib 1024 --no-diagnostics \
+        > gpurun_out/r05_force_dist_c5.json 2> gpurun_out/r05_force_dist_c5.err
+    ;;
 z)
     # the round-end sequence on the final library and bench: the whole GPU suite, smoke(), the default line, then
     # the C2 profile (kernel trace + stats, separate FETCH_SIZE / WRITE_SIZE passes, an unprofiled line)
@@ -218,7 +226,7 @@ z)
     bash tools/c2_profile.sh
     ;;
 *)
-    echo "usage: bash tools/gpu_round5.sh a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|z" >&2
+    echo "usage: bash tools/gpu_round5.sh a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|z" >&2
     exit 2
     ;;
 esac
