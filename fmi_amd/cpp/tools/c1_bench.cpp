@@ -46,7 +46,7 @@ double median(std::vector<double> v) {
 void run_peer(std::vector<int> fds, peer_num p, peer_num P, size_t n, int reps, size_t chunk, int device,
               double* out) {
     Communicator comm(p, P, "", "c1");
-    if (device >= 0) comm.use_device(device);
+    if (device >= 0) comm.use_device(device, true);  // every combine on the GPU, whatever the crossover
     auto channel = std::make_shared<FMI::Comm::LocalSocket>(std::move(fds), 60000);
     comm.register_channel("Local", channel);
     std::vector<float> init(n);
