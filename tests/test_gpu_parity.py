@@ -1035,3 +1035,22 @@ def test_dev_alloc_places_buckets_in_rotating_slots(device):
         b.free()
     with pytest.raises(fmi_amd.FmiError):
         fmi_amd.tune_set(Tune.ALLOC_SLOTS, 2)
+
+
+@pytest.mark.parametrize("chunk", [(1 << 16), (3 << 20) + 4096, (64 << 20)])
+def test_host_reduce_pair_staging_sizes(device, chunk):
+    """The pooled staging sets grow to the largest chunk they served (a power of two from 64 KiB, capped at the
+    tuned host chunk, which need not be one): pageable pairs of 1 element to 9 MiB in every dtype width, under a
+    small, an odd and the default chunk, every result bit-exact."""
+    old = fmi_amd.tune_get(Tune.HOST_CHUNK)
+    try:
+        fmi_amd.tune_set(Tune.HOST_CHUNK, chunk)
+        for dtype, n in ((np.float32, 1), (np.int8, 65537), (np.float64, (1 << 17) + 3), (np.int16, (3 << 20) + 5),
+                         (np.float32, (9 << 18) + 1), (np.int64, (9 << 17) - 1)):
+            a, b = inputs(dtype, n, 3), inputs(dtype, n, 4)
+            got = a.copy()
+            fmi_amd.host_reduce_pair(Op.SUM, got, b)
+            with np.errstate(all="ignore"):
+                assert_bit_equal(got, orc.pairwise("sum", a, b), f"{np.dtype(dtype).name} n={n} chunk={chunk}")
+    finally:
+        fmi_amd.tune_set(Tune.HOST_CHUNK, old)
