@@ -22,7 +22,7 @@
 #   bash tools/gpu_round5.sh i   FMI_TUNE_FUSED_INFLIGHT_KIB x FMI_TUNE_FUSED_POLICY on slotted buckets: tree8 1 GiB /
 #                                32 MiB, scan8 64 MiB, two interleaved rounds (r05_fused_retune.jsonl); then the 8-peer
 #                                shared-stream DMA with and without a concurrent HBM copy loop (r05_pcie_busy.jsonl)
-#   bash tools/gpu_round5.sh j   host pipeline 3 vs 2 chunk slots (build/ab_d2), C5 p1_copy + local_peers, 3 x
+#   bash tools/gpu_round5.sh j   host pipeline 3 vs 2 chunk slots (build/ab_d2; remove it from .gpurunignore to rerun), 3 x
 #                                interleaved processes (r05_depth_ab.jsonl)
 #   bash tools/gpu_round5.sh k   8-in / 1-out tree shape, U = 1 / 2 / 4 lane groups per thread x a cap of 2 / 4 / 8 / no
 #                                workgroups per CU, slotted buckets, 1 GiB and 32 MiB per peer (tools/microbench_tree_u.hip)
