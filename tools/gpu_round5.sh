@@ -32,6 +32,7 @@
 #                                (build/ab_prev), 3 x interleaved (r05_c5_start_ab.jsonl); then step m on the library
 #   bash tools/gpu_round5.sh o   the pair kernel's sc1 tiles re-checked on slotted buckets (r05_ab_pair_sc1.jsonl)
 #   bash tools/gpu_round5.sh p   bench.py --force-dist at world 1 over RCCL with C5 at 1 GiB (r05_force_dist_c5.json)
+#   bash tools/gpu_round5.sh q   the N > 1 line at full size, 8 PROC ranks on one GPU (r05_bench_proc8_rehearsal.json)
 #   bash tools/gpu_round5.sh z   the round-end sequence: GPU suite, smoke(), default line, C2 profile (r05z_*;
 #                                then tools/pmc_summarize.py --tag r05z_c2 --merge)
 set -o pipefail
@@ -216,6 +217,13 @@ p)
         --master-port 29533 bench.py --force-dist --steps 20 --warmup 5 --c5-mib 1024 --no-diagnostics \
         > gpurun_out/r05_force_dist_c5.json 2> gpurun_out/r05_force_dist_c5.err
     ;;
+q)
+    # the N > 1 line rehearsed at full size with 8 ranks as processes on the one GPU (PROC transport over gloo):
+    # 256 MiB buckets, C4 at 1 GiB per peer, C5 at 1 GiB per rank, diagnostics on
+    FMI_PROC_TIMEOUT_S=300 timeout -k 10 1000 python -m torch.distributed.run --nnodes=1 --nproc-per-node=8 \
+        --master-addr 127.0.0.1 --master-port 29544 bench.py --gpus 8 --transport proc --steps 20 --warmup 3 \
+        --diag-deadline 600 > gpurun_out/r05_bench_proc8_rehearsal.json 2> gpurun_out/r05_bench_proc8_rehearsal.err
+    ;;
 z)
     # the round-end sequence on the final library and bench: the whole GPU suite, smoke(), the default line, then
     # the C2 profile (kernel trace + stats, separate FETCH_SIZE / WRITE_SIZE passes, an unprofiled line)
@@ -226,7 +234,7 @@ z)
     bash tools/c2_profile.sh
     ;;
 *)
-    echo "usage: bash tools/gpu_round5.sh a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|z" >&2
+    echo "usage: bash tools/gpu_round5.sh a|b|c|d|e|f|g|h|i|j|k|l|m|n|o|p|q|z" >&2
     exit 2
     ;;
 esac
