@@ -1230,15 +1230,23 @@ def run_dist(args, world, rank, local_rank):
     else:
         dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
         # the fallback agreement votes on a gloo group of its own: a vote can never pair with an RCCL collective
-        # of the timed loop that another rank is still inside. If gloo cannot connect here, the vote
-        # runs on the RCCL group as before (every rank fails the same way: the group is made collectively).
+        # of the timed loop that another rank is still inside. If gloo cannot connect on ANY rank, every
+        # rank votes on the RCCL group instead: the ranks agree on that here, over the world group, before anything
+        # else runs on it (ranks voting on different groups would hang).
         try:
             import datetime
 
             vote = dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=120))
         except Exception as e:  # noqa: BLE001 - the vote still happens, on the world group
-            print(f"bench: rank {rank}: no gloo group for the fallback vote ({type(e).__name__}: {e}); voting over "
-                  "the RCCL group", file=sys.stderr, flush=True)
+            print(f"bench: rank {rank}: no gloo group for the fallback vote ({type(e).__name__}: {e})",
+                  file=sys.stderr, flush=True)
+            vote = None
+        have = torch.tensor([0 if vote is None else 1], dtype=torch.int32, device=torch.device("cuda", dev))
+        dist.all_reduce(have, op=dist.ReduceOp.MIN)
+        if int(have.item()) == 0:
+            if vote is not None:
+                print(f"bench: rank {rank}: another rank has no gloo group: every rank votes over the RCCL group",
+                      file=sys.stderr, flush=True)
             vote = None
 
     import fmi_amd

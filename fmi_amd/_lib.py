@@ -67,6 +67,7 @@ SIGNATURES = {
     "fmi_dev_describe": (_i, [_c.c_char_p, _sz]),
     "fmi_dev_pci_bus_id": (_i, [_i, _c.c_char_p, _sz]),
     "fmi_dev_alloc": (_i, [_c.POINTER(_vp), _sz]),
+    "fmi_dev_alloc_group": (_i, [_c.POINTER(_vp), _i, _sz]),
     "fmi_dev_free": (_i, [_vp]),
     "fmi_host_pin_alloc": (_i, [_c.POINTER(_vp), _sz]),
     "fmi_host_pin_free": (_i, [_vp]),
@@ -96,6 +97,7 @@ SIGNATURES = {
     "fmi_dev_scan_peers": (_i, [_i, _i, _i, _c.POINTER(_vp), _c.POINTER(_vp), _i, _sz, _vp]),
     "fmi_host_reduce_pair": (_i, [_i, _i, _vp, _vp, _sz]),
     "fmi_host_device_ptr": (_i, [_vp, _sz, _c.POINTER(_vp)]),
+    "fmi_host_page_locked": (_i, [_vp, _sz]),
     "fmi_comm_unique_id": (_i, [_i, _vp, _sz]),
     "fmi_comm_init": (_i, [_c.POINTER(_vp), _vp, _i, _i]),
     "fmi_comm_init_timeout": (_i, [_c.POINTER(_vp), _vp, _i, _i, _c.c_double]),

@@ -206,10 +206,13 @@ private:
                     // per combine: the GPU where it pays, else the host loop (the same op, so the same bits)
                     auto part = [dop, op, policy = policy, always = offload_always_, last = last_on_device_](
                                     char* a, char* b, std::size_t off, std::size_t len) {
-                        void* d = nullptr;
-                        const bool pinned = fmi_host_device_ptr(a + off, len, &d) == FMI_OK &&
-                                            fmi_host_device_ptr(b + off, len, &d) == FMI_OK;
-                        if (always || policy->host_combine_on_device(len, pinned)) {
+                        // below the policy's smallest GPU size the answer is the host whatever the pinning: no
+                        // probe; above it a query that sets no error text (a pageable bucket is no error)
+                        const bool device = always || (len >= policy->host_combine_min_bytes() &&
+                                                       policy->host_combine_on_device(
+                                                           len, fmi_host_page_locked(a + off, len) == 1 &&
+                                                                    fmi_host_page_locked(b + off, len) == 1));
+                        if (device) {
                             last->store(true);
                             Dev::check(fmi_host_reduce_pair(dop.op, dop.dtype, a + off, b + off, len / sizeof(A)),
                                        "fmi_host_reduce_pair");

@@ -73,6 +73,18 @@ public:
         ptr_ = static_cast<A*>(p);
     }
     explicit Bucket(const std::vector<A>& host) : Bucket(host.size()) { upload(host); }
+    //! `count` buckets of n elements that one kernel streams together (a peer set's inputs and outputs): bucket j
+    //! in 4 KiB slot j mod 16 whatever was allocated before (fmi_dev_alloc_group).
+    static std::vector<Bucket> group(std::size_t count, std::size_t n) {
+        std::vector<void*> ptrs(count);
+        check(fmi_dev_alloc_group(ptrs.data(), static_cast<int>(count), n * sizeof(A)), "fmi_dev_alloc_group");
+        std::vector<Bucket> out(count);
+        for (std::size_t j = 0; j < count; ++j) {
+            out[j].ptr_ = static_cast<A*>(ptrs[j]);
+            out[j].n_ = n;
+        }
+        return out;
+    }
     //! A bucket over memory owned elsewhere (e.g. a communicator window): never freed by the bucket.
     static Bucket borrow(A* ptr, std::size_t n) {
         Bucket b;

@@ -51,6 +51,8 @@ public:
     virtual bool host_combine_on_device(std::size_t bucket_bytes, bool page_locked) const {
         return bucket_bytes >= (page_locked ? host_pinned_min_ : host_pageable_min_);
     }
+    //! Below this no host combine goes to the GPU, page-locked or not: the Communicator asks nothing more then.
+    virtual std::size_t host_combine_min_bytes() const { return std::min(host_pageable_min_, host_pinned_min_); }
     void set_host_combine_min_bytes(std::size_t pageable, std::size_t page_locked) {
         host_pageable_min_ = pageable;
         host_pinned_min_ = page_locked;

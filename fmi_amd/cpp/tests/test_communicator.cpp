@@ -1036,6 +1036,45 @@ GPU_TEST(host_combine_follows_the_policy_crossover) {
     }
 }
 
+GPU_TEST(pageable_host_combine_sets_no_error_text) {
+    // VERDICT r05 item 4 / ADVICE r05: a pageable bucket is the ordinary answer of the per-combine pinning probe,
+    // not an error. Below the policy's smallest GPU size no probe runs; above it the probe is a query
+    // (fmi_host_page_locked). Either way the peer thread's fmi_last_error() stays empty and the combine stays on
+    // the host (Loopback runs each combine on the peer's own thread).
+    for (std::size_t n : {std::size_t(1) << 18, (std::size_t(40) << 20) / 4 + 3}) {
+        bool clean[2] = {}, on_device[2] = {true, true};
+        with_peers(2, [&](Communicator& c, peer_num p) {
+            c.use_device(0);
+            Data<std::vector<float>> a(synth_f32(n, 9, p)), r(n);
+            c.allreduce(a, r, Function<std::vector<float>>(Op::sum));
+            clean[p] = std::string(fmi_last_error()).empty();
+            on_device[p] = c.last_host_combine_on_device();
+        });
+        for (int p = 0; p < 2; ++p) {
+            CHECK(clean[p]);
+            CHECK(!on_device[p]);
+        }
+    }
+}
+
+GPU_TEST(bucket_group_places_each_bucket_by_index) {
+    // Dev::Bucket<A>::group (fmi_dev_alloc_group): bucket j in 4 KiB slot j mod 16 modulo 64 KiB,
+    // whatever was allocated before; each is a working bucket freed by its destructor
+    Dev::init(0);
+    const std::size_t n = (std::size_t(1) << 20) / 4 + 7;
+    Dev::Bucket<float> before(n);
+    auto g = Dev::Bucket<float>::group(18, n);
+    CHECK(g.size() == 18);
+    for (std::size_t j = 0; j < g.size(); ++j) {
+        CHECK((reinterpret_cast<std::uintptr_t>(g[j].data()) % 65536) / 4096 == j % 16);
+        CHECK(g[j].size() == n);
+    }
+    g[3].fill_synthetic(4, 1);
+    const std::vector<float> x = g[3].download();
+    g[17].upload(x);
+    CHECK(std::memcmp(g[17].download().data(), x.data(), n * sizeof(float)) == 0);
+}
+
 GPU_TEST(device_buckets_need_builtin_op) {
     Dev::init(0);
     with_peers(1, [](Communicator& c, peer_num) {

@@ -279,9 +279,12 @@ public:
     // shards short or empty), so a bucket needs no zero padding. all_to_all_ragged: recv[j * shard ...] = rank
     // j's shard `rank` (span(rank) bytes); all_gather_ragged: recv[j * shard ...] = rank j's send (span(j)).
     virtual bool ragged() const { return false; }
-    // Several ranks of this communicator drive the same device from this process (their host pipelines share the
-    // device's copy streams, shared_copy_streams).
+    // Several ranks of this communicator drive the same device from this process: their host pipelines share one
+    // H2D and one D2H stream (copy_streams). Every other rank owns its pair (HostPipe::init).
     virtual bool co_resident() const { return false; }
+    virtual int copy_streams(hipStream_t*, hipStream_t*) {
+        return fail(FMI_ERR_UNSUPPORTED, "copy streams are shared only among co-resident ranks");
+    }
     virtual int all_to_all_ragged(const char*, char*, size_t, size_t, hipStream_t) {
         return fail(FMI_ERR_UNSUPPORTED, "transport has no ragged exchanges");
     }
@@ -596,7 +599,15 @@ private:
 // Ranks of one process on one device: a rendezvous hub per communicator id.
 struct Hub {
     explicit Hub(int n) : n(n), ptrs(n, nullptr) {}
+    ~Hub() {
+        // A poisoned hub's ranks may have left copies queued that never drain: leak the streams then.
+        if (!poisoned)
+            for (hipStream_t st : {h2d, d2h})
+                if (st) (void)hipStreamDestroy(st);
+    }
     int n;
+    // The host pipelines' copy streams, shared by this communicator's ranks only (LocalTransport::copy_streams).
+    hipStream_t h2d = nullptr, d2h = nullptr;
     std::mutex mu;
     std::condition_variable cv;
     int arrived = 0;
@@ -645,6 +656,14 @@ public:
     LocalTransport(std::shared_ptr<Hub> hub, int n, int rank) : Transport(n, rank), hub_(std::move(hub)) {}
 
     bool co_resident() const override { return n_ > 1; }  // the ranks are threads sharing this device
+    int copy_streams(hipStream_t* h2d, hipStream_t* d2h) override {
+        std::lock_guard<std::mutex> lk(hub_->mu);
+        for (hipStream_t* st : {&hub_->h2d, &hub_->d2h})
+            if (!*st) FMI_COMM_HIP(hipStreamCreateWithFlags(st, hipStreamNonBlocking));
+        *h2d = hub_->h2d;
+        *d2h = hub_->d2h;
+        return FMI_OK;
+    }
 
     // Every exchange below runs the RCCL transport's own plan (fmi_exchange_plan.h): each receive copies
     // from the matching send of the peer's plan (same peer order, same length, or the call fails), so the
@@ -1117,66 +1136,60 @@ private:
 // ---------------------------------------------------------------------------------------------------
 // communicator
 // ---------------------------------------------------------------------------------------------------
-// The host pipeline's DMA streams: ONE host -> device and ONE device -> host stream per device for the whole
-// process, shared by every communicator's fmi_comm_allreduce_host. The runtime hands its
-// DMA engines to streams: with one stream per direction the two directions run on separate engines, at the
-// link's duplex rate (1 GiB each way in 22.4 ms, 96 GB/s); with a pair per LOCAL rank (8 ranks, 16 copy streams)
-// the directions land on shared engines and serialise, 178-241 ms for 8 GiB each way depending on the streams
-// the runtime had handed out before, against 178.0 ms on one shared pair every time
-// (profiles/r05_pcie_peers.jsonl, tools/microbench_pcie_peers.hip). Per-rank order is kept by each rank's own
-// events; the ranks' chunks interleave on the shared streams in the order their threads issue them, which the
-// LOCAL rendezvous of every chunk keeps rank-major per chunk. Never destroyed (like the library stream).
-static int shared_copy_streams(hipStream_t* h2d, hipStream_t* d2h) {
-    static std::mutex mu;
-    static auto* by_device = new std::map<int, std::pair<hipStream_t, hipStream_t>>;
-    int device = -1;
-    FMI_COMM_HIP(hipGetDevice(&device));
-    std::lock_guard<std::mutex> lk(mu);
-    auto it = by_device->find(device);
-    if (it == by_device->end()) {
-        hipStream_t a = nullptr, b = nullptr;
-        FMI_COMM_HIP(hipStreamCreateWithFlags(&a, hipStreamNonBlocking));
-        const hipError_t e = hipStreamCreateWithFlags(&b, hipStreamNonBlocking);
-        if (e != hipSuccess) {
-            (void)hipStreamDestroy(a);
-            return fail(FMI_ERR_HIP, std::string("hipStreamCreateWithFlags (shared D2H stream): ") + hipGetErrorString(e));
-        }
-        it = by_device->emplace(device, std::make_pair(a, b)).first;
-    }
-    *h2d = it->second.first;
-    *d2h = it->second.second;
-    return FMI_OK;
-}
-
 // Streams and events of the host-ingress pipeline (fmi_comm_allreduce_host), created on first use: the chunk's
-// sharded allreduce runs on the communicator's own stream, the copies on the device's shared pair.
+// sharded allreduce runs on the communicator's own stream, the copies on one H2D and one D2H stream.
+//
+// Whose copy streams. The runtime hands its DMA engines to streams: with one stream per direction the two
+// directions run on separate engines at the link's duplex rate (1 GiB each way in 22.4 ms, 96 GB/s); with a pair per
+// co-resident LOCAL rank (8 ranks, 16 copy streams) the directions land on shared engines and serialise, 178-241 ms
+// for 8 GiB each way depending on the streams the runtime had handed out before, against 178.0 ms on one shared pair
+// every time (profiles/r05_pcie_peers.jsonl, tools/microbench_pcie_peers.hip). So the co-resident ranks of ONE
+// communicator share one pair (Transport::copy_streams, owned by their hub): each rank's order is kept by its own
+// events, and their chunks interleave in the order their threads issue them, which the LOCAL rendezvous of every
+// chunk keeps rank-major per chunk. Nothing wider shares a pair: two communicators whose loads waited
+// on each other's device events in one shared stream could be queued X-then-Y in one process and Y-then-X in
+// another and deadlock across processes, and an aborted communicator's undrained copies would block every later
+// one. Every other communicator's pipeline (one rank per device: RCCL, PROC, one-rank LOCAL) owns its pair.
 struct HostPipe {
-    // Chunk slots in flight: the load of chunk k waits for the allreduce of chunk k - depth. One rank per device
-    // (every communicator across GPUs): 2 — the wait paces the loads to the results draining, and the two
-    // directions stay overlapped (a 1 GiB one-rank pipeline 23.2-24.3 ms at 2, 32.7-33.0 ms at 3). Co-resident
-    // ranks sharing the device's copy streams (LOCAL): 3 — one rank's load waiting for its allreduce of chunk
-    // k - 2 would hold every other rank's loads behind it on the shared stream, and at depth 3 that wait is long
-    // finished when the load is queued (8 ranks x 1 GiB: 203-204 ms at 3, 217-240 ms at 2).
-    // profiles/r05_depth_ab.jsonl (build/ab_d2: make -C fmi_amd/csrc ab_depth2, FMI_HOST_PIPE_DEPTH=2 forces 2).
+    // Chunk slots in flight: the load of chunk k waits for the allreduce of chunk k - depth. One rank per device: 2 —
+    // the wait paces the loads to the results draining, and the two directions stay overlapped (a 1 GiB one-rank
+    // pipeline 23.2-24.3 ms at 2, 32.7-33.0 ms at 3). Co-resident ranks sharing their copy streams: 3 — one rank's
+    // load waiting for its allreduce of chunk k - 2 would hold every other rank's loads behind it on the shared
+    // stream, and at depth 3 that wait is long finished when the load is queued (8 ranks x 1 GiB: 203-204 ms at 3,
+    // 217-240 ms at 2; profiles/r05_depth_ab.jsonl).
     static constexpr int kDepth = 3;  // slots allocated
     hipStream_t cs = nullptr;   // the chunk's sharded allreduce (this communicator's own)
-    hipStream_t h2d = nullptr;  // host -> device loads (shared_copy_streams: not owned)
-    hipStream_t d2h = nullptr;  // device -> host results (shared_copy_streams: not owned)
+    hipStream_t h2d = nullptr;  // host -> device loads
+    hipStream_t d2h = nullptr;  // device -> host results
+    bool owns_copy_streams = false;  // false: the co-resident ranks' pair (their hub owns it)
     hipEvent_t loaded[kDepth] = {}, reduced[kDepth] = {}, drained[kDepth] = {};
     bool ready = false;
 
-    int init() {
+    int depth() const { return owns_copy_streams ? 2 : kDepth; }
+
+    int init(Transport& t) {
         if (ready) return FMI_OK;
-        FMI_COMM_RC(shared_copy_streams(&h2d, &d2h));
-        FMI_COMM_HIP(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+        if (!h2d) {
+            if (t.co_resident()) {
+                FMI_COMM_RC(t.copy_streams(&h2d, &d2h));
+            } else {
+                owns_copy_streams = true;
+                for (hipStream_t* st : {&h2d, &d2h})
+                    if (!*st) FMI_COMM_HIP(hipStreamCreateWithFlags(st, hipStreamNonBlocking));
+            }
+        }
+        if (!cs) FMI_COMM_HIP(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
         for (int k = 0; k < kDepth; ++k)
             for (hipEvent_t* ev : {&loaded[k], &reduced[k], &drained[k]})
-                FMI_COMM_HIP(hipEventCreateWithFlags(ev, hipEventDisableTiming));
+                if (!*ev) FMI_COMM_HIP(hipEventCreateWithFlags(ev, hipEventDisableTiming));
         ready = true;
         return FMI_OK;
     }
     ~HostPipe() {
         if (cs) (void)hipStreamDestroy(cs);
+        if (owns_copy_streams)
+            for (hipStream_t st : {h2d, d2h})
+                if (st) (void)hipStreamDestroy(st);
         for (int k = 0; k < kDepth; ++k)
             for (hipEvent_t ev : {loaded[k], reduced[k], drained[k]})
                 if (ev) (void)hipEventDestroy(ev);
@@ -1304,13 +1317,18 @@ struct Comm {
             bool drained = Transport::drain(library_stream(), 10.0);
             for (hipStream_t st : {pipe.cs, chunks.gs})
                 if (st) drained = Transport::drain(st, 10.0) && drained;
-            // the shared copy streams carry other communicators' chunks too: only this one's copies are waited for
+            // copy streams shared with the other co-resident ranks carry their chunks too: only this rank's copies
+            // are waited for (its own pair is drained whole)
+            if (pipe.owns_copy_streams)
+                for (hipStream_t st : {pipe.h2d, pipe.d2h})
+                    if (st) drained = Transport::drain(st, 10.0) && drained;
             for (int k = 0; k < HostPipe::kDepth; ++k)
                 for (hipEvent_t ev : {pipe.loaded[k], pipe.drained[k]})
                     if (ev) drained = Transport::drain_event(ev, 10.0) && drained;
             for (auto& [st, ev] : user_tail) drained = Transport::drain_event(ev, 10.0) && drained;
             if (!drained) {
                 pipe.cs = chunks.gs = nullptr;
+                pipe.owns_copy_streams = false;  // leaked with the rest
                 for (int k = 0; k < HostPipe::kDepth; ++k) pipe.loaded[k] = pipe.reduced[k] = pipe.drained[k] = nullptr;
                 for (void*& b : buf) b = nullptr;
                 windows.clear();
@@ -1885,8 +1903,8 @@ static int comm_allreduce_impl(fmi_comm_t comm, int op, int dtype, int alg, int 
     return allreduce_device(c, op, dtype, alg, path, send, recv, n, resolve_stream(stream));
 }
 
-// Three-stage pipeline over HostPipe::kDepth chunk slots: while chunk k is allreduced on pipe.cs, chunk k+1 loads on
-// pipe.h2d and chunk k-1 drains on pipe.d2h (the device's shared copy streams, shared_copy_streams). Slot reuse is
+// Three-stage pipeline over HostPipe::depth() chunk slots: while chunk k is allreduced on pipe.cs, chunk k+1 loads on
+// pipe.h2d and chunk k-1 drains on pipe.d2h (HostPipe: whose copy streams). Slot reuse is
 // ordered by events: a load into slot j waits until the allreduce that read it (chunk k - kDepth) has finished
 // (reduced), an allreduce into slot j waits until the previous result in it has drained to the host.
 static int comm_allreduce_host_impl(fmi_comm_t comm, int op, int dtype, int alg, int path, const void* send, void* recv,
@@ -1898,12 +1916,8 @@ static int comm_allreduce_host_impl(fmi_comm_t comm, int op, int dtype, int alg,
     Comm* c = static_cast<Comm*>(comm);
     std::lock_guard<std::mutex> lk(c->mu);
     HostPipe& p = c->pipe;
-    FMI_COMM_RC(p.init());
-#ifdef FMI_HOST_PIPE_DEPTH
-    const int D = FMI_HOST_PIPE_DEPTH;
-#else
-    const int D = c->t->co_resident() ? HostPipe::kDepth : 2;
-#endif
+    FMI_COMM_RC(p.init(*c->t));
+    const int D = p.depth();
     const size_t esz = dtype_size(dtype);
     if (chunk == 0) {
         long long bytes = 0;
@@ -1912,7 +1926,7 @@ static int comm_allreduce_host_impl(fmi_comm_t comm, int op, int dtype, int alg,
     }
     chunk = std::min(chunk, n);
     const size_t nchunks = (n + chunk - 1) / chunk;
-    static constexpr int kIn[3] = {4, 5, 16}, kOut[3] = {6, 7, 17};
+    static constexpr int kIn[HostPipe::kDepth] = {4, 5, 16}, kOut[HostPipe::kDepth] = {6, 7, 17};  // Comm scratch slots
     char* in[HostPipe::kDepth] = {};
     char* out[HostPipe::kDepth] = {};
     for (int j = 0; j < D && static_cast<size_t>(j) < nchunks; ++j) {

@@ -47,7 +47,7 @@ DeviceState g_state;
 constexpr size_t kSlotBytes = 4096, kSlots = 16, kSlotSpan = kSlotBytes * kSlots, kSlotMinBytes = size_t(1) << 20;
 std::mutex g_slots_mu;
 size_t g_next_slot = 0;
-std::map<void*, void*> g_slotted;  // pointer handed out -> its hipMalloc base  // one process drives one device (one process per GPU, as FMI runs one peer per process)
+std::map<void*, void*> g_slotted;  // pointer handed out -> its hipMalloc base
 
 // Host-ingress pipeline of fmi_host_reduce_pair: two slots of (a, b) device staging and two streams per SET. The
 // reference's peers combine concurrently when they are threads of one process (its allreduce's peers each call
@@ -976,7 +976,10 @@ int fmi_dev_alloc(void** ptr, size_t bytes) {
     const bool slotted = bytes >= kSlotMinBytes && bytes <= SIZE_MAX - kSlotSpan && g_tune[FMI_TUNE_ALLOC_SLOTS].load() != 0;
     void* base = nullptr;
     const hipError_t e = hipMalloc(&base, std::max<size_t>(bytes, 1) + (slotted ? kSlotSpan : 0));
-    if (e != hipSuccess) return fail(FMI_ERR_ALLOC, "hipMalloc(" + std::to_string(bytes) + "): " + hipGetErrorString(e));
+    if (e != hipSuccess) {
+        (void)hipGetLastError();  // not left for the next launch's error check to find
+        return fail(FMI_ERR_ALLOC, "hipMalloc(" + std::to_string(bytes) + "): " + hipGetErrorString(e));
+    }
     if (!slotted) {
         *ptr = base;
         return FMI_OK;
@@ -985,6 +988,34 @@ int fmi_dev_alloc(void** ptr, size_t bytes) {
     char* p = static_cast<char*>(base) + (g_next_slot++ % kSlots) * kSlotBytes;
     g_slotted[p] = base;
     *ptr = p;
+    return FMI_OK;
+}
+
+int fmi_dev_alloc_group(void** ptrs, int count, size_t bytes) {
+    if (!ptrs || count < 0) return fail(FMI_ERR_INVALID, "bad group");
+    for (int j = 0; j < count; ++j) ptrs[j] = nullptr;
+    if (int rc = require_device()) return rc;
+    const bool slotted = bytes >= kSlotMinBytes && bytes <= SIZE_MAX - kSlotSpan;
+    for (int j = 0; j < count; ++j) {
+        void* base = nullptr;
+        const hipError_t e = hipMalloc(&base, std::max<size_t>(bytes, 1) + (slotted ? kSlotSpan : 0));
+        if (e != hipSuccess) {
+            (void)hipGetLastError();  // not left for the next launch's error check to find
+            const std::string msg = "hipMalloc(" + std::to_string(bytes) + ") for group bucket " + std::to_string(j) +
+                                    ": " + hipGetErrorString(e);
+            for (int i = 0; i < j; ++i) (void)fmi_dev_free(ptrs[i]);
+            for (int i = 0; i < j; ++i) ptrs[i] = nullptr;
+            return fail(FMI_ERR_ALLOC, msg);
+        }
+        if (!slotted) {
+            ptrs[j] = base;
+            continue;
+        }
+        char* p = static_cast<char*>(base) + (static_cast<size_t>(j) % kSlots) * kSlotBytes;
+        std::lock_guard<std::mutex> lk(g_slots_mu);
+        g_slotted[p] = base;
+        ptrs[j] = p;
+    }
     return FMI_OK;
 }
 
@@ -1040,6 +1071,17 @@ int fmi_host_device_ptr(const void* host, size_t bytes, void** dev) {
         return fail(FMI_ERR_INVALID, "fmi_host_device_ptr: the range is not wholly inside one page-locked, device-mapped "
                                      "range (fmi_host_pin_alloc / fmi_host_register)");
     return FMI_OK;
+}
+
+int fmi_host_page_locked(const void* host, size_t bytes) {
+    if (!host || bytes == 0 || g_state.device < 0) return 0;
+    int cur = -1;
+    if (hipGetDevice(&cur) != hipSuccess || (cur != g_state.device && hipSetDevice(g_state.device) != hipSuccess)) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    void* d = nullptr;
+    return host_mapped(const_cast<void*>(host), bytes, &d) ? 1 : 0;
 }
 
 static int copy_async(void* dst, const void* src, size_t bytes, hipMemcpyKind kind, fmi_stream_t stream) {

@@ -154,6 +154,22 @@ class Bucket:
         return self.n * self.itemsize
 
     @classmethod
+    def group(cls, count: int, n: int, dtype) -> list:
+        """`count` buckets that one kernel streams together (a fused kernel's peers and outputs, a pair's two
+        operands): fmi_dev_alloc_group puts bucket j in 4 KiB slot j mod 16, whatever was allocated before
+        (DESIGN §4)."""
+        dt = dtype_of(dtype) if not isinstance(dtype, DType) else dtype
+        nbytes = int(n) * np.dtype(NP_DTYPE[dt]).itemsize
+        ptrs = (ctypes.c_void_p * max(int(count), 1))()
+        _lib.call("fmi_dev_alloc_group", ptrs, int(count), nbytes)
+        out = []
+        for j in range(int(count)):
+            b = cls(n, dt, ptr=ptrs[j])
+            b._owns = True
+            out.append(b)
+        return out
+
+    @classmethod
     def from_numpy(cls, arr: np.ndarray, stream=None) -> "Bucket":
         arr = np.ascontiguousarray(arr)
         b = cls(arr.size, dtype_of(arr))

@@ -108,6 +108,11 @@ int fmi_dev_pci_bus_id(int device, char* buf, size_t len);
  * fmi_dev_free only (the pointer may lie inside its hipMalloc, up to 60 KiB past its base, so it is not a
  * hipIpcGetMemHandle base either: memory shared across processes comes from fmi_comm_window_alloc). */
 int fmi_dev_alloc(void** ptr, size_t bytes);
+/* fmi_dev_alloc_group: `count` buckets of `bytes` each that one kernel streams together (a fused kernel's P
+ * inputs and its outputs). Buckets of >= 1 MiB: bucket j sits in 4 KiB slot j mod 16 (modulo 64 KiB) of its own
+ * hipMalloc, whatever was allocated before and whatever FMI_TUNE_ALLOC_SLOTS says, so the group's streams never
+ * collide in HBM. All or nothing: on failure every ptrs[j] is NULL. Free each with fmi_dev_free. */
+int fmi_dev_alloc_group(void** ptrs, int count, size_t bytes);
 int fmi_dev_free(void* ptr);
 int fmi_host_pin_alloc(void** ptr, size_t bytes);  /* page-locked host memory for recv buffers */
 int fmi_host_pin_free(void* ptr);
@@ -124,6 +129,10 @@ int fmi_host_unregister(void* ptr);
  * (fmi_host_pin_alloc / fmi_host_register): what a caller hands to fmi_dev_reduce_pair to combine host recv
  * buffers in place over PCIe. FMI_ERR_INVALID for pageable or straddling ranges. */
 int fmi_host_device_ptr(const void* host, size_t bytes, void** dev);
+/* 1 if [host, host + bytes) lies wholly inside one page-locked, device-mapped range, else 0 (also before
+ * fmi_dev_init). A query, not a request: it never sets fmi_last_error (the Communicator asks it per host combine,
+ * where a pageable bucket is the ordinary answer, ChannelPolicy::host_combine_on_device). */
+int fmi_host_page_locked(const void* host, size_t bytes);
 int fmi_dev_h2d_async(void* dst, const void* src, size_t bytes, fmi_stream_t stream);
 int fmi_dev_d2h_async(void* dst, const void* src, size_t bytes, fmi_stream_t stream);
 int fmi_dev_d2d_async(void* dst, const void* src, size_t bytes, fmi_stream_t stream);

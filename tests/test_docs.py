@@ -66,3 +66,59 @@ def test_cited_driver_records_exist(doc):
     text = open(os.path.join(ROOT, doc), encoding="utf-8").read()
     missing = sorted({r for r in DRIVER.findall(text) if not os.path.exists(os.path.join(ROOT, r))})
     assert not missing, f"{doc} cites driver records that do not exist: {missing}"
+
+
+# ---- figures quoted from the line's cpu_baseline and c5 blocks -----------------------------
+NUM = re.compile(r"(?<![\w.])(\d{1,3}(?:,\d{3})+(?:\.\d+)?|\d+\.\d+)(?![\w.]*\d)")
+QUOTES = re.compile(r"cpu_baseline|(?<![\w/-])c5(?:[._]|\b)")
+RECORD_GLOBS = ["BENCH_r0*.json", "profiles/*.json", "profiles/*.jsonl", "profiles/*.log", "profiles/*.txt",
+                "profiles/*.csv", "profiles/archive/*"]
+
+
+def _record_figures():
+    """Every decimal figure in a committed record, at every rounding from its own precision down to 0 places."""
+    out = set()
+    for g in RECORD_GLOBS:
+        for path in glob.glob(os.path.join(ROOT, g)):
+            if not os.path.isfile(path):
+                continue
+            text = open(path, encoding="utf-8", errors="replace").read()
+            for m in re.finditer(r"-?\d+(?:\.\d+)?(?:[eE][-+]?\d+)?", text):
+                v = float(m.group(0))
+                mant = m.group(0).split("e")[0].split("E")[0]
+                digits = len(mant.split(".")[1]) if "." in mant else 0
+                for d in range(0, digits + 1):
+                    out.add(f"{abs(v):.{d}f}")
+                for d in range(0, 3):  # kernel traces hold ns: the same figure in µs or ms
+                    out.add(f"{abs(v) / 1e3:.{d}f}")
+                    out.add(f"{abs(v) / 1e6:.{d}f}")
+    return out
+
+
+def _segments(text):
+    """Table rows one by one, other text by paragraph."""
+    for block in re.split(r"\n\s*\n", text):
+        lines = block.splitlines()
+        if lines and all(x.lstrip().startswith("|") for x in lines):
+            yield from lines
+        else:
+            yield " ".join(lines)
+
+
+@pytest.mark.parametrize("doc", ["DESIGN.md", "INTEGRATION.md"])
+def test_quoted_cpu_baseline_and_c5_figures_match_a_record(doc):
+    """A sentence (paragraph or table row) that names the line's `cpu_baseline` or `c5` blocks may quote only decimal
+    figures found in a committed record (BENCH_r0N.json, profiles/…), at the precision quoted: a number that no
+    record holds is a transcription error or a figure whose evidence is gone."""
+    figures = _record_figures()
+    bad = []
+    for seg in _segments(open(os.path.join(ROOT, doc), encoding="utf-8").read()):
+        if not QUOTES.search(seg):
+            continue
+        for raw in NUM.findall(seg):
+            f = raw.replace(",", "")
+            if "." not in f:
+                continue
+            if f not in figures:
+                bad.append((f, seg[:120]))
+    assert not bad, f"{doc} quotes figures no committed record holds: {bad}"

@@ -307,11 +307,12 @@ def test_comm_allreduce_host_pipeline(device, N, pinned):
             assert_bit_equal(res[r][1], xs[r], "send bucket untouched")
 
 
-def test_comm_allreduce_host_concurrent_communicators_share_copy_streams(device):
-    """Every communicator's host pipeline issues its copies on the device's ONE H2D and ONE D2H stream
-    (shared_copy_streams): three independent LOCAL communicators (1, 2 and 4 ranks: pipeline depth 2, 3 and 3)
-    run host allreduces at the same time, several calls each with different chunkings, so their chunks interleave
-    on the shared streams. Every rank's result equals the oracle's bit for bit."""
+def test_comm_allreduce_host_concurrent_communicators(device):
+    """Host pipelines of independent communicators at the same time (fmi_comm.hip HostPipe): three LOCAL
+    communicators (1, 2 and 4 ranks: a one-rank pipeline on its own copy-stream pair at depth 2, the co-resident
+    ranks of each larger one sharing their communicator's pair at depth 3) run host allreduces concurrently, several
+    calls each with different chunkings, so their copies overlap on the device's DMA engines. Every rank's result
+    equals the oracle's bit for bit."""
     sizes = {1: 9 * 4096 + 3, 2: 7 * 4096 + 5, 4: 11 * 4096 + 7}
     results, errors = {}, []
 
@@ -339,6 +340,41 @@ def test_comm_allreduce_host_concurrent_communicators_share_copy_streams(device)
             want, _ = orc.allreduce(xs[k], orc.OPS["sum"])
             for r in range(N):
                 assert_bit_equal(res[r][k], want[r], f"communicator N={N} call {k} rank {r}")
+
+
+def test_comm_allreduce_host_after_an_aborted_communicator(device):
+    """an aborted communicator must not hold up the host pipelines of later ones. A 2-rank LOCAL
+    communicator whose rank 1 never calls times out in its host allreduce (rank 0 has queued chunk copies by then);
+    then a new 2-rank communicator and a new one-rank communicator run host allreduces, bit-exact against the
+    oracle, well inside the old communicator's timeout."""
+    import time
+
+    from fmi_amd.comm import Timeout
+
+    uid = unique_id(Transport.LOCAL)
+    n, chunk = 5 * 4099 + 3, 4099
+
+    def absent():
+        c = Comm(uid, 2, 1, timeout_s=1.0)
+        time.sleep(3.0)  # present, but never calls the collective
+        c.destroy()
+
+    t = threading.Thread(target=absent)
+    c0 = Comm(uid, 2, 0, timeout_s=1.0)
+    t.start()
+    x = inputs(np.float32, n, 0, seed=5)
+    with pytest.raises(Timeout):
+        c0.allreduce_host(Op.SUM, x.copy(), np.zeros(n, np.float32), chunk=chunk)
+    c0.destroy()
+    t.join(timeout=30)
+    for N in (2, 1):
+        xs = [inputs(np.float32, n, r, seed=70 + N) for r in range(N)]
+        t0 = time.monotonic()
+        res = run_ranks(N, lambda c, r: _host_allreduce(c, r, xs[r], Op.SUM, False, r == 0, chunk))
+        assert time.monotonic() - t0 < 30
+        want, _ = orc.allreduce(xs, orc.OPS["sum"])
+        for r in range(N):
+            assert_bit_equal(res[r][0], want[r], f"after the aborted communicator: N={N} rank {r}")
 
 
 def test_comm_allreduce_host_default_chunk_matches_device(device):

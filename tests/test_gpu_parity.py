@@ -1037,6 +1037,44 @@ def test_dev_alloc_places_buckets_in_rotating_slots(device):
         fmi_amd.tune_set(Tune.ALLOC_SLOTS, 2)
 
 
+def test_dev_alloc_group_places_each_bucket_by_its_index(device):
+    """fmi_dev_alloc_group: bucket j of a group of >= 1 MiB buckets sits in 4 KiB slot j mod 16 modulo
+    64 KiB whatever was allocated before (here after 5 and 11 unrelated slotted allocations, and with
+    FMI_TUNE_ALLOC_SLOTS = 0), usable to its last byte, freed through fmi_dev_free; a fused kernel over a group
+    gives the same bits as over plain buckets; small groups are plain 4 KiB-aligned allocations; an impossible group
+    fails whole (FmiError, no bucket handed out); count 0 is a no-op."""
+    n = (1 << 20) // 4 + 7
+    old = fmi_amd.tune_get(Tune.ALLOC_SLOTS)
+    try:
+        for before, slots_on in ((5, 1), (11, 1), (3, 0)):
+            fmi_amd.tune_set(Tune.ALLOC_SLOTS, slots_on)
+            others = [Bucket(n, np.float32) for _ in range(before)]
+            g = Bucket.group(18, n, np.float32)
+            assert [(b.ptr % 65536) // 4096 for b in g] == [j % 16 for j in range(18)], [hex(b.ptr) for b in g]
+            for k, b in enumerate(g):
+                b.fill_synthetic(3, k)
+            for k, b in enumerate(g):
+                tail = b.view(n - 5, 5).numpy()
+                assert np.array_equal(tail.view(np.uint32), orc.synthetic(np.float32, n, 3, k)[-5:].view(np.uint32))
+            fmi_amd.reduce_tree(Op.SUM, Alg.ALLREDUCE, g[8], g[:8])
+            fmi_amd.tune_set(Tune.ALLOC_SLOTS, 0)
+            plain = [Bucket.from_numpy(b.numpy()) for b in g[:8]]
+            out = Bucket(n, np.float32)
+            fmi_amd.reduce_tree(Op.SUM, Alg.ALLREDUCE, out, plain)
+            assert out.numpy().tobytes() == g[8].numpy().tobytes()
+            for b in others + g + plain + [out]:
+                b.free()
+    finally:
+        fmi_amd.tune_set(Tune.ALLOC_SLOTS, old)
+    small = Bucket.group(4, 1000, np.float32)
+    assert all(b.ptr % 4096 == 0 for b in small)
+    for b in small:
+        b.free()
+    assert Bucket.group(0, n, np.float32) == []
+    with pytest.raises(fmi_amd.FmiError, match="group bucket"):
+        Bucket.group(3, 1 << 46, np.uint8)  # 64 TiB each: the first hipMalloc already fails
+
+
 @pytest.mark.parametrize("chunk", [(1 << 16), (3 << 20) + 4096, (64 << 20)])
 def test_host_reduce_pair_staging_sizes(device, chunk):
     """The pooled staging sets grow to the largest chunk they served (a power of two from 64 KiB, capped at the

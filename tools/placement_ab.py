@@ -1,0 +1,184 @@
+"""Bucket placement A/B on the bench's own allocation orders (round 6).
+
+Each block allocates its buckets EXACTLY as bench.py does (or through the group allocator), fills them, waits a quiet
+second (the driver clears freed VRAM in the background), launches `warmup` untimed and `steps` timed kernels
+(bench.py's 5 / 20 by default), and frees. Modes, interleaved `--reps` times in one process:
+
+  pair  (C2, bench.py run_single: 16 sets, per set a then b, 256 MiB f32 each)
+        plain     FMI_TUNE_ALLOC_SLOTS = 0: every bucket a plain hipMalloc (2 MiB aligned: a, b at the same offset)
+        rotating  FMI_TUNE_ALLOC_SLOTS = 1: round 5's rotating 4 KiB slots (a in slot g, b in slot g + 1)
+        group     Bucket.group(2): a in slot 0, b in slot 1 of their own hipMallocs (fmi_dev_alloc_group)
+        same_slot both operands in slot k = 1 + s % 15 (same relative offset as plain, not 2 MiB aligned)
+  scan  (C3 scan, bench.py c3_single: 8 sets of 8 inputs ALL allocated first, then all 8 x 8 outputs, 64 MiB f32)
+        plain / rotating as above; group: Bucket.group(16) per set (inputs slots 0-7, outputs 8-15)
+  tree  (bench.py c4_single: 8 inputs then the output, 1 GiB f32 each, one set)
+        plain / rotating; group: Bucket.group(9)
+
+One JSON line per block: kernel, mode, rep, mean launch time from two HIP events around the timed launches on the
+library stream, fraction of 8 TB/s, and a bit-exact check of one window per set. Under
+`rocprofv3 --kernel-trace` the blocks' launches are attributed by tools/placement_ab_trace.py (the lines give each
+block's launch counts in order).
+
+  python tools/placement_ab.py [--kernels pair,scan,tree] [--reps 3] [--modes ...]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import numpy as np  # noqa: E402
+
+import fmi_amd  # noqa: E402
+from bench import eval_bracketing  # noqa: E402
+from fmi_amd import Alg, Bucket, Event, Op, Tune  # noqa: E402
+
+MIB = 1 << 20
+PEAK = 8e12
+SLOT = 4096
+
+
+def alloc(mode, count, n, dtype=np.float32, slot=None):
+    """`count` buckets of n elements, one allocation each, placed per `mode` (owners to free, views to use)."""
+    if mode == "group":
+        bs = Bucket.group(count, n, dtype)
+        return bs, bs
+    if mode == "same_slot":
+        fmi_amd.tune_set(Tune.ALLOC_SLOTS, 0)
+        item = np.dtype(dtype).itemsize
+        owners = [Bucket(n + 16 * SLOT // item, dtype) for _ in range(count)]
+        return [o.view(slot * SLOT // item, n) for o in owners], owners
+    fmi_amd.tune_set(Tune.ALLOC_SLOTS, 1 if mode == "rotating" else 0)
+    bs = [Bucket(n, dtype) for _ in range(count)]
+    return bs, bs
+
+
+def timed(launch, warmup, steps):
+    fmi_amd.sync()
+    time.sleep(1.0)
+    for k in range(warmup):
+        launch(k)
+    e0, e1 = Event(), Event()
+    e0.record()
+    for k in range(warmup, warmup + steps):
+        launch(k)
+    e1.record()
+    e1.sync()
+    us = e0.elapsed_ms(e1) * 1e3 / steps
+    e0.destroy()
+    e1.destroy()
+    return us
+
+
+def pair(mode, warmup, steps):
+    n, S = 256 * MIB // 4, 16
+    sets, owners = [], []
+    for s in range(S):  # bench.py run_single: a then b, set after set
+        (a, b), own = alloc(mode, 2, n, slot=1 + s % 15)
+        a.fill_synthetic(42 + s, 0)
+        b.fill_synthetic(42 + s, 1)
+        sets.append((a, b))
+        owners += own
+    slots = sorted({(x.ptr % (64 * 1024)) // SLOT for st in sets for x in st})
+    used = [0] * S
+
+    def launch(k):
+        used[k % S] += 1
+        fmi_amd.reduce_pair(Op.SUM, *sets[k % S])
+
+    us = timed(launch, warmup, steps)
+    bad = 0
+    for s, (a, b) in enumerate(sets):
+        x = Bucket(1 << 16, np.float32).fill_synthetic(42 + s, 0).numpy()
+        y = b.view(0, 1 << 16).numpy()
+        for _ in range(used[s]):
+            x = x + y
+        bad += int(np.count_nonzero(a.view(0, 1 << 16).numpy().view(np.uint32) != x.view(np.uint32)))
+    for o in owners:
+        o.free()
+    return {"us": round(us, 2), "frac": round(3 * n * 4 / (us * 1e-6) / PEAK, 4), "mismatches": bad,
+            "slots_mod_64k": slots}
+
+
+def scan(mode, warmup, steps):
+    n, P, S = 64 * MIB // 4, 8, 8
+    owners = []
+    if mode == "group":
+        groups = [Bucket.group(2 * P, n, np.float32) for _ in range(S)]
+        ins = [g[:P] for g in groups]
+        outs = [g[P:] for g in groups]
+        owners = [b for g in groups for b in g]
+    else:  # bench.py c3_single: every set's inputs first, then every set's outputs
+        fmi_amd.tune_set(Tune.ALLOC_SLOTS, 1 if mode == "rotating" else 0)
+        ins = [[Bucket(n, np.float32) for _ in range(P)] for _ in range(S)]
+        outs = [[Bucket(n, np.float32) for _ in range(P)] for _ in range(S)]
+        owners = [b for s in ins + outs for b in s]
+    for s in range(S):
+        for p in range(P):
+            ins[s][p].fill_synthetic(7 + s, p)
+    distinct = [len({(b.ptr % (64 * 1024)) // SLOT for b in ins[s] + outs[s]}) for s in range(S)]
+    us = timed(lambda k: fmi_amd.scan_peers(Op.SUM, Alg.SCAN, outs[k % S], ins[k % S]), warmup, steps)
+    bad = 0
+    for s in range(S):
+        xs = [b.view(0, 1 << 14).numpy() for b in ins[s]]
+        for r in range(P):
+            want = eval_bracketing(fmi_amd.schedule_expr(Alg.SCAN, P, r), xs)
+            bad += int(np.count_nonzero(outs[s][r].view(0, 1 << 14).numpy().view(np.uint32) != want.view(np.uint32)))
+    for o in owners:
+        o.free()
+    return {"us": round(us, 2), "frac": round(2 * P * n * 4 / (us * 1e-6) / PEAK, 4), "mismatches": bad,
+            "distinct_slots_per_set": distinct}
+
+
+def tree(mode, warmup, steps):
+    n, P = 1024 * MIB // 4, 8
+    if mode == "group":
+        bs = Bucket.group(P + 1, n, np.float32)
+    else:  # bench.py c4_single: the 8 inputs, then the output
+        fmi_amd.tune_set(Tune.ALLOC_SLOTS, 1 if mode == "rotating" else 0)
+        bs = [Bucket(n, np.float32) for _ in range(P + 1)]
+    for p in range(P):
+        bs[p].fill_synthetic(11, p)
+    distinct = len({(b.ptr % (64 * 1024)) // SLOT for b in bs})
+    us = timed(lambda k: fmi_amd.reduce_tree(Op.SUM, Alg.ALLREDUCE, bs[P], bs[:P]), warmup, steps)
+    want = eval_bracketing(fmi_amd.schedule_expr(Alg.ALLREDUCE, P, 0), [b.view(0, 1 << 14).numpy() for b in bs[:P]])
+    bad = int(np.count_nonzero(bs[P].view(0, 1 << 14).numpy().view(np.uint32) != want.view(np.uint32)))
+    for b in bs:
+        b.free()
+    return {"us": round(us, 2), "frac": round((P + 1) * n * 4 / (us * 1e-6) / PEAK, 4), "mismatches": bad,
+            "distinct_slots": distinct}
+
+
+KERNELS = {"pair": (pair, "plain,rotating,group,same_slot", "pair_tile<fmi::dev::OpSum, float, 4, 3>"),
+           "scan": (scan, "plain,rotating,group", "scan_kernel<fmi::dev::OpSum, float, 3, 8>"),
+           "tree": (tree, "plain,rotating,group", "tree_kernel<fmi::dev::OpSum, float, 0, 8, false>")}
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--kernels", default="pair,scan,tree")
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--modes", default="", help="comma list overriding every kernel's default modes")
+    a = ap.parse_args()
+    fmi_amd.init(0)
+    default_slots = fmi_amd.tune_get(Tune.ALLOC_SLOTS)
+    bad = 0
+    for rep in range(a.reps):
+        for k in a.kernels.split(","):
+            fn, modes, trace_name = KERNELS[k]
+            for mode in (a.modes or modes).split(","):
+                r = fn(mode, a.warmup, a.steps)
+                fmi_amd.tune_set(Tune.ALLOC_SLOTS, default_slots)
+                bad += r["mismatches"]
+                print(json.dumps(dict(kernel=k, mode=mode, rep=rep, warmup=a.warmup, steps=a.steps,
+                                      trace_name=trace_name, **r)), flush=True)
+    if bad:
+        raise SystemExit(f"{bad} mismatching elements")
+
+
+if __name__ == "__main__":
+    main()
