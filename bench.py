@@ -712,6 +712,22 @@ C3_PAIR_SETS = 64  # 63 x 8 MiB of sc1 tile writes between two uses of a set (se
 C3_SCAN_SETS = 8
 
 
+GROUP_PLACEMENT = ("fmi_dev_alloc_group: the launch's buckets as one group, bucket j in 4 KiB slot j mod 16 "
+                   "(mod 64 KiB) of its own hipMalloc")
+
+
+def scan_sets(sets: int, peers: int, n: int):
+    """The C3 scan's buckets: each set's `peers` inputs and `peers` outputs allocated as ONE group
+    (fmi_dev_alloc_group), so the 16 streams of one launch sit in 16 distinct 4 KiB slots whatever was allocated
+    before (tests/test_bench_contract.py checks the order, tests/test_gpu_parity.py the slots)."""
+    import numpy as np
+
+    from fmi_amd import Bucket
+
+    groups = [Bucket.group(2 * peers, n, np.float32) for _ in range(sets)]
+    return [g[:peers] for g in groups], [g[peers:] for g in groups]
+
+
 def c3_single(reps: int = 60) -> dict:
     """Config C3 on this GPU, in the driver's run: the int64 max pairwise combine of 64 MiB buckets (64
     rotating sets, 8 GiB: no set is re-read from the 256 MiB MALL) and the f32 peer-axis scan (scan_no_order)
@@ -762,8 +778,10 @@ def c3_single(reps: int = 60) -> dict:
         b.free()
     P, n32 = 8, 64 * MIB // 4
     S = C3_SCAN_SETS
-    ins = [[Bucket(n32, np.float32).fill_synthetic(7 + s, p) for p in range(P)] for s in range(S)]
-    outs = [[Bucket(n32, np.float32) for _ in range(P)] for _ in range(S)]
+    ins, outs = scan_sets(S, P, n32)
+    for s in range(S):
+        for p in range(P):
+            ins[s][p].fill_synthetic(7 + s, p)
     quiet_device()  # the 8 GiB of i64 pairs were just freed
     ms_scan = timed(lambda i: fmi_amd.scan_peers(Op.SUM, Alg.SCAN, outs[i % S], ins[i % S]), 3 * S)
     per_set = [(Event(), Event()) for _ in range(S)]  # diagnostic, untimed: one launch per set, its own events
@@ -791,6 +809,7 @@ def c3_single(reps: int = 60) -> dict:
                                        rotating_sets=C3_PAIR_SETS, self_check=max_check),
             "f32_scan_P8_64MiB": dict(row(ms_scan, 2 * P * 64 * MIB, "scan_kernel<fmi::dev::OpSum, float, 3, 8>"),
                                       rotating_sets=C3_SCAN_SETS, per_set_launch_us=per_set_us,
+                                      placement=GROUP_PLACEMENT,
                                       self_check=scan_check),
             "timing": "two HIP events around back-to-back launches on the library stream (gaps included)"}
 
@@ -808,8 +827,10 @@ def c4_single(peers: int = 8, mib: int = 1024, launches: int = 10) -> dict:
     from fmi_amd import Alg, Bucket, Event, Op
 
     n = mib * MIB // 4
-    ins = [Bucket(n, np.float32).fill_synthetic(11, p) for p in range(peers)]
-    out = Bucket(n, np.float32)
+    group = Bucket.group(peers + 1, n, np.float32)  # the launch's 8 inputs and output in distinct slots
+    ins, out = group[:peers], group[peers]
+    for p, b in enumerate(ins):
+        b.fill_synthetic(11, p)
     # The driver clears the VRAM C3 just freed (9 GiB) in the background, on the same HBM: measured right after
     # C3 this launch ran at 0.68 of peak, after a quiet second at 0.76-0.78 (profiles/r04_tree8_sizes.jsonl).
     quiet_device()
@@ -839,7 +860,7 @@ def c4_single(peers: int = 8, mib: int = 1024, launches: int = 10) -> dict:
             "kernel_avg_us": round(ms * 1e3, 2), "algorithmic_bytes": algo,
             "GB_s": round(algo / (ms * 1e-3) / 1e9, 1), "frac": round(algo / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "GiB_s_reduced_buckets": round(peers * n * 4 / GIB / (ms * 1e-3), 2),
-            "traffic": traffic, "traffic_source": src, "launches": launches,
+            "traffic": traffic, "traffic_source": src, "launches": launches, "placement": GROUP_PLACEMENT,
             "timing": "two HIP events around back-to-back launches on the library stream (gaps included)",
             "self_check": {"ok": bad == 0, "mismatches": bad, "elements_checked": checked,
                            "against": "numpy float32 evaluation of rank 0's allreduce_no_order bracketing "

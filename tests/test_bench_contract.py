@@ -391,3 +391,53 @@ def test_line_names_the_bucket_placement():
             fmi_amd.tune_set(fmi_amd.Tune.ALLOC_SLOTS, 3)
     finally:
         fmi_amd.tune_set(fmi_amd.Tune.ALLOC_SLOTS, old)
+
+
+def _emulated_allocator(monkeypatch, rotating):
+    """The C-ABI's documented placement rules (include/fmi_dev.h) on fake 2 MiB-aligned bases, no device:
+    fmi_dev_alloc puts buckets of >= 1 MiB in slot g++ mod 16 (rotating) or at the base (plain);
+    fmi_dev_alloc_group puts bucket j in slot j mod 16."""
+    from fmi_amd import _lib
+
+    state = {"base": 1 << 40, "g": 0}
+
+    def base():
+        state["base"] += 1 << 30
+        return state["base"]
+
+    def call(name, *args):
+        if name == "fmi_dev_alloc":
+            slot = (state["g"] % 16) if rotating and args[1] >= 1 << 20 else 0
+            state["g"] += 1 if rotating and args[1] >= 1 << 20 else 0
+            args[0]._obj.value = base() + slot * 4096
+        elif name == "fmi_dev_alloc_group":
+            for j in range(args[1]):
+                args[0][j] = base() + (j % 16) * 4096 * (args[2] >= 1 << 20)
+        else:
+            raise AssertionError(f"unexpected call {name}")
+
+    monkeypatch.setattr(_lib, "call", call)
+
+
+@pytest.mark.parametrize("rotating", [0, 1])
+def test_c3_scan_sets_give_every_launch_16_distinct_slots(monkeypatch, rotating):
+    """whatever was allocated before and whatever FMI_TUNE_ALLOC_SLOTS says, every C3 scan set's
+    8 inputs and 8 outputs sit in 16 distinct 4 KiB slots mod 64 KiB (bench.scan_sets allocates each set as one
+    group). The order bench.py used in round 5 — every set's inputs, then every set's outputs, one fmi_dev_alloc each
+    — gives set s's input p and output p the same slot, the collision the group removes."""
+    import numpy as np
+
+    from fmi_amd import Bucket
+
+    _emulated_allocator(monkeypatch, rotating)
+    P, S, n = 8, 8, 64 * (1 << 20) // 4
+    [Bucket(n, np.float32) for _ in range(5)]  # unrelated allocations before
+    ins, outs = bench.scan_sets(S, P, n)
+    for s in range(S):
+        assert len({(b.ptr % 65536) // 4096 for b in ins[s] + outs[s]}) == 16, s
+    old_ins = [[Bucket(n, np.float32) for _ in range(P)] for _ in range(S)]
+    old_outs = [[Bucket(n, np.float32) for _ in range(P)] for _ in range(S)]
+    for s in range(S):
+        assert len({(b.ptr % 65536) // 4096 for b in old_ins[s] + old_outs[s]}) == (8 if rotating else 1)
+    for b in [b for g in ins + outs + old_ins + old_outs for b in g]:
+        b._owns = False

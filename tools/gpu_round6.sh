@@ -3,7 +3,9 @@
 #                                C++); then the placement A/B on bench.py's own allocation orders (pair / scan / tree x
 #                                plain / rotating / group, pair also same_slot), interleaved 3x in one process under a
 #                                rocprofv3 kernel trace (tools/placement_ab.py, tools/placement_ab_trace.py)
-#   bash tools/gpu_round6.sh b   the same A/B on another box (TAG=r06b)
+#                                then the N > 1 shard kernel on its receive layout, packed vs 4 KiB-skewed shards
+#                                (tools/shard_layout_ab.py)
+#   bash tools/gpu_round6.sh b   the placement A/B on another box (TAG=r06b)
 set -o pipefail
 cd /root/repo
 mkdir -p gpurun_out
@@ -17,7 +19,12 @@ a)
         > gpurun_out/${TAG}_tests.log 2>&1 &&
     timeout -k 10 300 python -u -m pytest -x -v --timeout 240 --timeout-method thread -p no:cacheprovider \
         tests/test_cpp_communicator.py -m gpu >> gpurun_out/${TAG}_tests.log 2>&1 &&
-    bash tools/gpu_round6.sh ab
+    bash tools/gpu_round6.sh ab &&
+    bash tools/gpu_round6.sh shard
+    ;;
+shard)
+    timeout -k 10 300 python -u tools/shard_layout_ab.py --reps 3 > gpurun_out/${TAG}_shard_layout.jsonl \
+        2> gpurun_out/${TAG}_shard_layout.err
     ;;
 b)
     bash tools/gpu_round6.sh ab
