@@ -5,7 +5,8 @@
 #                                rocprofv3 kernel trace (tools/placement_ab.py, tools/placement_ab_trace.py)
 #                                then the N > 1 shard kernel on its receive layout, packed vs 4 KiB-skewed shards
 #                                (tools/shard_layout_ab.py)
-#   bash tools/gpu_round6.sh b   the placement A/B on another box (TAG=r06b)
+#   bash tools/gpu_round6.sh b   placement, round two (TAG=r06b): the allocator's placements beside explicit slot lists,
+#                                mode order rotated per rep, under a kernel trace
 set -o pipefail
 cd /root/repo
 mkdir -p gpurun_out
@@ -27,7 +28,18 @@ shard)
         2> gpurun_out/${TAG}_shard_layout.err
     ;;
 b)
-    bash tools/gpu_round6.sh ab
+    # placement, round two: the allocator's own placements beside explicit slot lists made by identical allocation
+    # calls (s:...), the mode order rotated by one per rep (so no mode always follows the same one), under a trace
+    cd /tmp
+    timeout -k 10 900 rocprofv3 --kernel-trace --output-format csv -d $R/gpurun_out/${TAG}_placement_trace -o run -- \
+        python3 $R/tools/placement_ab.py --reps 3 --rotate-order \
+        --modes-pair plain,rotating,group,s:0.5,s:5.0,s:5.6,s:0.0 \
+        --modes-scan plain,rotating,group,s:0.1.2.3.4.5.6.7.8.9.10.11.12.13.14.15,s:0.1.2.3.4.5.6.7.0.1.2.3.4.5.6.7,s:0.2.4.6.8.10.12.14.1.3.5.7.9.11.13.15 \
+        --modes-tree plain,rotating,group,s:0.1.2.3.4.5.6.7.8,s:1.2.3.4.5.6.7.8.0,s:8.9.10.11.12.13.14.15.0 \
+        > $R/gpurun_out/${TAG}_placement_ab.jsonl 2> $R/gpurun_out/${TAG}_placement_ab.err &&
+    cd $R &&
+    python3 tools/placement_ab_trace.py gpurun_out/${TAG}_placement_ab.jsonl gpurun_out/${TAG}_placement_trace \
+        > gpurun_out/${TAG}_placement_ab_trace.jsonl
     ;;
 ab)
     cd /tmp

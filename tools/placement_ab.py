@@ -9,6 +9,8 @@ second (the driver clears freed VRAM in the background), launches `warmup` untim
         rotating  FMI_TUNE_ALLOC_SLOTS = 1: round 5's rotating 4 KiB slots (a in slot g, b in slot g + 1)
         group     Bucket.group(2): a in slot 0, b in slot 1 of their own hipMallocs (fmi_dev_alloc_group)
         same_slot both operands in slot k = 1 + s % 15 (same relative offset as plain, not 2 MiB aligned)
+  any kernel: s:i.j.k...  bucket j (allocation order: pair a, b; scan 8 inputs then 8 outputs; tree 8 inputs then
+            the output) at 4 KiB slot list[j] of a plain hipMalloc 64 KiB larger, every set alike
   scan  (C3 scan, bench.py c3_single: 8 sets of 8 inputs ALL allocated first, then all 8 x 8 outputs, 64 MiB f32)
         plain / rotating as above; group: Bucket.group(16) per set (inputs slots 0-7, outputs 8-15)
   tree  (bench.py c4_single: 8 inputs then the output, 1 GiB f32 each, one set)
@@ -40,8 +42,24 @@ PEAK = 8e12
 SLOT = 4096
 
 
+def at_slots(slots, n, dtype=np.float32):
+    """One plain hipMalloc 64 KiB larger per bucket (as the slotted allocator makes), bucket j viewed at 4 KiB slot
+    slots[j]: any placement, from the same allocation calls (owners to free, views to use)."""
+    fmi_amd.tune_set(Tune.ALLOC_SLOTS, 0)
+    item = np.dtype(dtype).itemsize
+    owners = [Bucket(n + 16 * SLOT // item, dtype) for _ in slots]
+    return [o.view(k * SLOT // item, n) for o, k in zip(owners, slots)], owners
+
+
+def slot_mode(mode):
+    """'s:0,1,...' -> the slot list, else None"""
+    return [int(x) for x in mode[2:].split(".")] if mode.startswith("s:") else None
+
+
 def alloc(mode, count, n, dtype=np.float32, slot=None):
     """`count` buckets of n elements, one allocation each, placed per `mode` (owners to free, views to use)."""
+    if slot_mode(mode):
+        return at_slots(slot_mode(mode), n, dtype)
     if mode == "group":
         bs = Bucket.group(count, n, dtype)
         return bs, bs
@@ -105,11 +123,14 @@ def pair(mode, warmup, steps):
 def scan(mode, warmup, steps):
     n, P, S = 64 * MIB // 4, 8, 8
     owners = []
-    if mode == "group":
-        groups = [Bucket.group(2 * P, n, np.float32) for _ in range(S)]
+    if mode == "group" or slot_mode(mode):
+        groups, owners = [], []
+        for _ in range(S):
+            g, own = (Bucket.group(2 * P, n, np.float32), None) if mode == "group" else at_slots(slot_mode(mode), n)
+            groups.append(g)
+            owners += own or g
         ins = [g[:P] for g in groups]
         outs = [g[P:] for g in groups]
-        owners = [b for g in groups for b in g]
     else:  # bench.py c3_single: every set's inputs first, then every set's outputs
         fmi_amd.tune_set(Tune.ALLOC_SLOTS, 1 if mode == "rotating" else 0)
         ins = [[Bucket(n, np.float32) for _ in range(P)] for _ in range(S)]
@@ -134,8 +155,11 @@ def scan(mode, warmup, steps):
 
 def tree(mode, warmup, steps):
     n, P = 1024 * MIB // 4, 8
+    owners = None
     if mode == "group":
         bs = Bucket.group(P + 1, n, np.float32)
+    elif slot_mode(mode):
+        bs, owners = at_slots(slot_mode(mode), n)
     else:  # bench.py c4_single: the 8 inputs, then the output
         fmi_amd.tune_set(Tune.ALLOC_SLOTS, 1 if mode == "rotating" else 0)
         bs = [Bucket(n, np.float32) for _ in range(P + 1)]
@@ -145,10 +169,11 @@ def tree(mode, warmup, steps):
     us = timed(lambda k: fmi_amd.reduce_tree(Op.SUM, Alg.ALLREDUCE, bs[P], bs[:P]), warmup, steps)
     want = eval_bracketing(fmi_amd.schedule_expr(Alg.ALLREDUCE, P, 0), [b.view(0, 1 << 14).numpy() for b in bs[:P]])
     bad = int(np.count_nonzero(bs[P].view(0, 1 << 14).numpy().view(np.uint32) != want.view(np.uint32)))
-    for b in bs:
+    slots = [(b.ptr % (64 * 1024)) // SLOT for b in bs]
+    for b in owners or bs:
         b.free()
     return {"us": round(us, 2), "frac": round((P + 1) * n * 4 / (us * 1e-6) / PEAK, 4), "mismatches": bad,
-            "distinct_slots": distinct}
+            "distinct_slots": distinct, "slots": slots}
 
 
 KERNELS = {"pair": (pair, "plain,rotating,group,same_slot", "pair_tile<fmi::dev::OpSum, float, 4, 3>"),
@@ -163,6 +188,9 @@ def main() -> None:
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--modes", default="", help="comma list overriding every kernel's default modes")
+    for k in KERNELS:
+        ap.add_argument(f"--modes-{k}", default="", help=f"{k}'s modes; 's:0.1.2' = bucket j at 4 KiB slot j-th entry")
+    ap.add_argument("--rotate-order", action="store_true", help="rotate the mode order by one per rep")
     a = ap.parse_args()
     fmi_amd.init(0)
     default_slots = fmi_amd.tune_get(Tune.ALLOC_SLOTS)
@@ -170,7 +198,10 @@ def main() -> None:
     for rep in range(a.reps):
         for k in a.kernels.split(","):
             fn, modes, trace_name = KERNELS[k]
-            for mode in (a.modes or modes).split(","):
+            ms = (getattr(a, f"modes_{k}") or a.modes or modes).split(",")
+            if a.rotate_order:  # rep r starts at mode r: every mode runs after a different one in each rep
+                ms = ms[rep % len(ms):] + ms[:rep % len(ms)]
+            for mode in ms:
                 r = fn(mode, a.warmup, a.steps)
                 fmi_amd.tune_set(Tune.ALLOC_SLOTS, default_slots)
                 bad += r["mismatches"]
