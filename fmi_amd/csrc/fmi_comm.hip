@@ -253,6 +253,14 @@ public:
     }
     // recv[j*bytes ...] = rank j's send[rank*bytes ...]
     virtual int all_to_all(const char* send, char* recv, size_t bytes, hipStream_t s) = 0;
+    // all_to_all with rank j's block landing at recv + j * stride (stride >= bytes; the gaps untouched), for the
+    // shard kernel's inputs (shard_stride). Only transports whose all-to-all posts one receive per peer anyway take a
+    // stride other than bytes: for them the stride changes where the bytes land, never which operations run.
+    virtual bool receives_per_peer() const { return false; }
+    virtual int all_to_all_strided(const char* send, char* recv, size_t bytes, size_t stride, hipStream_t s) {
+        if (stride == bytes) return all_to_all(send, recv, bytes, s);
+        return fail(FMI_ERR_UNSUPPORTED, "transport has no strided all-to-all");
+    }
     // recv[j*bytes ...] = rank j's send[0 .. bytes)
     virtual int all_gather(const char* send, char* recv, size_t bytes, hipStream_t s) = 0;
     virtual int gather(const char* send, char* recv, size_t bytes, int root, hipStream_t s) = 0;
@@ -416,6 +424,14 @@ public:
             return FMI_OK;
         }
         return run_plan(plan::all_to_all(n_, rank_, bytes), send, recv, s);
+    }
+    // ncclAllToAll receives one contiguous buffer: only the grouped form (FMI_TUNE_COMM_A2A = 1, or a librccl
+    // without ncclAllToAll) takes a stride, with the same sends and receives as without one
+    bool receives_per_peer() const override { return !(api_->AllToAll && tune(FMI_TUNE_COMM_A2A) == 0); }
+    int all_to_all_strided(const char* send, char* recv, size_t bytes, size_t stride, hipStream_t s) override {
+        if (stride == bytes) return all_to_all(send, recv, bytes, s);
+        if (!receives_per_peer()) return fail(FMI_ERR_UNSUPPORTED, "ncclAllToAll takes no receive stride");
+        return run_plan(plan::all_to_all(n_, rank_, bytes, stride), send, recv, s);
     }
     int all_gather(const char* send, char* recv, size_t bytes, hipStream_t s) override {
         if (tune(FMI_TUNE_COMM_GATHER) == 0) {
@@ -671,6 +687,10 @@ public:
     int all_to_all(const char* send, char* recv, size_t bytes, hipStream_t s) override {
         return run_plan([&](int r) { return plan::all_to_all(n_, r, bytes); }, send, recv, s);
     }
+    bool receives_per_peer() const override { return true; }
+    int all_to_all_strided(const char* send, char* recv, size_t bytes, size_t stride, hipStream_t s) override {
+        return run_plan([&](int r) { return plan::all_to_all(n_, r, bytes, stride); }, send, recv, s);
+    }
     int all_gather(const char* send, char* recv, size_t bytes, hipStream_t s) override {
         return run_plan([&](int r) { return plan::all_gather(n_, r, bytes); }, send, recv, s);
     }
@@ -917,6 +937,10 @@ public:
     }
 
     int all_to_all(const char* send, char* recv, size_t bytes, hipStream_t s) override {
+        return all_to_all_strided(send, recv, bytes, bytes, s);
+    }
+    bool receives_per_peer() const override { return true; }
+    int all_to_all_strided(const char* send, char* recv, size_t bytes, size_t stride, hipStream_t s) override {
         const size_t c = std::max<size_t>(1, kProcSlot / static_cast<size_t>(n_));
         return pieces(bytes, c, s,
                       [&](size_t o, size_t len) -> int {
@@ -926,7 +950,7 @@ public:
                       },
                       [&](size_t o, size_t len) -> int {
                           for (int j = 0; j < n_; ++j)
-                              FMI_COMM_HIP(hipMemcpyAsync(recv + j * bytes + o, slot(j) + rank_ * c, len, hipMemcpyHostToDevice, s));
+                              FMI_COMM_HIP(hipMemcpyAsync(recv + j * stride + o, slot(j) + rank_ * c, len, hipMemcpyHostToDevice, s));
                           return FMI_OK;
                       });
     }
@@ -1402,6 +1426,19 @@ size_t shard_elems(size_t n, int ranks) {
     return (per + kShardAlign - 1) / kShardAlign * kShardAlign;
 }
 
+// Where the all-to-all lands the N shards the fused shard kernel then streams together. Back to
+// back at `bytes` (a multiple of 64 KiB for the headline's buckets), all N streams sit at one offset modulo HBM's
+// 64 KiB interleave and collide, as DESIGN §4 measured for buckets; at a stride of bytes rounded up to 64 KiB plus
+// 4 KiB, shard j sits in 4 KiB slot j mod 16 and the reduced shard (shard_out) in slot N mod 16. The fused 8-way kernel
+// at the N = 8 shard shape (32 MiB): 0.738 packed, 0.790 skewed; N = 4: 0.741 / 0.764; N = 2: 0.784 / 0.806
+// (profiles/r06a_shard_layout.jsonl, tools/shard_layout_ab.py). Taken where the transport posts a receive per peer
+// anyway (receives_per_peer) and FMI_TUNE_COMM_SHARD_SKEW is on; shards under 1 MiB stay back to back.
+constexpr size_t kShardSlot = 4096, kShardSpan = 16 * kShardSlot;
+size_t shard_stride(const Transport& t, size_t bytes) {
+    if (!tune(FMI_TUNE_COMM_SHARD_SKEW) || bytes < (size_t(1) << 20) || !t.receives_per_peer()) return bytes;
+    return (bytes + kShardSpan - 1) / kShardSpan * kShardSpan + kShardSlot;
+}
+
 int aborted_error() {
     return fail(FMI_ERR_COMM, "communicator was aborted (a timeout or a transport error); destroy it");
 }
@@ -1626,14 +1663,18 @@ int allreduce_device(Comm* c, int op, int dtype, int alg, int path, const void* 
     }
     const char* src = nullptr;
     FMI_COMM_RC(padded_source(c, n, padded, esz, send, s, &src));
+    // the shard kernel's inputs each in their own 4 KiB slot, and its output in the next (shard_stride)
+    const size_t stride = path != FMI_PATH_RCCL && !per_rank ? shard_stride(*c->t, shard * esz) : shard * esz;
+    const size_t red_at = stride != shard * esz ? (static_cast<size_t>(N) % 16) * kShardSlot : 0;
     char* red = nullptr;
-    FMI_COMM_RC(c->scratch(2, (per_rank ? padded : shard) * esz, s, &red));
+    FMI_COMM_RC(c->scratch(2, (per_rank ? padded : shard) * esz + (red_at ? kShardSpan : 0), s, &red));
+    red += red_at;
     if (path != FMI_PATH_RCCL) {
         char* staging = nullptr;
-        FMI_COMM_RC(c->scratch(1, padded * esz, s, &staging));
-        FMI_COMM_RC(c->t->all_to_all(src, staging, shard * esz, s));
+        FMI_COMM_RC(c->scratch(1, static_cast<size_t>(N) * stride, s, &staging));
+        FMI_COMM_RC(c->t->all_to_all_strided(src, staging, shard * esz, stride, s));
         std::vector<const void*> parts(N);
-        for (int j = 0; j < N; ++j) parts[j] = staging + j * shard * esz;
+        for (int j = 0; j < N; ++j) parts[j] = staging + j * stride;
         if (per_rank) {
             FMI_COMM_RC(c->timing.begin(s));
             if (N >= 2 && N <= sched::kMaxFusedPeers) {

@@ -42,13 +42,15 @@ inline void add(std::vector<Xfer>& v, int peer, size_t off, size_t len) {
 }
 }  // namespace detail
 
-// recv[j * bytes ...] = rank j's send[rank * bytes ...]; the own part travels as a send / receive to self.
-inline Plan all_to_all(int n, int rank, size_t bytes) {
+// recv[j * stride ...] = rank j's send[rank * bytes ...] (stride 0: bytes, the blocks back to back); the own part
+// travels as a send / receive to self. The stride changes only where this rank's receives land, never the pairing.
+inline Plan all_to_all(int n, int rank, size_t bytes, size_t recv_stride = 0) {
     (void)rank;
+    const size_t stride = recv_stride ? recv_stride : bytes;
     Plan p;
     for (int j = 0; j < n; ++j) {
         detail::add(p.sends, j, j * bytes, bytes);
-        detail::add(p.recvs, j, j * bytes, bytes);
+        detail::add(p.recvs, j, j * stride, bytes);
     }
     return p;
 }

@@ -64,6 +64,7 @@ class Tune(enum.IntEnum):
     PAIR_SC1_OF_8 = 12
     COMM_ONE_RANK_EXCHANGE = 13
     ALLOC_SLOTS = 14
+    COMM_SHARD_SKEW = 15
 
 
 NP_DTYPE = {DType.F32: np.float32, DType.F64: np.float64, DType.I32: np.int32, DType.I64: np.int64,

@@ -404,7 +404,14 @@ typedef enum {
     FMI_TUNE_ALLOC_SLOTS = 14     /* fmi_dev_alloc of >= 1 MiB: 1 (default) = place successive buckets in
                                     successive of 16 4-KiB slots (modulo 64 KiB) of a hipMalloc 64 KiB larger,
                                     so the buckets a fused kernel streams at one offset do not collide in HBM
-                                    (DESIGN §4); 0 = plain hipMalloc. fmi_dev_free takes either. Same bits */
+                                    (DESIGN §4); 0 = plain hipMalloc. fmi_dev_free takes either. Same bits */,
+    FMI_TUNE_COMM_SHARD_SKEW = 15 /* sharded collectives (path TREE allreduce): 1 (default) = the all-to-all lands
+                                    the N shards the fused shard kernel streams together in distinct 4 KiB slots
+                                    (stride: the shard rounded up to 64 KiB plus 4 KiB), its output in the next one,
+                                    where the transport posts a receive per peer anyway (LOCAL, PROC, RCCL's grouped
+                                    form FMI_TUNE_COMM_A2A = 1; never ncclAllToAll); 0 = back to back. Shards under
+                                    1 MiB stay back to back. Ranks may differ (only local placement changes). Same
+                                    bits */
 } fmi_tune_key_t;
 int fmi_tune_set(int key, long long value);
 int fmi_tune_get(int key, long long* value);

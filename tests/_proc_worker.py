@@ -17,7 +17,8 @@ from tests.test_gpu_parity import inputs
 # (name, dtype, op, n): n = 10 Mi + 3 floats makes every exchange larger than the 32 MiB staging slot
 ALLREDUCE_CASES = [("f32_sum", np.float32, Op.SUM, 1027), ("i64_prod", np.int64, Op.PROD, 3 * 65536 + 5),
                    ("f64_max", np.float64, Op.MAX, 1), ("i32_min", np.int32, Op.MIN, 4099),
-                   ("u8_sum", np.uint8, Op.SUM, 65536 + 3), ("f32_big", np.float32, Op.SUM, 10 * (1 << 20) + 3)]
+                   ("u8_sum", np.uint8, Op.SUM, 65536 + 3), ("f32_big", np.float32, Op.SUM, 10 * (1 << 20) + 3),
+                   ("f32_div", np.float32, Op.SUM, 3 * (1 << 20))]  # divisible by N = 2, 3, 4: skewed shards
 BIG = 10 * (1 << 20) + 3
 
 

@@ -121,6 +121,14 @@ bool check_all(int N, size_t unit) {
               [=](int) { return N * B; }, [=](int) { return N * B; },
               [=](int r, size_t b) { return P{int(b / B), r * B + b % B}; }}))
         return false;
+    // the shard kernel's receive at a stride (each shard in its own 4 KiB slot): the gap bytes stay untouched
+    for (size_t gap : {size_t(1), size_t(5)}) {
+        const size_t S = B + gap;
+        if (!run({"all_to_all stride +" + std::to_string(gap), N, [=](int r) { return fmi::plan::all_to_all(N, r, B, S); },
+                  [=](int) { return N * B; }, [=](int) { return N * S; },
+                  [=](int r, size_t b) { return b % S < B ? P{int(b / S), r * B + b % S} : none; }}))
+            return false;
+    }
     if (!run({"all_gather", N, [=](int r) { return fmi::plan::all_gather(N, r, B); }, [=](int) { return B; },
               [=](int) { return N * B; }, [=](int, size_t b) { return P{int(b / B), b % B}; }}))
         return false;

@@ -342,6 +342,43 @@ def test_comm_allreduce_host_concurrent_communicators(device):
                 assert_bit_equal(res[r][k], want[r], f"communicator N={N} call {k} rank {r}")
 
 
+@pytest.mark.parametrize("N", [2, 3, 8])
+def test_comm_allreduce_skewed_shards_same_bits(device, N):
+    """FMI_TUNE_COMM_SHARD_SKEW (fmi_comm.hip shard_stride): with shards of >= 1 MiB the
+    all-to-all lands shard j at stride (shard rounded up to 64 KiB) + 4 KiB and the reduced shard in the next slot.
+    Divisible and padded buckets, f32 sum and i64 max, give the same bits skewed and back to back, and equal the
+    oracle."""
+    from fmi_amd import Tune
+
+    cases = [(np.float32, Op.SUM, N * (1 << 18)), (np.float32, Op.SUM, N * 3 * (1 << 18) + 64 * N),
+             (np.int64, Op.MAX, N * (1 << 17) + 5)]
+    old = fmi_amd.tune_get(Tune.COMM_SHARD_SKEW)
+    try:
+        for dtype, op, n in cases:
+            xs = [inputs(dtype, n, r, seed=80 + N) for r in range(N)]
+            got = {}
+            for skew in (1, 0):
+                fmi_amd.tune_set(Tune.COMM_SHARD_SKEW, skew)
+
+                def body(c, r):
+                    s, o = Bucket.from_numpy(xs[r]), Bucket(n, dtype)
+                    c.allreduce(op, s, o)
+                    fmi_amd.sync()
+                    res = o.numpy()
+                    s.free()
+                    o.free()
+                    return res
+
+                got[skew] = run_ranks(N, body)
+            with np.errstate(all="ignore"):
+                want, _ = orc.allreduce(xs, orc.OPS[OPNAME[op]])
+            for r in range(N):
+                assert got[1][r].tobytes() == got[0][r].tobytes(), f"{np.dtype(dtype).name} n={n} rank {r}"
+                assert_bit_equal(got[1][r], want[r], f"{np.dtype(dtype).name} n={n} rank {r}")
+    finally:
+        fmi_amd.tune_set(Tune.COMM_SHARD_SKEW, old)
+
+
 def test_comm_allreduce_host_after_an_aborted_communicator(device):
     """an aborted communicator must not hold up the host pipelines of later ones. A 2-rank LOCAL
     communicator whose rank 1 never calls times out in its host allreduce (rank 0 has queued chunk copies by then);

@@ -7,6 +7,9 @@
 #                                (tools/shard_layout_ab.py)
 #   bash tools/gpu_round6.sh b   placement, round two (TAG=r06b): the allocator's placements beside explicit slot lists,
 #                                mode order rotated per rep, under a kernel trace
+#   bash tools/gpu_round6.sh c   placement, round three (TAG=r06c): per-set slot shifts (s:...@K), pair and scan
+#   bash tools/gpu_round6.sh d   the skewed shard receive: its GPU suites, then the shard kernel in fmi_comm_allreduce
+#                                with 8 LOCAL ranks, skew on / off (TAG=r06d)
 set -o pipefail
 cd /root/repo
 mkdir -p gpurun_out
@@ -48,6 +51,30 @@ ab)
     cd $R &&
     python3 tools/placement_ab_trace.py gpurun_out/${TAG}_placement_ab.jsonl gpurun_out/${TAG}_placement_trace \
         > gpurun_out/${TAG}_placement_ab_trace.jsonl
+    ;;
+c)
+    # placement, round three: is it the slot of each stream, or how consecutive launches' slots differ? Explicit
+    # lists with a per-set shift (s:...@K): the bench's rotating layouts rebuilt exactly, and the group's with the
+    # sets alternating halves; order rotated per rep, 4 reps
+    cd /tmp
+    timeout -k 10 900 rocprofv3 --kernel-trace --output-format csv -d $R/gpurun_out/${TAG}_placement_trace -o run -- \
+        python3 $R/tools/placement_ab.py --reps 4 --rotate-order --kernels pair,scan \
+        --modes-pair plain,rotating,group,s:0.1@2,s:0.0@2,s:0.0@0 \
+        --modes-scan rotating,group,s:0.1.2.3.4.5.6.7.0.1.2.3.4.5.6.7@8,s:0.1.2.3.4.5.6.7.0.1.2.3.4.5.6.7@0,s:0.1.2.3.4.5.6.7.8.9.10.11.12.13.14.15@8,s:0.1.2.3.4.5.6.7.8.9.10.11.12.13.14.15@0 \
+        > $R/gpurun_out/${TAG}_placement_ab.jsonl 2> $R/gpurun_out/${TAG}_placement_ab.err &&
+    cd $R &&
+    python3 tools/placement_ab_trace.py gpurun_out/${TAG}_placement_ab.jsonl gpurun_out/${TAG}_placement_trace \
+        > gpurun_out/${TAG}_placement_ab_trace.jsonl
+    ;;
+d)
+    # the skewed shard receive in the product (FMI_TUNE_COMM_SHARD_SKEW): its parity tests (LOCAL, PROC, the full-size
+    # C4 and C5 allreduces, the communicator sweep at its default seeds), then the shard kernel inside fmi_comm_allreduce
+    # with 8 LOCAL ranks, skew on / off interleaved (tools/shard_skew_comm.py)
+    timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread -p no:cacheprovider \
+        tests/test_gpu_comm.py tests/test_gpu_proc.py tests/test_gpu_comm_random_sweep.py \
+        > gpurun_out/${TAG}_tests.log 2>&1 &&
+    timeout -k 10 400 python -u tools/shard_skew_comm.py --ranks 8 --reps 4 > gpurun_out/${TAG}_shard_skew_comm.jsonl \
+        2> gpurun_out/${TAG}_shard_skew_comm.err
     ;;
 *)
     echo "unknown step $1" >&2

@@ -10,7 +10,8 @@ second (the driver clears freed VRAM in the background), launches `warmup` untim
         group     Bucket.group(2): a in slot 0, b in slot 1 of their own hipMallocs (fmi_dev_alloc_group)
         same_slot both operands in slot k = 1 + s % 15 (same relative offset as plain, not 2 MiB aligned)
   any kernel: s:i.j.k...  bucket j (allocation order: pair a, b; scan 8 inputs then 8 outputs; tree 8 inputs then
-            the output) at 4 KiB slot list[j] of a plain hipMalloc 64 KiB larger, every set alike
+            the output) at 4 KiB slot list[j] of a plain hipMalloc 64 KiB larger, every set alike;
+            s:i.j.k...@K  the same with set s's slots moved by K x s (mod 16)
   scan  (C3 scan, bench.py c3_single: 8 sets of 8 inputs ALL allocated first, then all 8 x 8 outputs, 64 MiB f32)
         plain / rotating as above; group: Bucket.group(16) per set (inputs slots 0-7, outputs 8-15)
   tree  (bench.py c4_single: 8 inputs then the output, 1 GiB f32 each, one set)
@@ -51,15 +52,18 @@ def at_slots(slots, n, dtype=np.float32):
     return [o.view(k * SLOT // item, n) for o, k in zip(owners, slots)], owners
 
 
-def slot_mode(mode):
-    """'s:0,1,...' -> the slot list, else None"""
-    return [int(x) for x in mode[2:].split(".")] if mode.startswith("s:") else None
+def slot_mode(mode, s=0):
+    """'s:0.1...' -> the slot list; 's:0.1...@K' -> each slot + K x set index (mod 16); else None"""
+    if not mode.startswith("s:"):
+        return None
+    body, _, k = mode[2:].partition("@")
+    return [(int(x) + int(k or 0) * s) % 16 for x in body.split(".")]
 
 
 def alloc(mode, count, n, dtype=np.float32, slot=None):
     """`count` buckets of n elements, one allocation each, placed per `mode` (owners to free, views to use)."""
     if slot_mode(mode):
-        return at_slots(slot_mode(mode), n, dtype)
+        return at_slots(slot_mode(mode, slot), n, dtype)
     if mode == "group":
         bs = Bucket.group(count, n, dtype)
         return bs, bs
@@ -94,7 +98,7 @@ def pair(mode, warmup, steps):
     n, S = 256 * MIB // 4, 16
     sets, owners = [], []
     for s in range(S):  # bench.py run_single: a then b, set after set
-        (a, b), own = alloc(mode, 2, n, slot=1 + s % 15)
+        (a, b), own = alloc(mode, 2, n, slot=s if slot_mode(mode) else 1 + s % 15)
         a.fill_synthetic(42 + s, 0)
         b.fill_synthetic(42 + s, 1)
         sets.append((a, b))
@@ -125,8 +129,8 @@ def scan(mode, warmup, steps):
     owners = []
     if mode == "group" or slot_mode(mode):
         groups, owners = [], []
-        for _ in range(S):
-            g, own = (Bucket.group(2 * P, n, np.float32), None) if mode == "group" else at_slots(slot_mode(mode), n)
+        for s in range(S):
+            g, own = (Bucket.group(2 * P, n, np.float32), None) if mode == "group" else at_slots(slot_mode(mode, s), n)
             groups.append(g)
             owners += own or g
         ins = [g[:P] for g in groups]
