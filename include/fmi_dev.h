@@ -409,7 +409,7 @@ typedef enum {
                                     the N shards the fused shard kernel streams together in distinct 4 KiB slots
                                     (stride: the shard rounded up to 64 KiB plus 4 KiB), its output in the next one,
                                     where the transport posts a receive per peer anyway (LOCAL, PROC, RCCL's grouped
-                                    form FMI_TUNE_COMM_A2A = 1; never ncclAllToAll); 0 = back to back. Shards under
+                                    form, FMI_TUNE_COMM_A2A set to 1; never ncclAllToAll); 0 = back to back. Shards under
                                     1 MiB stay back to back. Ranks may differ (only local placement changes). Same
                                     bits */
 } fmi_tune_key_t;
