@@ -486,7 +486,9 @@ def placement() -> str:
     except Exception as e:  # reported, never required
         return f"unknown ({type(e).__name__}: {e})"
     return ("fmi_dev_alloc: every bucket of >= 1 MiB in the next of 16 rotating 4 KiB slots (mod 64 KiB) of its own "
-            "hipMalloc (FMI_TUNE_ALLOC_SLOTS = 1)" if on else "fmi_dev_alloc: plain hipMalloc (FMI_TUNE_ALLOC_SLOTS = 0)")
+            "hipMalloc (FMI_TUNE_ALLOC_SLOTS = 1)" if on else
+            "fmi_dev_alloc: plain hipMalloc, 2 MiB aligned (FMI_TUNE_ALLOC_SLOTS = 0, the default: the pair kernel's "
+            "best placement, profiles/r06a_placement_ab.jsonl)")
 
 
 def _headline(args, value, step_ms, workload, parallelism, n, roofline):

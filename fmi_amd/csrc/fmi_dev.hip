@@ -35,15 +35,17 @@ struct DeviceState {
 std::mutex g_mu;
 DeviceState g_state;
 
-// Bucket placement (fmi_dev_alloc, round 5). A fused kernel reads its P buckets at the same offset at the same time.
-// Separate hipMallocs of large buckets start on 2 MiB boundaries, so those P streams sit at the same offset modulo
-// every HBM interleave period below 2 MiB, and they collide: the 8-way tree at 512 MiB per peer ran 0.71 of peak on
-// separate allocations, 0.62 with the buckets packed back to back, and 0.83 with bucket j shifted by j x 4 KiB
-// (profiles/r05_skew_sweep.jsonl, tools/skew_sweep.py; the C3 scan 0.75 -> 0.80, the N = 8 shard shape 0.73 ->
-// 0.79; the pair and copy kernels, 2-3 streams, within 1 %). Shifts of 16, 32 or 64 KiB collide again: what counts
-// is a distinct 4 KiB slot modulo 64 KiB for each stream. So every allocation of >= 1 MiB is placed at the next of
-// 16 such slots inside a hipMalloc 64 KiB larger: any 16 buckets allocated one after another (a fused kernel's
-// inputs and outputs, up to 8 in + 8 out) sit in distinct slots. FMI_TUNE_ALLOC_SLOTS = 0 turns it off.
+// Bucket placement (fmi_dev_alloc / fmi_dev_alloc_group). A fused kernel reads its P buckets at the same
+// offset at the same time. Separate hipMallocs of large buckets start on 2 MiB boundaries, so those P streams sit at
+// the same offset modulo every HBM interleave period below 2 MiB, and they collide: the 8-way tree at 512 MiB per
+// peer ran 0.71 of peak on separate allocations, 0.62 with the buckets packed back to back, and 0.83 with bucket j
+// shifted by j x 4 KiB (profiles/r05_skew_sweep.jsonl, tools/skew_sweep.py). Shifts of 16, 32 or 64 KiB collide
+// again: what counts is a distinct 4 KiB slot modulo 64 KiB for each stream. The pairwise kernel is the other way
+// round: it runs fastest with both operands at their 2 MiB-aligned base, and 1.8-1.9 % slower when they sit in
+// nonzero slots (profiles/r06a_placement_ab.jsonl, r06b_placement_ab.jsonl: two boxes, kernel traces). So a plain
+// fmi_dev_alloc is a plain hipMalloc (FMI_TUNE_ALLOC_SLOTS = 0, the default since round 6), and the buckets one fused
+// kernel streams together are allocated as one group (fmi_dev_alloc_group): bucket j in slot j mod 16, whatever was
+// allocated before. FMI_TUNE_ALLOC_SLOTS = 1 restores round 5's rotation of every fmi_dev_alloc over the 16 slots.
 constexpr size_t kSlotBytes = 4096, kSlots = 16, kSlotSpan = kSlotBytes * kSlots, kSlotMinBytes = size_t(1) << 20;
 std::mutex g_slots_mu;
 size_t g_next_slot = 0;
@@ -145,7 +147,7 @@ std::atomic<long long> g_tune[16] = {2 /*variant: nontemporal tiles*/, 4 /*unrol
                                      0 /*no allreduce pipelining*/, 1 /*fused kernels: buffer ops where measured faster*/,
                                      1 /*pairwise: tiles t % 8 < 1 (one XCD) store sc1 (tools/ab_pair_sc1.py)*/,
                                      0 /*one-rank communicators copy*/,
-                                     1 /*bucket allocations rotate over 16 4-KiB slots (profiles/r05_skew_sweep.jsonl)*/,
+                                     0 /*plain allocations; groups take slots (profiles/r06a_placement_ab.jsonl)*/,
                                      1 /*shard kernel inputs in their own 4 KiB slots (profiles/r06a_shard_layout.jsonl)*/};
 
 int hip_fail(const char* what, hipError_t e) {

@@ -103,10 +103,10 @@ int fmi_dev_describe(char* buf, size_t len);
 int fmi_dev_pci_bus_id(int device, char* buf, size_t len);
 
 /* ---- memory (replaces the reference's new[]/std::vector bucket storage, include/comm/Data.h:50-97)
- * fmi_dev_alloc: device memory, 4 KiB aligned. Buckets of >= 1 MiB are placed in rotating 4 KiB slots
- * (FMI_TUNE_ALLOC_SLOTS) so that the buckets one fused kernel streams together do not collide in HBM; free with
- * fmi_dev_free only (the pointer may lie inside its hipMalloc, up to 60 KiB past its base, so it is not a
- * hipIpcGetMemHandle base either: memory shared across processes comes from fmi_comm_window_alloc). */
+ * fmi_dev_alloc: device memory, 4 KiB aligned: a plain hipMalloc (the pairwise kernel's best placement), or with
+ * FMI_TUNE_ALLOC_SLOTS = 1 buckets of >= 1 MiB in rotating 4 KiB slots. Free with fmi_dev_free only (a slotted
+ * pointer lies inside its hipMalloc, up to 60 KiB past its base, so it is not a hipIpcGetMemHandle base either:
+ * memory shared across processes comes from fmi_comm_window_alloc). */
 int fmi_dev_alloc(void** ptr, size_t bytes);
 /* fmi_dev_alloc_group: `count` buckets of `bytes` each that one kernel streams together (a fused kernel's P
  * inputs and its outputs). Buckets of >= 1 MiB: bucket j sits in 4 KiB slot j mod 16 (modulo 64 KiB) of its own
@@ -401,10 +401,11 @@ typedef enum {
                                     reduce-scatter, window mapping, the pipelined split — exchanging with
                                     itself, instead of the reference's P = 1 copy. Same bits; exists so that
                                     a 1-GPU box runs the RCCL transport's real collectives (tests). Default 0 */
-    FMI_TUNE_ALLOC_SLOTS = 14     /* fmi_dev_alloc of >= 1 MiB: 1 (default) = place successive buckets in
-                                    successive of 16 4-KiB slots (modulo 64 KiB) of a hipMalloc 64 KiB larger,
-                                    so the buckets a fused kernel streams at one offset do not collide in HBM
-                                    (DESIGN §4); 0 = plain hipMalloc. fmi_dev_free takes either. Same bits */,
+    FMI_TUNE_ALLOC_SLOTS = 14     /* fmi_dev_alloc of >= 1 MiB: 0 (default since round 6) = plain hipMalloc;
+                                    1 = place successive buckets in successive of 16 4-KiB slots (modulo 64 KiB)
+                                    of a hipMalloc 64 KiB larger (round 5). The buckets of one fused kernel belong
+                                    in one fmi_dev_alloc_group, which places them whatever this says.
+                                    fmi_dev_free takes either. Same bits */,
     FMI_TUNE_COMM_SHARD_SKEW = 15 /* sharded collectives (path TREE allreduce): 1 (default) = the all-to-all lands
                                     the N shards the fused shard kernel streams together in distinct 4 KiB slots
                                     (stride: the shard rounded up to 64 KiB plus 4 KiB), its output in the next one,

@@ -378,15 +378,15 @@ def test_cpu_baseline_falls_back_to_the_port_only_without_oracle_ref(monkeypatch
 
 
 def test_line_names_the_bucket_placement():
-    """The N = 1 / N > 1 line's config.placement says how the device buckets were placed: the
-    allocator's rotating 4 KiB slots by default, plain hipMalloc when FMI_TUNE_ALLOC_SLOTS = 0."""
+    """The N = 1 / N > 1 line's config.placement says how the device buckets were placed: plain
+    hipMallocs by default (the pair's buckets), the allocator's rotating 4 KiB slots when FMI_TUNE_ALLOC_SLOTS = 1."""
     import fmi_amd
 
     old = fmi_amd.tune_get(fmi_amd.Tune.ALLOC_SLOTS)
     try:
-        assert old == 1 and "FMI_TUNE_ALLOC_SLOTS = 1" in bench.placement()
-        fmi_amd.tune_set(fmi_amd.Tune.ALLOC_SLOTS, 0)
-        assert "plain hipMalloc" in bench.placement()
+        assert old == 0 and "plain hipMalloc" in bench.placement()
+        fmi_amd.tune_set(fmi_amd.Tune.ALLOC_SLOTS, 1)
+        assert "FMI_TUNE_ALLOC_SLOTS = 1" in bench.placement()
         with pytest.raises(fmi_amd.FmiError):
             fmi_amd.tune_set(fmi_amd.Tune.ALLOC_SLOTS, 3)
     finally:

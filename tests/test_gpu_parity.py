@@ -1003,12 +1003,21 @@ def test_beyond_2pow32_elements_64bit_indexing(device):
 
 
 def test_dev_alloc_places_buckets_in_rotating_slots(device):
-    """fmi_dev_alloc: 16 buckets of >= 1 MiB allocated one after another sit in 16 distinct 4 KiB slots
-    modulo 64 KiB (the buckets a fused kernel streams at one offset must not collide in HBM), are 4 KiB aligned,
-    usable to their last byte and freed through fmi_dev_free; small buckets and FMI_TUNE_ALLOC_SLOTS = 0 are plain
-    hipMallocs; a fused kernel over slotted buckets gives the same bits as over plain ones."""
+    """fmi_dev_alloc with FMI_TUNE_ALLOC_SLOTS = 1 (round 5's placement): 16 buckets of >= 1 MiB
+    allocated one after another sit in 16 distinct 4 KiB slots modulo 64 KiB, are 4 KiB aligned, usable to their
+    last byte and freed through fmi_dev_free; small buckets and the default (0) are plain hipMallocs; a fused kernel
+    over slotted buckets gives the same bits as over plain ones."""
     n = (1 << 20) // 4 + 7
-    bs = [Bucket(n, np.float32) for _ in range(16)]
+    default = fmi_amd.tune_get(Tune.ALLOC_SLOTS)
+    assert default == 0
+    plain_first = Bucket(16 << 20, np.float32)  # by default a plain hipMalloc: a large bucket at its aligned base
+    assert plain_first.ptr % 65536 == 0, hex(plain_first.ptr)
+    plain_first.free()
+    fmi_amd.tune_set(Tune.ALLOC_SLOTS, 1)
+    try:
+        bs = [Bucket(n, np.float32) for _ in range(16)]
+    finally:
+        fmi_amd.tune_set(Tune.ALLOC_SLOTS, default)
     slots = {(b.ptr % 65536) // 4096 for b in bs}
     assert len(slots) == 16 and all(b.ptr % 4096 == 0 for b in bs), [hex(b.ptr) for b in bs]
     for k, b in enumerate(bs):
@@ -1021,7 +1030,6 @@ def test_dev_alloc_places_buckets_in_rotating_slots(device):
     fmi_amd.reduce_tree(Op.SUM, Alg.ALLREDUCE, out_slotted, bs[:8])
     old = fmi_amd.tune_get(Tune.ALLOC_SLOTS)
     try:
-        fmi_amd.tune_set(Tune.ALLOC_SLOTS, 0)
         plain = [Bucket.from_numpy(x) for x in xs]
         out_plain = Bucket(n, np.float32)
         fmi_amd.reduce_tree(Op.SUM, Alg.ALLREDUCE, out_plain, plain)
