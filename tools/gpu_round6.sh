@@ -10,6 +10,7 @@
 #   bash tools/gpu_round6.sh c   placement, round three (TAG=r06c): per-set slot shifts (s:...@K), pair and scan
 #   bash tools/gpu_round6.sh d   the skewed shard receive: its GPU suites, then the shard kernel in fmi_comm_allreduce
 #                                with 8 LOCAL ranks, skew on / off (TAG=r06d)
+#   bash tools/gpu_round6.sh z   the round-end sequence: GPU suite, smoke(), default line, C2 profile (TAG=r06z...)
 set -o pipefail
 cd /root/repo
 mkdir -p gpurun_out
@@ -75,6 +76,16 @@ d)
         > gpurun_out/${TAG}_tests.log 2>&1 &&
     timeout -k 10 400 python -u tools/shard_skew_comm.py --ranks 8 --reps 4 > gpurun_out/${TAG}_shard_skew_comm.jsonl \
         2> gpurun_out/${TAG}_shard_skew_comm.err
+    ;;
+z)
+    # the round-end sequence on the current library and bench: the whole GPU suite, smoke(), the default line, then
+    # the C2 profile (kernel trace + stats, separate FETCH_SIZE / WRITE_SIZE passes, an unprofiled line; then
+    # tools/pmc_summarize.py --tag $TAG_c2 --merge here)
+    timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+        -p no:cacheprovider > gpurun_out/${TAG}_full_gpu.log 2>&1 &&
+    timeout -k 10 300 python -u -c 'import __graft_entry__ as g; g.smoke()' > gpurun_out/${TAG}_smoke.log 2>&1 &&
+    timeout -k 10 600 python bench.py > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err &&
+    bash tools/c2_profile.sh
     ;;
 *)
     echo "unknown step $1" >&2
