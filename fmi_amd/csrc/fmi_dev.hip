@@ -50,6 +50,11 @@ constexpr size_t kSlotBytes = 4096, kSlots = 16, kSlotSpan = kSlotBytes * kSlots
 std::mutex g_slots_mu;
 size_t g_next_slot = 0;
 std::map<void*, void*> g_slotted;  // pointer handed out -> its hipMalloc base
+struct Group {
+    void* base;  // the group's one hipMalloc
+    int live;    // its buckets not yet freed
+};
+std::map<void*, Group*> g_grouped;  // a group's bucket -> its group
 
 // Host-ingress pipeline of fmi_host_reduce_pair: two slots of (a, b) device staging and two streams per SET. The
 // reference's peers combine concurrently when they are threads of one process (its allreduce's peers each call
@@ -998,26 +1003,39 @@ int fmi_dev_alloc_group(void** ptrs, int count, size_t bytes) {
     if (!ptrs || count < 0) return fail(FMI_ERR_INVALID, "bad group");
     for (int j = 0; j < count; ++j) ptrs[j] = nullptr;
     if (int rc = require_device()) return rc;
-    const bool slotted = bytes >= kSlotMinBytes && bytes <= SIZE_MAX - kSlotSpan;
-    for (int j = 0; j < count; ++j) {
-        void* base = nullptr;
-        const hipError_t e = hipMalloc(&base, std::max<size_t>(bytes, 1) + (slotted ? kSlotSpan : 0));
-        if (e != hipSuccess) {
-            (void)hipGetLastError();  // not left for the next launch's error check to find
-            const std::string msg = "hipMalloc(" + std::to_string(bytes) + ") for group bucket " + std::to_string(j) +
-                                    ": " + hipGetErrorString(e);
-            for (int i = 0; i < j; ++i) (void)fmi_dev_free(ptrs[i]);
-            for (int i = 0; i < j; ++i) ptrs[i] = nullptr;
-            return fail(FMI_ERR_ALLOC, msg);
+    if (count == 0) return FMI_OK;
+    if (bytes < kSlotMinBytes) {  // small buckets: plain allocations, nothing to place
+        for (int j = 0; j < count; ++j) {
+            const hipError_t e = hipMalloc(&ptrs[j], std::max<size_t>(bytes, 1));
+            if (e != hipSuccess) {
+                (void)hipGetLastError();  // not left for the next launch's error check to find
+                for (int i = 0; i < j; ++i) (void)hipFree(ptrs[i]);
+                for (int i = 0; i < count; ++i) ptrs[i] = nullptr;
+                return fail(FMI_ERR_ALLOC, "hipMalloc(" + std::to_string(bytes) + ") for group bucket " +
+                                               std::to_string(j) + ": " + hipGetErrorString(e));
+            }
         }
-        if (!slotted) {
-            ptrs[j] = base;
-            continue;
-        }
-        char* p = static_cast<char*>(base) + (static_cast<size_t>(j) % kSlots) * kSlotBytes;
-        std::lock_guard<std::mutex> lk(g_slots_mu);
-        g_slotted[p] = base;
-        ptrs[j] = p;
+        return FMI_OK;
+    }
+    // One allocation for the whole group, bucket j at j x stride: each bucket in its own 4 KiB slot (stride = the
+    // bucket rounded up to 64 KiB, plus 4 KiB), and the group's memory one range (see the placement note above).
+    const size_t n = static_cast<size_t>(count);
+    if (bytes > (SIZE_MAX - kSlotSpan) / (n + 1)) return fail(FMI_ERR_INVALID, "group too large");
+    const size_t stride = (bytes + kSlotSpan - 1) / kSlotSpan * kSlotSpan + kSlotBytes;
+    const size_t total = (n - 1) * stride + bytes + kSlotSpan;  // + room to start the range on a 64 KiB boundary
+    void* base = nullptr;
+    const hipError_t e = hipMalloc(&base, total);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();  // not left for the next launch's error check to find
+        return fail(FMI_ERR_ALLOC, "hipMalloc(" + std::to_string(total) + ") for a group of " + std::to_string(count) +
+                                       " buckets of " + std::to_string(bytes) + " B: " + hipGetErrorString(e));
+    }
+    char* first = static_cast<char*>(base) + (kSlotSpan - reinterpret_cast<uintptr_t>(base) % kSlotSpan) % kSlotSpan;
+    std::lock_guard<std::mutex> lk(g_slots_mu);
+    auto* g = new Group{base, count};
+    for (size_t j = 0; j < n; ++j) {
+        ptrs[j] = first + j * stride;
+        g_grouped[ptrs[j]] = g;
     }
     return FMI_OK;
 }
@@ -1032,6 +1050,14 @@ int fmi_dev_free(void* ptr) {
         if (it != g_slotted.end()) {
             base = it->second;
             g_slotted.erase(it);
+        }
+        auto gt = g_grouped.find(ptr);
+        if (gt != g_grouped.end()) {  // a group's bucket: its range goes with the group's last bucket
+            Group* g = gt->second;
+            g_grouped.erase(gt);
+            if (--g->live > 0) return FMI_OK;
+            base = g->base;
+            delete g;
         }
     }
     FMI_HIP_TRY(hipFree(base));

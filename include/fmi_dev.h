@@ -109,9 +109,11 @@ int fmi_dev_pci_bus_id(int device, char* buf, size_t len);
  * memory shared across processes comes from fmi_comm_window_alloc). */
 int fmi_dev_alloc(void** ptr, size_t bytes);
 /* fmi_dev_alloc_group: `count` buckets of `bytes` each that one kernel streams together (a fused kernel's P
- * inputs and its outputs). Buckets of >= 1 MiB: bucket j sits in 4 KiB slot j mod 16 (modulo 64 KiB) of its own
- * hipMalloc, whatever was allocated before and whatever FMI_TUNE_ALLOC_SLOTS says, so the group's streams never
- * collide in HBM. All or nothing: on failure every ptrs[j] is NULL. Free each with fmi_dev_free. */
+ * inputs and its outputs). Buckets of >= 1 MiB are carved from ONE allocation at a stride of `bytes` rounded up to
+ * 64 KiB plus 4 KiB, so bucket j sits in 4 KiB slot j mod 16 (modulo 64 KiB) whatever was allocated before and
+ * whatever FMI_TUNE_ALLOC_SLOTS says, and the group's streams never collide in HBM; smaller ones are
+ * plain allocations. All or nothing: on failure every ptrs[j] is NULL. Free each with fmi_dev_free, in any order: a
+ * carved group's memory is released with its last bucket. */
 int fmi_dev_alloc_group(void** ptrs, int count, size_t bytes);
 int fmi_dev_free(void* ptr);
 int fmi_host_pin_alloc(void** ptr, size_t bytes);  /* page-locked host memory for recv buffers */

@@ -1048,9 +1048,10 @@ def test_dev_alloc_places_buckets_in_rotating_slots(device):
 def test_dev_alloc_group_places_each_bucket_by_its_index(device):
     """fmi_dev_alloc_group: bucket j of a group of >= 1 MiB buckets sits in 4 KiB slot j mod 16 modulo
     64 KiB whatever was allocated before (here after 5 and 11 unrelated slotted allocations, and with
-    FMI_TUNE_ALLOC_SLOTS = 0), usable to its last byte, freed through fmi_dev_free; a fused kernel over a group
-    gives the same bits as over plain buckets; small groups are plain 4 KiB-aligned allocations; an impossible group
-    fails whole (FmiError, no bucket handed out); count 0 is a no-op."""
+    FMI_TUNE_ALLOC_SLOTS = 0), carved from one allocation, usable to its last byte, freed through fmi_dev_free in any
+    order (the range goes with the last bucket); a fused kernel over a group gives the same bits as over plain
+    buckets; small groups are plain 4 KiB-aligned allocations; an impossible group fails whole (FmiError, no bucket
+    handed out, and no error left behind for the next launch); count 0 is a no-op."""
     n = (1 << 20) // 4 + 7
     old = fmi_amd.tune_get(Tune.ALLOC_SLOTS)
     try:
@@ -1059,6 +1060,7 @@ def test_dev_alloc_group_places_each_bucket_by_its_index(device):
             others = [Bucket(n, np.float32) for _ in range(before)]
             g = Bucket.group(18, n, np.float32)
             assert [(b.ptr % 65536) // 4096 for b in g] == [j % 16 for j in range(18)], [hex(b.ptr) for b in g]
+            assert len({g[j + 1].ptr - g[j].ptr for j in range(17)}) == 1  # one range, a fixed stride
             for k, b in enumerate(g):
                 b.fill_synthetic(3, k)
             for k, b in enumerate(g):
@@ -1070,7 +1072,7 @@ def test_dev_alloc_group_places_each_bucket_by_its_index(device):
             out = Bucket(n, np.float32)
             fmi_amd.reduce_tree(Op.SUM, Alg.ALLREDUCE, out, plain)
             assert out.numpy().tobytes() == g[8].numpy().tobytes()
-            for b in others + g + plain + [out]:
+            for b in others + (g[::-1] if before == 11 else g) + plain + [out]:
                 b.free()
     finally:
         fmi_amd.tune_set(Tune.ALLOC_SLOTS, old)
@@ -1079,8 +1081,13 @@ def test_dev_alloc_group_places_each_bucket_by_its_index(device):
     for b in small:
         b.free()
     assert Bucket.group(0, n, np.float32) == []
-    with pytest.raises(fmi_amd.FmiError, match="group bucket"):
-        Bucket.group(3, 1 << 46, np.uint8)  # 64 TiB each: the first hipMalloc already fails
+    with pytest.raises(fmi_amd.FmiError, match="group of 3 buckets"):
+        Bucket.group(3, 1 << 46, np.uint8)  # 64 TiB each: the group's one allocation fails
+    a, b = Bucket.from_numpy(np.ones(4099, np.float32)), Bucket.from_numpy(np.ones(4099, np.float32))
+    fmi_amd.reduce_pair(Op.SUM, a, b)  # the failed allocation left no error behind for the next launch to find
+    assert np.array_equal(a.numpy(), np.full(4099, 2, np.float32))
+    a.free()
+    b.free()
 
 
 @pytest.mark.parametrize("chunk", [(1 << 16), (3 << 20) + 4096, (64 << 20)])

@@ -10,6 +10,10 @@
 #   bash tools/gpu_round6.sh c   placement, round three (TAG=r06c): per-set slot shifts (s:...@K), pair and scan
 #   bash tools/gpu_round6.sh d   the skewed shard receive: its GPU suites, then the shard kernel in fmi_comm_allreduce
 #                                with 8 LOCAL ranks, skew on / off (TAG=r06d)
+#   bash tools/gpu_round6.sh f   carved groups: their GPU tests, placement round four (group vs rotating vs the same
+#                                slots as separate allocations), the default line (TAG=r06f)
+#   bash tools/gpu_round6.sh p   bench.py --force-dist at world 1 over RCCL, diagnostics and C5 at 1 GiB (TAG=r06p)
+#   bash tools/gpu_round6.sh q   the N > 1 line at full size, 8 PROC ranks on one GPU (TAG=r06q)
 #   bash tools/gpu_round6.sh z   the round-end sequence: GPU suite, smoke(), default line, C2 profile (TAG=r06z...)
 set -o pipefail
 cd /root/repo
@@ -76,6 +80,41 @@ d)
         > gpurun_out/${TAG}_tests.log 2>&1 &&
     timeout -k 10 400 python -u tools/shard_skew_comm.py --ranks 8 --reps 4 > gpurun_out/${TAG}_shard_skew_comm.jsonl \
         2> gpurun_out/${TAG}_shard_skew_comm.err
+    ;;
+f)
+    # the carved groups (fmi_dev_alloc_group: one allocation per group, bucket j at j x (bucket + 4 KiB)): their GPU
+    # tests; then placement, round four: the carved group against rotating slots and the same slots as separate
+    # allocations (s:...), order rotated per rep, 4 reps, under a trace; then the default line
+    timeout -k 10 600 python -u -m pytest -x -v --timeout 120 --timeout-method thread -p no:cacheprovider \
+        tests/test_gpu_parity.py -k "alloc" > gpurun_out/${TAG}_tests.log 2>&1 &&
+    timeout -k 10 300 python -u -m pytest -x -v --timeout 240 --timeout-method thread -p no:cacheprovider \
+        tests/test_cpp_communicator.py -m gpu >> gpurun_out/${TAG}_tests.log 2>&1 &&
+    cd /tmp &&
+    timeout -k 10 900 rocprofv3 --kernel-trace --output-format csv -d $R/gpurun_out/${TAG}_placement_trace -o run -- \
+        python3 $R/tools/placement_ab.py --reps 4 --rotate-order \
+        --modes-pair plain,group,rotating \
+        --modes-scan rotating,group,s:0.1.2.3.4.5.6.7.8.9.10.11.12.13.14.15 \
+        --modes-tree rotating,group,s:0.1.2.3.4.5.6.7.8,plain \
+        > $R/gpurun_out/${TAG}_placement_ab.jsonl 2> $R/gpurun_out/${TAG}_placement_ab.err &&
+    cd $R &&
+    python3 tools/placement_ab_trace.py gpurun_out/${TAG}_placement_ab.jsonl gpurun_out/${TAG}_placement_trace \
+        > gpurun_out/${TAG}_placement_ab_trace.jsonl &&
+    timeout -k 10 600 python bench.py > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err
+    ;;
+p)
+    # the N > 1 code path at world size 1 over RCCL with the full exchange (--force-dist, diagnostics on: the
+    # exchange variants run the grouped all-to-all, i.e. RCCL's grouped ncclSend / ncclRecv with the skewed shard
+    # receive), C5 at 1 GiB
+    timeout -k 10 500 python -m torch.distributed.run --nnodes=1 --nproc-per-node=1 --master-addr 127.0.0.1 \
+        --master-port 29633 bench.py --force-dist --steps 20 --warmup 5 --c5-mib 1024 \
+        > gpurun_out/${TAG}_force_dist.json 2> gpurun_out/${TAG}_force_dist.err
+    ;;
+q)
+    # the N > 1 line rehearsed at full size with 8 ranks as processes on the one GPU (PROC transport over gloo):
+    # 256 MiB buckets, C4 at 1 GiB per peer, C5 at 1 GiB per rank, diagnostics on
+    FMI_PROC_TIMEOUT_S=300 timeout -k 10 1000 python -m torch.distributed.run --nnodes=1 --nproc-per-node=8 \
+        --master-addr 127.0.0.1 --master-port 29644 bench.py --gpus 8 --transport proc --steps 20 --warmup 3 \
+        --diag-deadline 600 > gpurun_out/${TAG}_bench_proc8_rehearsal.json 2> gpurun_out/${TAG}_bench_proc8_rehearsal.err
     ;;
 z)
     # the round-end sequence on the current library and bench: the whole GPU suite, smoke(), the default line, then
