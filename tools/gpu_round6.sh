@@ -12,6 +12,7 @@
 #                                with 8 LOCAL ranks, skew on / off (TAG=r06d)
 #   bash tools/gpu_round6.sh f   carved groups: their GPU tests, placement round four (group vs rotating vs the same
 #                                slots as separate allocations), the default line (TAG=r06f)
+#   bash tools/gpu_round6.sh g   the pair's buckets: plain, carved group, per-set carve, one 8 GiB carve (TAG=r06g)
 #   bash tools/gpu_round6.sh p   bench.py --force-dist at world 1 over RCCL, diagnostics and C5 at 1 GiB (TAG=r06p)
 #   bash tools/gpu_round6.sh q   the N > 1 line at full size, 8 PROC ranks on one GPU (TAG=r06q)
 #   bash tools/gpu_round6.sh z   the round-end sequence: GPU suite, smoke(), default line, C2 profile (TAG=r06z...)
@@ -100,6 +101,18 @@ f)
     python3 tools/placement_ab_trace.py gpurun_out/${TAG}_placement_ab.jsonl gpurun_out/${TAG}_placement_trace \
         > gpurun_out/${TAG}_placement_ab_trace.jsonl &&
     timeout -k 10 600 python bench.py > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err
+    ;;
+g)
+    # the pair kernel's buckets: plain separate allocations, the carved group, each set carved at stride bucket + 0,
+    # and all 16 sets carved from one 8 GiB allocation at + 0 / + 4 KiB; order rotated per rep, 4 reps, under a trace
+    cd /tmp &&
+    timeout -k 10 900 rocprofv3 --kernel-trace --output-format csv -d $R/gpurun_out/${TAG}_placement_trace -o run -- \
+        python3 $R/tools/placement_ab.py --reps 4 --rotate-order --kernels pair \
+        --modes-pair plain,group,c:0,call:0,call:4 \
+        > $R/gpurun_out/${TAG}_placement_ab.jsonl 2> $R/gpurun_out/${TAG}_placement_ab.err &&
+    cd $R &&
+    python3 tools/placement_ab_trace.py gpurun_out/${TAG}_placement_ab.jsonl gpurun_out/${TAG}_placement_trace \
+        > gpurun_out/${TAG}_placement_ab_trace.jsonl
     ;;
 p)
     # the N > 1 code path at world size 1 over RCCL with the full exchange (--force-dist, diagnostics on: the

@@ -12,6 +12,8 @@ second (the driver clears freed VRAM in the background), launches `warmup` untim
   any kernel: s:i.j.k...  bucket j (allocation order: pair a, b; scan 8 inputs then 8 outputs; tree 8 inputs then
             the output) at 4 KiB slot list[j] of a plain hipMalloc 64 KiB larger, every set alike;
             s:i.j.k...@K  the same with set s's slots moved by K x s (mod 16)
+  pair only: c:K    each set's a and b carved from one allocation at stride bucket + K KiB
+             call:K every set's a and b carved from ONE allocation (8 GiB) at stride bucket + K KiB
   scan  (C3 scan, bench.py c3_single: 8 sets of 8 inputs ALL allocated first, then all 8 x 8 outputs, 64 MiB f32)
         plain / rotating as above; group: Bucket.group(16) per set (inputs slots 0-7, outputs 8-15)
   tree  (bench.py c4_single: 8 inputs then the output, 1 GiB f32 each, one set)
@@ -97,12 +99,27 @@ def timed(launch, warmup, steps):
 def pair(mode, warmup, steps):
     n, S = 256 * MIB // 4, 16
     sets, owners = [], []
+    if mode.startswith("call:"):  # every set's a and b carved from ONE allocation at stride bucket + K KiB
+        fmi_amd.tune_set(Tune.ALLOC_SLOTS, 0)
+        stride = n + int(mode[5:]) * 1024 // 4
+        owner = Bucket(stride * 2 * S, np.float32)
+        owners = [owner]
+        views = [owner.view(j * stride, n) for j in range(2 * S)]
     for s in range(S):  # bench.py run_single: a then b, set after set
-        (a, b), own = alloc(mode, 2, n, slot=s if slot_mode(mode) else 1 + s % 15)
+        if mode.startswith("call:"):
+            a, b = views[2 * s], views[2 * s + 1]
+        elif mode.startswith("c:"):  # the set's a and b carved from one allocation at stride bucket + K KiB
+            fmi_amd.tune_set(Tune.ALLOC_SLOTS, 0)
+            stride = n + int(mode[2:]) * 1024 // 4
+            o = Bucket(stride + n, np.float32)
+            a, b = o.view(0, n), o.view(stride, n)
+            owners.append(o)
+        else:
+            (a, b), own = alloc(mode, 2, n, slot=s if slot_mode(mode) else 1 + s % 15)
+            owners += own
         a.fill_synthetic(42 + s, 0)
         b.fill_synthetic(42 + s, 1)
         sets.append((a, b))
-        owners += own
     slots = sorted({(x.ptr % (64 * 1024)) // SLOT for st in sets for x in st})
     used = [0] * S
 
