@@ -1429,7 +1429,7 @@ size_t shard_elems(size_t n, int ranks) {
 // Where the all-to-all lands the N shards the fused shard kernel then streams together. Back to
 // back at `bytes` (a multiple of 64 KiB for the headline's buckets), all N streams sit at one offset modulo HBM's
 // 64 KiB interleave and collide, as DESIGN §4 measured for buckets; at a stride of bytes rounded up to 64 KiB plus
-// 4 KiB, shard j sits in 4 KiB slot j mod 16 and the reduced shard (shard_out) in slot N mod 16. The fused 8-way kernel
+// 4 KiB, shard j sits in 4 KiB slot j mod 16 and the reduced shard in slot N mod 16 of the same range. The fused 8-way kernel
 // at the N = 8 shard shape (32 MiB): 0.738 packed, 0.790 skewed; N = 4: 0.741 / 0.764; N = 2: 0.784 / 0.806
 // (profiles/r06a_shard_layout.jsonl, tools/shard_layout_ab.py). Taken where the transport posts a receive per peer
 // anyway (receives_per_peer) and FMI_TUNE_COMM_SHARD_SKEW is on; shards under 1 MiB stay back to back.
@@ -1663,15 +1663,20 @@ int allreduce_device(Comm* c, int op, int dtype, int alg, int path, const void* 
     }
     const char* src = nullptr;
     FMI_COMM_RC(padded_source(c, n, padded, esz, send, s, &src));
-    // the shard kernel's inputs each in their own 4 KiB slot, and its output in the next (shard_stride)
+    // skewed (shard_stride): the shard kernel's N inputs and its output carved from one scratch range, each in its
+    // own 4 KiB slot (a carved group); otherwise the inputs back to back and the output apart
     const size_t stride = path != FMI_PATH_RCCL && !per_rank ? shard_stride(*c->t, shard * esz) : shard * esz;
-    const size_t red_at = stride != shard * esz ? (static_cast<size_t>(N) % 16) * kShardSlot : 0;
+    const bool skewed = stride != shard * esz;
     char* red = nullptr;
-    FMI_COMM_RC(c->scratch(2, (per_rank ? padded : shard) * esz + (red_at ? kShardSpan : 0), s, &red));
-    red += red_at;
+    char* staging = nullptr;
+    if (skewed) {
+        FMI_COMM_RC(c->scratch(1, (static_cast<size_t>(N) + 1) * stride, s, &staging));
+        red = staging + static_cast<size_t>(N) * stride;
+    } else {
+        FMI_COMM_RC(c->scratch(2, (per_rank ? padded : shard) * esz, s, &red));
+    }
     if (path != FMI_PATH_RCCL) {
-        char* staging = nullptr;
-        FMI_COMM_RC(c->scratch(1, static_cast<size_t>(N) * stride, s, &staging));
+        if (!skewed) FMI_COMM_RC(c->scratch(1, padded * esz, s, &staging));
         FMI_COMM_RC(c->t->all_to_all_strided(src, staging, shard * esz, stride, s));
         std::vector<const void*> parts(N);
         for (int j = 0; j < N; ++j) parts[j] = staging + j * stride;

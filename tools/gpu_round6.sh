@@ -12,7 +12,9 @@
 #                                with 8 LOCAL ranks, skew on / off (TAG=r06d)
 #   bash tools/gpu_round6.sh f   carved groups: their GPU tests, placement round four (group vs rotating vs the same
 #                                slots as separate allocations), the default line (TAG=r06f)
-#   bash tools/gpu_round6.sh g   the pair's buckets: plain, carved group, per-set carve, one 8 GiB carve (TAG=r06g)
+#   bash tools/gpu_round6.sh g   the pair's buckets: plain, carved group, per-set carve, one 8 GiB carve; then the
+#                                shard kernel's output carved into the staging range: its tests and the layout A/B
+#                                (TAG=r06g)
 #   bash tools/gpu_round6.sh p   bench.py --force-dist at world 1 over RCCL, diagnostics and C5 at 1 GiB (TAG=r06p)
 #   bash tools/gpu_round6.sh q   the N > 1 line at full size, 8 PROC ranks on one GPU (TAG=r06q)
 #   bash tools/gpu_round6.sh z   the round-end sequence: GPU suite, smoke(), default line, C2 profile (TAG=r06z...)
@@ -112,7 +114,11 @@ g)
         > $R/gpurun_out/${TAG}_placement_ab.jsonl 2> $R/gpurun_out/${TAG}_placement_ab.err &&
     cd $R &&
     python3 tools/placement_ab_trace.py gpurun_out/${TAG}_placement_ab.jsonl gpurun_out/${TAG}_placement_trace \
-        > gpurun_out/${TAG}_placement_ab_trace.jsonl
+        > gpurun_out/${TAG}_placement_ab_trace.jsonl &&
+    timeout -k 10 300 python -u -m pytest -x -v --timeout 300 --timeout-method thread -p no:cacheprovider \
+        tests/test_gpu_comm.py -k "skewed or c4_8peer or c5_host" tests/test_gpu_proc.py > gpurun_out/${TAG}_tests.log 2>&1 &&
+    timeout -k 10 300 python -u tools/shard_layout_ab.py --reps 3 > gpurun_out/${TAG}_shard_layout.jsonl \
+        2> gpurun_out/${TAG}_shard_layout.err
     ;;
 p)
     # the N > 1 code path at world size 1 over RCCL with the full exchange (--force-dist, diagnostics on: the

@@ -3,8 +3,9 @@
 fmi_comm_allreduce (path TREE) receives the N shards of a 256 MiB bucket into one plain hipMalloc (Comm::scratch), back
 to back at stride `shard` (a multiple of 64 KiB), and its fused kernel (tree_kernel, allreduce_no_order order) streams
 all N at the same offset, plus the reduced shard into another plain hipMalloc. This tool runs that kernel on exactly
-that layout ("packed") and on the layout a receive stride of shard + 4 KiB would give ("skewed": shard j at
-j x (shard + 4 KiB), the output in the next 4 KiB slot), one kernel at a time as on each GPU of an N-GPU node,
+that layout ("packed") and on the product's skewed layout (fmi_comm.hip shard_stride: shard j at j x (shard + 4 KiB),
+the output at N x (shard + 4 KiB) of the same range; round 6's first run, profiles/r06a_shard_layout.jsonl, had the
+output in a separate allocation), one kernel at a time as on each GPU of an N-GPU node,
 rotating over 8 staging sets (no MALL re-use), interleaved `--reps` times. Every launch's result window is checked
 against numpy's evaluation of rank 0's bracketing.
 
@@ -31,18 +32,22 @@ SLOT = 4096
 
 def run(N, layout, launches, sets=8):
     shard = 256 * MIB // 4 // N  # elements (a multiple of 64 KiB for N = 2, 4, 8)
-    skew = SLOT // 4 if layout == "skewed" else 0
-    stride = shard + skew
+    stride = shard
     fmi_amd.tune_set(Tune.ALLOC_SLOTS, 0)  # Comm::scratch is a plain hipMalloc
     st = []
     for s in range(sets):
-        staging = Bucket(N * stride, np.float32)
+        if layout == "skewed":  # the product's layout (fmi_comm.hip shard_stride): inputs and output in one range
+            stride = (shard * 4 + 65535) // 65536 * 65536 // 4 + SLOT // 4
+            staging = Bucket((N + 1) * stride, np.float32)
+            red_owner, red = staging, staging.view(N * stride, shard)
+        else:
+            staging = Bucket(N * stride, np.float32)
+            red_owner = Bucket(shard, np.float32)
+            red = red_owner
         parts = [staging.view(j * stride, shard) for j in range(N)]
         for j, p in enumerate(parts):
             p.fill_synthetic(100 + s, j)
-        red_owner = Bucket(shard + 16 * SLOT // 4, np.float32)
-        red = red_owner.view((N % 16) * skew, shard)
-        st.append((staging, parts, red_owner, red))
+        st.append((staging, parts, red_owner if red_owner is not staging else None, red))
     fmi_amd.sync()
     time.sleep(1.0)
     for i in range(sets):
@@ -62,7 +67,8 @@ def run(N, layout, launches, sets=8):
         bad += int(np.count_nonzero(red.view(0, 1 << 14).numpy().view(np.uint32) != want.view(np.uint32)))
     for staging, _, red_owner, _ in st:
         staging.free()
-        red_owner.free()
+        if red_owner is not None:
+            red_owner.free()
     return {"ranks": N, "layout": layout, "shard_mib": shard * 4 // MIB, "us": round(us, 2),
             "frac": round((N + 1) * shard * 4 / (us * 1e-6) / PEAK, 4), "mismatches": bad}
 
