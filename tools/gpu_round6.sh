@@ -17,6 +17,7 @@
 #                                (TAG=r06g)
 #   bash tools/gpu_round6.sh p   bench.py --force-dist at world 1 over RCCL, diagnostics and C5 at 1 GiB (TAG=r06p)
 #   bash tools/gpu_round6.sh q   the N > 1 line at full size, 8 PROC ranks on one GPU (TAG=r06q)
+#   bash tools/gpu_round6.sh s   soaks: the P-way and communicator random sweeps at fresh seeds
 #   bash tools/gpu_round6.sh z   the round-end sequence: GPU suite, smoke(), default line, C2 profile (TAG=r06z...)
 set -o pipefail
 cd /root/repo
@@ -134,6 +135,14 @@ q)
     FMI_PROC_TIMEOUT_S=300 timeout -k 10 1000 python -m torch.distributed.run --nnodes=1 --nproc-per-node=8 \
         --master-addr 127.0.0.1 --master-port 29644 bench.py --gpus 8 --transport proc --steps 20 --warmup 3 \
         --diag-deadline 600 > gpurun_out/${TAG}_bench_proc8_rehearsal.json 2> gpurun_out/${TAG}_bench_proc8_rehearsal.err
+    ;;
+s)
+    # soaks on the final library (placement changed: plain allocations by default, carved groups, skewed shards):
+    # the P-way sweep and the communicator sweep at fresh seeds, every case bit-exact against the oracle
+    FMI_SWEEP_SEEDS=70000:70400 timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread \
+        -p no:cacheprovider tests/test_gpu_random_sweep.py > gpurun_out/r06_random_sweep_soak_70000_70400.log 2>&1 &&
+    FMI_SWEEP_SEEDS=80000:80600 timeout -k 10 800 python -u -m pytest -x -q --timeout 300 --timeout-method thread \
+        -p no:cacheprovider tests/test_gpu_comm_random_sweep.py > gpurun_out/r06_comm_sweep_soak_80000_80600.log 2>&1
     ;;
 z)
     # the round-end sequence on the current library and bench: the whole GPU suite, smoke(), the default line, then
