@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <cstddef>
 #include <cstdint>
+#include <limits>
 #include <stdexcept>
 #include <string>
 #include <type_traits>
@@ -76,6 +77,8 @@ public:
     //! `count` buckets of n elements that one kernel streams together (a peer set's inputs and outputs): bucket j
     //! in 4 KiB slot j mod 16 whatever was allocated before (fmi_dev_alloc_group).
     static std::vector<Bucket> group(std::size_t count, std::size_t n) {
+        if (count > static_cast<std::size_t>(std::numeric_limits<int>::max()))
+            throw std::runtime_error("Bucket::group: too many buckets");
         std::vector<void*> ptrs(count);
         check(fmi_dev_alloc_group(ptrs.data(), static_cast<int>(count), n * sizeof(A)), "fmi_dev_alloc_group");
         std::vector<Bucket> out(count);

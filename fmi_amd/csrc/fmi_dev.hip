@@ -1020,9 +1020,11 @@ int fmi_dev_alloc_group(void** ptrs, int count, size_t bytes) {
     // One allocation for the whole group, bucket j at j x stride: each bucket in its own 4 KiB slot (stride = the
     // bucket rounded up to 64 KiB, plus 4 KiB), and the group's memory one range (see the placement note above).
     const size_t n = static_cast<size_t>(count);
-    if (bytes > (SIZE_MAX - kSlotSpan) / (n + 1)) return fail(FMI_ERR_INVALID, "group too large");
+    if (bytes > SIZE_MAX - 2 * kSlotSpan) return fail(FMI_ERR_INVALID, "group too large");
     const size_t stride = (bytes + kSlotSpan - 1) / kSlotSpan * kSlotSpan + kSlotBytes;
-    const size_t total = (n - 1) * stride + bytes + kSlotSpan;  // + room to start the range on a 64 KiB boundary
+    size_t total = 0;  // the buckets, plus room to start the range on a 64 KiB boundary
+    if (__builtin_mul_overflow(n - 1, stride, &total) || __builtin_add_overflow(total, bytes + kSlotSpan, &total))
+        return fail(FMI_ERR_INVALID, "group too large");
     void* base = nullptr;
     const hipError_t e = hipMalloc(&base, total);
     if (e != hipSuccess) {

@@ -1083,6 +1083,8 @@ def test_dev_alloc_group_places_each_bucket_by_its_index(device):
     assert Bucket.group(0, n, np.float32) == []
     with pytest.raises(fmi_amd.FmiError, match="group of 3 buckets"):
         Bucket.group(3, 1 << 46, np.uint8)  # 64 TiB each: the group's one allocation fails
+    with pytest.raises(fmi_amd.FmiError, match="group too large"):
+        Bucket.group(1 << 20, 1 << 45, np.uint8)  # its size does not fit in 64 bits
     a, b = Bucket.from_numpy(np.ones(4099, np.float32)), Bucket.from_numpy(np.ones(4099, np.float32))
     fmi_amd.reduce_pair(Op.SUM, a, b)  # the failed allocation left no error behind for the next launch to find
     assert np.array_equal(a.numpy(), np.full(4099, 2, np.float32))
