@@ -134,9 +134,10 @@ i)
     timeout -k 10 200 build/mbpciepeers 3 0 1 > gpurun_out/r05_pcie_busy.jsonl 2> gpurun_out/r05_pcie_busy.err
     ;;
 j)
-    # the host pipeline depth of the library (2, or 3 for co-resident LOCAL ranks) vs always 2 (build/ab_d2, make -C
-    # fmi_amd/csrc ab_depth2; first run: the library at 3 for every communicator), separate processes,
-    # interleaved three times: C5's p1_copy and local_peers blocks
+    # the host pipeline depth of the library (2, or 3 for co-resident LOCAL ranks) vs always 2 (build/ab_d2, made by
+    # round 5's `ab_depth2` Makefile target, removed with its compile-time hook in round 6: this step is history;
+    # first run: the library at 3 for every communicator), separate processes, interleaved three times: C5's
+    # p1_copy and local_peers blocks
     for k in 1 2 3; do
         for lib in fmi_amd/lib/libfmi_dev.so build/ab_d2/libfmi_dev.so; do
             FMI_DEV_LIB=$PWD/$lib timeout -k 10 200 python -u -c "
