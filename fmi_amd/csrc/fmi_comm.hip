@@ -1193,7 +1193,7 @@ struct HostPipe {
 
     int init(Transport& t) {
         if (ready) return FMI_OK;
-        if (!h2d) {
+        if (!h2d || !d2h) {  // (a failed creation is retried on the next call)
             if (t.co_resident()) {
                 FMI_COMM_RC(t.copy_streams(&h2d, &d2h));
             } else {
