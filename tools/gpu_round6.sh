@@ -18,6 +18,7 @@
 #   bash tools/gpu_round6.sh p   bench.py --force-dist at world 1 over RCCL, diagnostics and C5 at 1 GiB (TAG=r06p)
 #   bash tools/gpu_round6.sh q   the N > 1 line at full size, 8 PROC ranks on one GPU (TAG=r06q)
 #   bash tools/gpu_round6.sh s   soaks: the P-way and communicator random sweeps at fresh seeds
+#   bash tools/gpu_round6.sh cold  C2 as the first work of a fresh box, twice, then after a 60 s pause (TAG=r06k)
 #   bash tools/gpu_round6.sh z   the round-end sequence: GPU suite, smoke(), default line, C2 profile (TAG=r06z...)
 set -o pipefail
 cd /root/repo
@@ -143,6 +144,14 @@ s)
         -p no:cacheprovider tests/test_gpu_random_sweep.py > gpurun_out/r06_random_sweep_soak_70000_70400.log 2>&1 &&
     FMI_SWEEP_SEEDS=80000:80600 timeout -k 10 800 python -u -m pytest -x -q --timeout 300 --timeout-method thread \
         -p no:cacheprovider tests/test_gpu_comm_random_sweep.py > gpurun_out/r06_comm_sweep_soak_80000_80600.log 2>&1
+    ;;
+cold)
+    # is C2 slower as the first work of a fresh box (the driver's bench runs so)? The line twice, back to back, as
+    # the first GPU work of the call, then once more after a 60 s idle pause
+    timeout -k 10 300 python bench.py --no-c5 --no-cpu-baseline > gpurun_out/${TAG}_cold1.json 2> gpurun_out/${TAG}_cold1.err &&
+    timeout -k 10 300 python bench.py --no-c5 --no-cpu-baseline > gpurun_out/${TAG}_cold2.json 2> gpurun_out/${TAG}_cold2.err &&
+    sleep 60 &&
+    timeout -k 10 300 python bench.py --no-c5 --no-cpu-baseline > gpurun_out/${TAG}_cold3.json 2> gpurun_out/${TAG}_cold3.err
     ;;
 z)
     # the round-end sequence on the current library and bench: the whole GPU suite, smoke(), the default line, then
