@@ -18,6 +18,7 @@
 #   bash tools/gpu_round6.sh p   bench.py --force-dist at world 1 over RCCL, diagnostics and C5 at 1 GiB (TAG=r06p)
 #   bash tools/gpu_round6.sh q   the N > 1 line at full size, 8 PROC ranks on one GPU (TAG=r06q)
 #   bash tools/gpu_round6.sh s   soaks: the P-way and communicator random sweeps at fresh seeds
+#   bash tools/gpu_round6.sh h   the device copy by placement (TAG=r06h)
 #   bash tools/gpu_round6.sh cold  C2 as the first work of a fresh box, twice, then after a 60 s pause (TAG=r06k)
 #   bash tools/gpu_round6.sh z   the round-end sequence: GPU suite, smoke(), default line, C2 profile (TAG=r06z...)
 set -o pipefail
@@ -144,6 +145,17 @@ s)
         -p no:cacheprovider tests/test_gpu_random_sweep.py > gpurun_out/r06_random_sweep_soak_70000_70400.log 2>&1 &&
     FMI_SWEEP_SEEDS=80000:80600 timeout -k 10 800 python -u -m pytest -x -q --timeout 300 --timeout-method thread \
         -p no:cacheprovider tests/test_gpu_comm_random_sweep.py > gpurun_out/r06_comm_sweep_soak_80000_80600.log 2>&1
+    ;;
+h)
+    # the device copy (the P = 1 allreduce, 1 in : 1 out) by placement: plain, carved group (dst in slot 1), carved
+    # at + 0; 4 reps rotated, under a trace
+    cd /tmp &&
+    timeout -k 10 600 rocprofv3 --kernel-trace --output-format csv -d $R/gpurun_out/${TAG}_placement_trace -o run -- \
+        python3 $R/tools/placement_ab.py --reps 4 --rotate-order --kernels copy --steps 40 \
+        > $R/gpurun_out/${TAG}_placement_ab.jsonl 2> $R/gpurun_out/${TAG}_placement_ab.err &&
+    cd $R &&
+    python3 tools/placement_ab_trace.py gpurun_out/${TAG}_placement_ab.jsonl gpurun_out/${TAG}_placement_trace \
+        > gpurun_out/${TAG}_placement_ab_trace.jsonl
     ;;
 cold)
     # is C2 slower as the first work of a fresh box (the driver's bench runs so)? The line twice, back to back, as

@@ -141,6 +141,30 @@ def pair(mode, warmup, steps):
             "slots_mod_64k": slots}
 
 
+def copy(mode, warmup, steps):
+    """the P = 1 allreduce's device copy (copy_tile<1>, bench.py allreduce_1peer's shape): 8 sets of (src, dst),
+    256 MiB each"""
+    n, S = 256 * MIB // 4, 8
+    sets, owners = [], []
+    for s in range(S):
+        if mode.startswith("c:"):
+            fmi_amd.tune_set(Tune.ALLOC_SLOTS, 0)
+            stride = n + int(mode[2:]) * 1024 // 4
+            o = Bucket(stride + n, np.float32)
+            a, b = o.view(0, n), o.view(stride, n)
+            owners.append(o)
+        else:
+            (a, b), own = alloc(mode, 2, n, slot=s if slot_mode(mode) else 1 + s % 15)
+            owners += own
+        a.fill_synthetic(3 + s, 0)
+        sets.append((a, b))
+    us = timed(lambda k: sets[k % S][1].copy_from(sets[k % S][0]), warmup, steps)
+    bad = sum(int(np.count_nonzero(a.view(0, 1 << 14).numpy() != b.view(0, 1 << 14).numpy())) for a, b in sets)
+    for o in owners:
+        o.free()
+    return {"us": round(us, 2), "frac": round(2 * n * 4 / (us * 1e-6) / PEAK, 4), "mismatches": bad}
+
+
 def scan(mode, warmup, steps):
     n, P, S = 64 * MIB // 4, 8, 8
     owners = []
@@ -199,7 +223,8 @@ def tree(mode, warmup, steps):
 
 KERNELS = {"pair": (pair, "plain,rotating,group,same_slot", "pair_tile<fmi::dev::OpSum, float, 4, 3>"),
            "scan": (scan, "plain,rotating,group", "scan_kernel<fmi::dev::OpSum, float, 3, 8>"),
-           "tree": (tree, "plain,rotating,group", "tree_kernel<fmi::dev::OpSum, float, 0, 8, false>")}
+           "tree": (tree, "plain,rotating,group", "tree_kernel<fmi::dev::OpSum, float, 0, 8, false>"),
+           "copy": (copy, "plain,group,c:0", "copy_tile<1>")}
 
 
 def main() -> None:

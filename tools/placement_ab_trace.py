@@ -16,7 +16,7 @@ import statistics
 import sys
 
 PEAK = 8e12
-BYTES = {"pair": 3 * 256 << 20, "scan": 16 * 64 << 20, "tree": 9 * 1024 << 20}
+BYTES = {"pair": 3 * 256 << 20, "scan": 16 * 64 << 20, "tree": 9 * 1024 << 20, "copy": 2 * 256 << 20}
 
 
 def main(lines_path: str, trace_dir: str) -> None:
