@@ -318,21 +318,26 @@ def local_equivalent(world: int, n: int, launches: int = 10, sets: int = 2) -> d
     from . import device as fdev
 
     N = world
-    ins = [[fdev.Bucket(n, np.float32).fill_synthetic(42 + s, p) for p in range(N)] for s in range(sets)]
-    out = fdev.Bucket(n, np.float32)
-    for s in range(sets):
-        fdev.reduce_tree(Op.SUM, Alg.ALLREDUCE, out, ins[s])
+    # each set's N inputs and its output one carved group (fmi_dev_alloc_group): the placement the
+    # library gives the buckets a fused kernel streams together
+    groups = [fdev.Bucket.group(N + 1, n, np.float32) for _ in range(sets)]
+    for s, g in enumerate(groups):
+        for p in range(N):
+            g[p].fill_synthetic(42 + s, p)
+    for g in groups:
+        fdev.reduce_tree(Op.SUM, Alg.ALLREDUCE, g[N], g[:N])
     fdev.sync()
     e0, e1 = fdev.Event(), fdev.Event()
     e0.record()
     for k in range(launches):
-        fdev.reduce_tree(Op.SUM, Alg.ALLREDUCE, out, ins[k % sets])
+        g = groups[k % sets]
+        fdev.reduce_tree(Op.SUM, Alg.ALLREDUCE, g[N], g[:N])
     e1.record()
     e1.sync()
     ms = e0.elapsed_ms(e1) / launches
     e0.destroy()
     e1.destroy()
-    for b in [out] + [x for s in ins for x in s]:
+    for b in [x for g in groups for x in g]:
         b.free()
     S = n * 4
     return {"workload": f"{N} peers x {S >> 20} MiB f32 sum-allreduce on ONE GPU (fused {N}-way kernel, "
