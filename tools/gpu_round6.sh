@@ -19,6 +19,7 @@
 #   bash tools/gpu_round6.sh q   the N > 1 line at full size, 8 PROC ranks on one GPU (TAG=r06q)
 #   bash tools/gpu_round6.sh s   soaks: the P-way and communicator random sweeps at fresh seeds
 #   bash tools/gpu_round6.sh h   the device copy by placement (TAG=r06h)
+#   bash tools/gpu_round6.sh t   the N > 1 line's GPU tests (TAG=r06t)
 #   bash tools/gpu_round6.sh cold  C2 as the first work of a fresh box, twice, then after a 60 s pause (TAG=r06k)
 #   bash tools/gpu_round6.sh z   the round-end sequence: GPU suite, smoke(), default line, C2 profile (TAG=r06z...)
 set -o pipefail
@@ -156,6 +157,11 @@ h)
     cd $R &&
     python3 tools/placement_ab_trace.py gpurun_out/${TAG}_placement_ab.jsonl gpurun_out/${TAG}_placement_trace \
         > gpurun_out/${TAG}_placement_ab_trace.jsonl
+    ;;
+t)
+    # the N > 1 line's GPU tests after a change to its one-GPU anchor (local_equivalent on carved groups)
+    timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread -p no:cacheprovider \
+        tests/test_gpu_bench_dist.py > gpurun_out/${TAG}_bench_dist_tests.log 2>&1
     ;;
 cold)
     # is C2 slower as the first work of a fresh box (the driver's bench runs so)? The line twice, back to back, as
