@@ -20,6 +20,8 @@
 #   bash tools/gpu_round6.sh s   soaks: the P-way and communicator random sweeps at fresh seeds
 #   bash tools/gpu_round6.sh h   the device copy by placement (TAG=r06h)
 #   bash tools/gpu_round6.sh t   the N > 1 line's GPU tests (TAG=r06t)
+#   bash tools/gpu_round6.sh l   the LOCAL exchange ordered on the streams: its suites, then C5's co-resident block
+#                                async / synchronised (TAG=r06l)
 #   bash tools/gpu_round6.sh cold  C2 as the first work of a fresh box, twice, then after a 60 s pause (TAG=r06k)
 #   bash tools/gpu_round6.sh z   the round-end sequence: GPU suite, smoke(), default line, C2 profile (TAG=r06z...)
 set -o pipefail
@@ -162,6 +164,17 @@ t)
     # the N > 1 line's GPU tests after a change to its one-GPU anchor (local_equivalent on carved groups)
     timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread -p no:cacheprovider \
         tests/test_gpu_bench_dist.py > gpurun_out/${TAG}_bench_dist_tests.log 2>&1
+    ;;
+l)
+    # the LOCAL transport's exchange ordered on the streams (FMI_TUNE_COMM_LOCAL_ASYNC, default 1): the communicator,
+    # PROC, timeout and host suites on it; then C5's co-resident block, async / host-synchronised, interleaved 3x
+    timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider \
+        tests/test_gpu_comm.py tests/test_gpu_timeout.py tests/test_gpu_comm_random_sweep.py tests/test_gpu_fmi_python.py \
+        > gpurun_out/${TAG}_tests.log 2>&1 &&
+    timeout -k 10 300 python -u -m pytest -x -q --timeout 240 --timeout-method thread -p no:cacheprovider \
+        tests/test_cpp_communicator.py -m gpu >> gpurun_out/${TAG}_tests.log 2>&1 &&
+    timeout -k 10 600 python -u tools/local_async_ab.py --reps 3 > gpurun_out/${TAG}_local_async_ab.jsonl \
+        2> gpurun_out/${TAG}_local_async_ab.err
     ;;
 cold)
     # is C2 slower as the first work of a fresh box (the driver's bench runs so)? The line twice, back to back, as
