@@ -46,7 +46,6 @@ namespace {
 constexpr size_t kShardAlign = 64;  // elements: shards stay 256-B aligned for the 16-B vector kernels
 
 int hip_err(const char* what, hipError_t e) { return fail(FMI_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e)); }
-int hip_ok(hipError_t e, const char* what) { return e == hipSuccess ? FMI_OK : hip_err(what, e); }
 
 long long tune(int key) {
     long long v = 0;
@@ -615,22 +614,16 @@ private:
 
 // Ranks of one process on one device: a rendezvous hub per communicator id.
 struct Hub {
-    explicit Hub(int n) : n(n), ready(n, nullptr), done(n, nullptr), ptrs(n, nullptr) {}
+    explicit Hub(int n) : n(n), ptrs(n, nullptr) {}
     ~Hub() {
         // A poisoned hub's ranks may have left copies queued that never drain: leak the streams then.
         if (poisoned) return;
         for (hipStream_t st : {h2d, d2h})
             if (st) (void)hipStreamDestroy(st);
-        for (auto* evs : {&ready, &done})
-            for (hipEvent_t ev : *evs)
-                if (ev) (void)hipEventDestroy(ev);
     }
     int n;
     // The host pipelines' copy streams, shared by this communicator's ranks only (LocalTransport::copy_streams).
     hipStream_t h2d = nullptr, d2h = nullptr;
-    // Stream-ordered exchanges (LocalTransport::exchange, FMI_TUNE_COMM_LOCAL_ASYNC): rank r's "my send data is
-    // ready" and "my reads of the peers' data are done" events, each created and recorded by rank r only.
-    std::vector<hipEvent_t> ready, done;
     std::mutex mu;
     std::condition_variable cv;
     int arrived = 0;
@@ -848,7 +841,6 @@ private:
     // Publish my buffer, wait for everyone, run `work` over all ranks' buffers, wait until everyone's
     // copies have completed (so no rank reuses a published buffer while another still reads it).
     int exchange(const char* mine, hipStream_t s, const std::function<int(const std::vector<const char*>&)>& work) {
-        if (tune(FMI_TUNE_COMM_LOCAL_ASYNC)) return exchange_async(mine, s, work);
         FMI_COMM_HIP(hipStreamSynchronize(s));
         {
             std::lock_guard<std::mutex> lk(hub_->mu);
@@ -864,52 +856,6 @@ private:
         const hipError_t e = hipStreamSynchronize(s);
         if (!hub_->barrier(deadline())) return timed_out("local transport exchange (consumed)");
         if (rc == FMI_OK && e != hipSuccess) rc = hip_err("local transport exchange", e);
-        return rc;
-    }
-
-    // The same exchange ordered on the streams instead of the host: each rank records "ready" after the work that
-    // produced its published buffer, every rank's copies wait for all "ready" events, and each rank's stream then
-    // waits for every rank's "done" (its peers' reads of its buffer) before anything later may overwrite or free
-    // that buffer. The host still meets the peers twice (to trade pointers and to know every "done" is recorded:
-    // an event is waited for only after its record was queued, so a shared stream cannot deadlock), but it never
-    // waits for the device, so a rank's next work is queued while this exchange's copies still run.
-    int exchange_async(const char* mine, hipStream_t s,
-                       const std::function<int(const std::vector<const char*>&)>& work) {
-        for (hipEvent_t* ev : {&hub_->ready[rank_], &hub_->done[rank_]})  // this rank's own slots: no lock needed
-            if (!*ev) FMI_COMM_HIP(hipEventCreateWithFlags(ev, hipEventDisableTiming));
-        FMI_COMM_HIP(hipEventRecord(hub_->ready[rank_], s));
-        {
-            std::lock_guard<std::mutex> lk(hub_->mu);
-            hub_->ptrs[rank_] = mine;
-        }
-        if (!hub_->barrier(deadline())) return timed_out("local transport exchange (published)");
-        std::vector<const char*> all;
-        std::vector<hipEvent_t> ready;
-        {
-            std::lock_guard<std::mutex> lk(hub_->mu);
-            all = hub_->ptrs;
-            ready = hub_->ready;
-        }
-        int rc = FMI_OK;
-        for (int j = 0; j < n_ && rc == FMI_OK; ++j)
-            if (j != rank_) rc = hip_ok(hipStreamWaitEvent(s, ready[j], 0), "hipStreamWaitEvent (a peer's data)");
-        if (rc == FMI_OK) rc = work(all);
-        const hipError_t e = hipEventRecord(hub_->done[rank_], s);
-        if (!hub_->barrier(deadline())) {
-            (void)hipStreamSynchronize(s);  // this rank's reads of the peers' buffers, at least, have finished
-            return timed_out("local transport exchange (consumed)");
-        }
-        if (rc == FMI_OK && e != hipSuccess) rc = hip_err("local transport exchange", e);
-        std::vector<hipEvent_t> done;
-        {
-            std::lock_guard<std::mutex> lk(hub_->mu);
-            done = hub_->done;
-        }
-        for (int j = 0; j < n_; ++j)
-            if (j != rank_) {
-                const int w = hip_ok(hipStreamWaitEvent(s, done[j], 0), "hipStreamWaitEvent (a peer's reads)");
-                if (rc == FMI_OK) rc = w;
-            }
         return rc;
     }
 

@@ -145,7 +145,7 @@ size_t host_pipe_count(size_t* idle, size_t* staging_bytes) {
 
 // Defaults from tools/tune_pair.py on MI355X (C2, 256 MiB f32): nontemporal one-shot tiles, 4 × 16 B per
 // operand per thread, 256-thread workgroups — 125 µs = 6.4 TB/s vs 142 µs for plain loads/stores.
-std::atomic<long long> g_tune[17] = {2 /*variant: nontemporal tiles*/, 4 /*unroll*/, 256 /*block*/,
+std::atomic<long long> g_tune[16] = {2 /*variant: nontemporal tiles*/, 4 /*unroll*/, 256 /*block*/,
                                      8 /*grid per CU*/, 64ll << 20 /*host chunk*/, 1 /*host zero-copy*/,
                                      64 /*fused in-flight KiB per CU (tools/ab_fused_cap.py)*/,
                                      1 /*one-pass blocked scan*/, 0 /*ncclAllToAll*/, 0 /*ncclAllGather*/,
@@ -153,8 +153,7 @@ std::atomic<long long> g_tune[17] = {2 /*variant: nontemporal tiles*/, 4 /*unrol
                                      1 /*pairwise: tiles t % 8 < 1 (one XCD) store sc1 (tools/ab_pair_sc1.py)*/,
                                      0 /*one-rank communicators copy*/,
                                      0 /*plain allocations; groups take slots (profiles/r06a_placement_ab.jsonl)*/,
-                                     1 /*shard kernel inputs in their own 4 KiB slots (profiles/r06a_shard_layout.jsonl)*/,
-                                     1 /*LOCAL exchanges ordered on the streams*/};
+                                     1 /*shard kernel inputs in their own 4 KiB slots (profiles/r06a_shard_layout.jsonl)*/};
 
 int hip_fail(const char* what, hipError_t e) {
     return fail(FMI_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
@@ -1571,9 +1570,6 @@ int fmi_tune_set(int key, long long value) {
         case FMI_TUNE_COMM_SHARD_SKEW:
             if (value != 0 && value != 1) return fail(FMI_ERR_INVALID, "shard skew must be 0 or 1");
             break;
-        case FMI_TUNE_COMM_LOCAL_ASYNC:
-            if (value != 0 && value != 1) return fail(FMI_ERR_INVALID, "local async exchange must be 0 or 1");
-            break;
         default: return fail(FMI_ERR_INVALID, "unknown tuning key");
     }
     g_tune[key].store(value);
@@ -1581,7 +1577,7 @@ int fmi_tune_set(int key, long long value) {
 }
 
 int fmi_tune_get(int key, long long* value) {
-    if (!value || key < 0 || key > FMI_TUNE_COMM_LOCAL_ASYNC) return fail(FMI_ERR_INVALID, "bad tuning query");
+    if (!value || key < 0 || key > FMI_TUNE_COMM_SHARD_SKEW) return fail(FMI_ERR_INVALID, "bad tuning query");
     *value = g_tune[key].load();
     return FMI_OK;
 }

@@ -65,7 +65,6 @@ class Tune(enum.IntEnum):
     COMM_ONE_RANK_EXCHANGE = 13
     ALLOC_SLOTS = 14
     COMM_SHARD_SKEW = 15
-    COMM_LOCAL_ASYNC = 16
 
 
 NP_DTYPE = {DType.F32: np.float32, DType.F64: np.float64, DType.I32: np.int32, DType.I64: np.int64,

@@ -414,12 +414,7 @@ typedef enum {
                                     where the transport posts a receive per peer anyway (LOCAL, PROC, RCCL's grouped
                                     form, FMI_TUNE_COMM_A2A set to 1; never ncclAllToAll); 0 = back to back. Shards under
                                     1 MiB stay back to back. Ranks may differ (only local placement changes). Same
-                                    bits */,
-    FMI_TUNE_COMM_LOCAL_ASYNC = 16 /* LOCAL transport (ranks as threads of one process): 1 (default) = every
-                                    exchange is ordered on the ranks' streams by events (the host meets the peers
-                                    but never waits for the device); 0 = the host synchronises each rank's stream
-                                    before and after the copies. Process-wide: change it only while no LOCAL
-                                    collective runs. Same bits */
+                                    bits */
 } fmi_tune_key_t;
 int fmi_tune_set(int key, long long value);
 int fmi_tune_get(int key, long long* value);

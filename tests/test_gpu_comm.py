@@ -380,11 +380,10 @@ def test_comm_allreduce_skewed_shards_same_bits(device, N):
 
 
 @pytest.mark.parametrize("N", [3, 8])
-def test_comm_local_exchange_host_synchronised_same_bits(device, N):
-    """FMI_TUNE_COMM_LOCAL_ASYNC = 0 (the LOCAL transport's host-synchronised exchange; the default orders every
-    exchange on the ranks' streams by events): allreduce, reduce (every root), scan and the host-ingress allreduce
-    give the oracle's bits either way, with the ranks on the library stream and on streams of their own."""
-    from fmi_amd import Stream, Tune
+def test_comm_local_ranks_on_streams_of_their_own(device, N):
+    """LOCAL ranks on the library stream and on streams of their own: allreduce, reduce (every root), scan and the
+    host-ingress allreduce give the oracle's bits either way."""
+    from fmi_amd import Stream
 
     n = 3 * 4099 + 5
     xs = [inputs(np.float32, n, r, seed=90 + N) for r in range(N)]
@@ -392,42 +391,35 @@ def test_comm_local_exchange_host_synchronised_same_bits(device, N):
         want_ar, _ = orc.allreduce(xs, orc.op_sum)
         want_sc, _ = orc.scan(xs, orc.op_sum)
         want_red = [orc.reduce(xs, orc.op_sum, root=root)[0] for root in range(N)]
-    old = fmi_amd.tune_get(Tune.COMM_LOCAL_ASYNC)
-    try:
-        for asynchronous in (0, 1):
-            fmi_amd.tune_set(Tune.COMM_LOCAL_ASYNC, asynchronous)
-            for own_stream in (False, True):
-                def body(c, r):
-                    st = Stream() if own_stream else None
-                    s, o = Bucket.from_numpy(xs[r]), Bucket(n, np.float32)
-                    c.allreduce(Op.SUM, s, o, stream=st)
-                    c.sync(st)
-                    ar = o.numpy(st)
-                    c.scan(Op.SUM, s, o, stream=st)
-                    c.sync(st)
-                    sc = o.numpy(st)
-                    red = []
-                    for root in range(N):
-                        c.reduce(Op.SUM, s, o if r == root else None, root, stream=st)
-                        c.sync(st)
-                        red.append(o.numpy(st) if r == root else None)
-                    host = _host_allreduce(c, r, xs[r], Op.SUM, False, r % 2 == 0, 4099)[0]
-                    s.free()
-                    o.free()
-                    if st is not None:
-                        st.destroy()
-                    return ar, sc, red, host
+    for own_stream in (False, True):
+        def body(c, r):
+            st = Stream() if own_stream else None
+            s, o = Bucket.from_numpy(xs[r]), Bucket(n, np.float32)
+            c.allreduce(Op.SUM, s, o, stream=st)
+            c.sync(st)
+            ar = o.numpy(st)
+            c.scan(Op.SUM, s, o, stream=st)
+            c.sync(st)
+            sc = o.numpy(st)
+            red = []
+            for root in range(N):
+                c.reduce(Op.SUM, s, o if r == root else None, root, stream=st)
+                c.sync(st)
+                red.append(o.numpy(st) if r == root else None)
+            host = _host_allreduce(c, r, xs[r], Op.SUM, False, r % 2 == 0, 4099)[0]
+            s.free()
+            o.free()
+            if st is not None:
+                st.destroy()
+            return ar, sc, red, host
 
-                res = run_ranks(N, body)
-                tag = f"async={asynchronous} own_stream={own_stream}"
-                for r in range(N):
-                    assert_bit_equal(res[r][0], want_ar[r], f"allreduce rank {r} {tag}")
-                    assert_bit_equal(res[r][1], want_sc[r], f"scan rank {r} {tag}")
-                    assert_bit_equal(res[r][3], want_ar[r], f"host allreduce rank {r} {tag}")
-                for root in range(N):
-                    assert_bit_equal(res[root][2][root], want_red[root], f"reduce root {root} {tag}")
-    finally:
-        fmi_amd.tune_set(Tune.COMM_LOCAL_ASYNC, old)
+        res = run_ranks(N, body)
+        for r in range(N):
+            assert_bit_equal(res[r][0], want_ar[r], f"allreduce rank {r} own_stream={own_stream}")
+            assert_bit_equal(res[r][1], want_sc[r], f"scan rank {r} own_stream={own_stream}")
+            assert_bit_equal(res[r][3], want_ar[r], f"host allreduce rank {r} own_stream={own_stream}")
+        for root in range(N):
+            assert_bit_equal(res[root][2][root], want_red[root], f"reduce root {root} own_stream={own_stream}")
 
 
 def test_comm_allreduce_host_after_an_aborted_communicator(device):

@@ -166,8 +166,9 @@ t)
         tests/test_gpu_bench_dist.py > gpurun_out/${TAG}_bench_dist_tests.log 2>&1
     ;;
 l)
-    # the LOCAL transport's exchange ordered on the streams (FMI_TUNE_COMM_LOCAL_ASYNC, default 1): the communicator,
-    # PROC, timeout and host suites on it; then C5's co-resident block, async / host-synchronised, interleaved 3x
+    # history (commit 8631a58, removed after this run: slower): the LOCAL transport's exchange ordered on the streams
+    # by events (its FMI_TUNE_COMM_LOCAL_ASYNC key and tools/local_async_ab.py are gone): the communicator, PROC,
+    # timeout and host suites on it; then C5's co-resident block, async / host-synchronised, interleaved 3x
     timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider \
         tests/test_gpu_comm.py tests/test_gpu_timeout.py tests/test_gpu_comm_random_sweep.py tests/test_gpu_fmi_python.py \
         > gpurun_out/${TAG}_tests.log 2>&1 &&
