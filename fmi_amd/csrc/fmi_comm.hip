@@ -617,9 +617,9 @@ struct Hub {
     explicit Hub(int n) : n(n), ptrs(n, nullptr) {}
     ~Hub() {
         // A poisoned hub's ranks may have left copies queued that never drain: leak the streams then.
-        if (poisoned) return;
-        for (hipStream_t st : {h2d, d2h})
-            if (st) (void)hipStreamDestroy(st);
+        if (!poisoned)
+            for (hipStream_t st : {h2d, d2h})
+                if (st) (void)hipStreamDestroy(st);
     }
     int n;
     // The host pipelines' copy streams, shared by this communicator's ranks only (LocalTransport::copy_streams).
