@@ -1,4 +1,5 @@
-"""Re-tune of the fused P-way kernels' two launch knobs on slotted buckets (round 5). FMI_TUNE_FUSED_INFLIGHT_KIB
+"""Re-tune of the fused P-way kernels' two launch knobs on slotted buckets (round 5), and on carved groups (round 6,
+the default; --separate for one allocation per bucket). FMI_TUNE_FUSED_INFLIGHT_KIB
 (the LDS reservation that caps workgroups per CU) and FMI_TUNE_FUSED_POLICY (buffer loads nt + sc1 stores vs global
 nt accesses) were chosen in rounds 1-2 on buckets whose streams collided in HBM; with fmi_dev_alloc's
 rotating 4 KiB slots the best setting may differ. Shapes: the 8-way tree at 1 GiB per peer (C4 on one GPU) and at
@@ -26,11 +27,20 @@ MIB = 1 << 20
 PEAK = 8e12
 
 
+GROUPS = True  # round 6: each set one carved group (fmi_dev_alloc_group); --separate: one fmi_dev_alloc per bucket
+
+
+def buckets(count, n):
+    return Bucket.group(count, n, np.float32) if GROUPS else [Bucket(n, np.float32) for _ in range(count)]
+
+
 def make_tree(mib, sets, P=8):
     n = mib * MIB // 4
     out = []
     for s in range(sets):
-        bs = [Bucket(n, np.float32).fill_synthetic(11 + s, p) for p in range(P)] + [Bucket(n, np.float32)]
+        bs = buckets(P + 1, n)
+        for p in range(P):
+            bs[p].fill_synthetic(11 + s, p)
         out.append(bs)
     return n, out
 
@@ -39,7 +49,9 @@ def make_scan(mib, sets, P=8):
     n = mib * MIB // 4
     out = []
     for s in range(sets):
-        bs = [Bucket(n, np.float32).fill_synthetic(7 + s, p) for p in range(P)] + [Bucket(n, np.float32) for _ in range(P)]
+        bs = buckets(2 * P, n)
+        for p in range(P):
+            bs[p].fill_synthetic(7 + s, p)
         out.append(bs)
     return n, out
 
@@ -63,7 +75,10 @@ def main() -> None:
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--budgets", default="0,64,128,256")
     ap.add_argument("--policies", default="2,0")
+    ap.add_argument("--separate", action="store_true", help="one fmi_dev_alloc per bucket instead of carved groups")
     a = ap.parse_args()
+    global GROUPS
+    GROUPS = not a.separate
     fmi_amd.init(0)
     P = 8
     shapes = {}

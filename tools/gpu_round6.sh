@@ -22,6 +22,7 @@
 #   bash tools/gpu_round6.sh t   the N > 1 line's GPU tests (TAG=r06t)
 #   bash tools/gpu_round6.sh l   the LOCAL exchange ordered on the streams: its suites, then C5's co-resident block
 #                                async / synchronised (TAG=r06l)
+#   bash tools/gpu_round6.sh i   the fused kernels' launch knobs re-checked on carved groups (TAG=r06i)
 #   bash tools/gpu_round6.sh cold  C2 as the first work of a fresh box, twice, then after a 60 s pause (TAG=r06k)
 #   bash tools/gpu_round6.sh z   the round-end sequence: GPU suite, smoke(), default line, C2 profile (TAG=r06z...)
 set -o pipefail
@@ -176,6 +177,11 @@ l)
         tests/test_cpp_communicator.py -m gpu >> gpurun_out/${TAG}_tests.log 2>&1 &&
     timeout -k 10 600 python -u tools/local_async_ab.py --reps 3 > gpurun_out/${TAG}_local_async_ab.jsonl \
         2> gpurun_out/${TAG}_local_async_ab.err
+    ;;
+i)
+    # the fused kernels' in-flight cap x access policy re-checked on carved groups, two interleaved rounds
+    timeout -k 10 400 python -u tools/fused_retune.py --rounds 2 --budgets 0,32,64,128 --policies 2,0 \
+        > gpurun_out/${TAG}_fused_retune.jsonl 2> gpurun_out/${TAG}_fused_retune.err
     ;;
 cold)
     # is C2 slower as the first work of a fresh box (the driver's bench runs so)? The line twice, back to back, as
