@@ -17,6 +17,7 @@
 #                                (TAG=r06g)
 #   bash tools/gpu_round6.sh p   bench.py --force-dist at world 1 over RCCL, diagnostics and C5 at 1 GiB (TAG=r06p)
 #   bash tools/gpu_round6.sh q   the N > 1 line at full size, 8 PROC ranks on one GPU (TAG=r06q)
+#   bash tools/gpu_round6.sh r   the N > 1 line at N = 2 and 4, PROC ranks on one GPU (TAG=r06r)
 #   bash tools/gpu_round6.sh s   soaks: the P-way and communicator random sweeps at fresh seeds
 #   bash tools/gpu_round6.sh h   the device copy by placement (TAG=r06h)
 #   bash tools/gpu_round6.sh t   the N > 1 line's GPU tests (TAG=r06t)
@@ -190,6 +191,15 @@ cold)
     timeout -k 10 300 python bench.py --no-c5 --no-cpu-baseline > gpurun_out/${TAG}_cold2.json 2> gpurun_out/${TAG}_cold2.err &&
     sleep 60 &&
     timeout -k 10 300 python bench.py --no-c5 --no-cpu-baseline > gpurun_out/${TAG}_cold3.json 2> gpurun_out/${TAG}_cold3.err
+    ;;
+r)
+    # the N > 1 line rehearsed at the scaling curve's other sizes, N = 2 and 4 PROC ranks on the one GPU, full size
+    FMI_PROC_TIMEOUT_S=300 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node=2 \
+        --master-addr 127.0.0.1 --master-port 29655 bench.py --gpus 2 --transport proc --steps 20 --warmup 3 \
+        --diag-deadline 400 > gpurun_out/${TAG}_bench_proc2_rehearsal.json 2> gpurun_out/${TAG}_bench_proc2_rehearsal.err &&
+    FMI_PROC_TIMEOUT_S=300 timeout -k 10 800 python -m torch.distributed.run --nnodes=1 --nproc-per-node=4 \
+        --master-addr 127.0.0.1 --master-port 29666 bench.py --gpus 4 --transport proc --steps 20 --warmup 3 \
+        --diag-deadline 500 > gpurun_out/${TAG}_bench_proc4_rehearsal.json 2> gpurun_out/${TAG}_bench_proc4_rehearsal.err
     ;;
 z)
     # the round-end sequence on the current library and bench: the whole GPU suite, smoke(), the default line, then
