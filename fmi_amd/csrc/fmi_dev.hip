@@ -44,8 +44,11 @@ DeviceState g_state;
 // round: it runs fastest with both operands at their 2 MiB-aligned base, and 1.8-1.9 % slower when they sit in
 // nonzero slots (profiles/r06a_placement_ab.jsonl, r06b_placement_ab.jsonl: two boxes, kernel traces). So a plain
 // fmi_dev_alloc is a plain hipMalloc (FMI_TUNE_ALLOC_SLOTS = 0, the default since round 6), and the buckets one fused
-// kernel streams together are allocated as one group (fmi_dev_alloc_group): bucket j in slot j mod 16, whatever was
-// allocated before. FMI_TUNE_ALLOC_SLOTS = 1 restores round 5's rotation of every fmi_dev_alloc over the 16 slots.
+// kernel streams together are allocated as one group (fmi_dev_alloc_group): carved from ONE allocation, bucket j in
+// slot j mod 16, whatever was allocated before. One allocation matters as much as the slots: the 8-way tree over 1 GiB
+// buckets reads 0.83 carved against 0.79-0.81 for the same slots in separate hipMallocs, whose rate also swings with
+// where each allocation's memory comes from (profiles/r06f_placement_ab_trace.jsonl, r06b_placement_ab_trace.jsonl).
+// FMI_TUNE_ALLOC_SLOTS = 1 restores round 5's rotation of every fmi_dev_alloc over the 16 slots.
 constexpr size_t kSlotBytes = 4096, kSlots = 16, kSlotSpan = kSlotBytes * kSlots, kSlotMinBytes = size_t(1) << 20;
 std::mutex g_slots_mu;
 size_t g_next_slot = 0;
