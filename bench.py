@@ -816,44 +816,66 @@ def c3_single(reps: int = 60) -> dict:
             "timing": "two HIP events around back-to-back launches on the library stream (gaps included)"}
 
 
-def c4_single(peers: int = 8, mib: int = 1024, launches: int = 10) -> dict:
+C4_SETS = 3  # like C3's scan sets: the rate depends on where a set's 9 GiB lands, so average over draws
+
+
+def c4_single(peers: int = 8, mib: int = 1024, launches: int = 15, sets: int = C4_SETS) -> dict:
     """Config C4's data on ONE GPU: 8 peers x 1 GiB f32 buckets resident in HBM, their sum-allreduce computed by
     one pass of the fused 8-way kernel (fmi_dev_reduce_tree, allreduce_no_order: the reference's recursive-doubling
     bracketing, PeerToPeer.cpp:96-130). The kernel the N > 1 path runs on every shard, at the whole bucket:
-    (P + 1) x 1 GiB algorithmic bytes per launch (9 GiB, far past the 256 MB MALL: one buffer set is honest).
-    Mean launch time from two HIP events around back-to-back launches on the library stream; the result is
-    checked on head / middle / tail windows against numpy's float32 evaluation of rank 0's bracketing."""
+    (P + 1) x 1 GiB algorithmic bytes per launch (9 GiB, far past the 256 MB MALL). Each of `sets` buffer sets is one
+    carved group; the timed launches rotate over them, so one set's placement cannot decide the line
+    (round 6: one of 13 single-set lines read 0.761 against 0.827-0.847). Mean launch time from two HIP events
+    around back-to-back launches on the library stream, plus one isolated launch per set (`per_set_launch_us`);
+    every set's result is checked on head / middle / tail windows against numpy's float32 evaluation of rank 0's
+    bracketing."""
     import numpy as np
 
     import fmi_amd
     from fmi_amd import Alg, Bucket, Event, Op
 
     n = mib * MIB // 4
-    group = Bucket.group(peers + 1, n, np.float32)  # the launch's 8 inputs and output in distinct slots (DESIGN §4)
-    ins, out = group[:peers], group[peers]
-    for p, b in enumerate(ins):
-        b.fill_synthetic(11, p)
+    groups = [Bucket.group(peers + 1, n, np.float32) for _ in range(sets)]  # inputs + output in distinct slots
+    for g in groups:
+        for p in range(peers):
+            g[p].fill_synthetic(11, p)
     # The driver clears the VRAM C3 just freed (9 GiB) in the background, on the same HBM: measured right after
     # C3 this launch ran at 0.68 of peak, after a quiet second at 0.76-0.78 (profiles/r04_tree8_sizes.jsonl).
     quiet_device()
-    for _ in range(2):
-        fmi_amd.reduce_tree(Op.SUM, Alg.ALLREDUCE, out, ins)
+
+    def launch(k):
+        g = groups[k % sets]
+        fmi_amd.reduce_tree(Op.SUM, Alg.ALLREDUCE, g[peers], g[:peers])
+
+    for k in range(sets):
+        launch(k)
     e0, e1 = Event(), Event()
     e0.record()
-    for _ in range(launches):
-        fmi_amd.reduce_tree(Op.SUM, Alg.ALLREDUCE, out, ins)
+    for k in range(launches):
+        launch(k)
     e1.record()
     e1.sync()
     ms = e0.elapsed_ms(e1) / launches
     e0.destroy()
     e1.destroy()
+    per_set = [(Event(), Event()) for _ in range(sets)]  # diagnostic, untimed: one launch per set, its own events
+    for k, (a, b) in enumerate(per_set):
+        a.record()
+        launch(k)
+        b.record()
+    fmi_amd.sync()
+    per_set_us = [round(a.elapsed_ms(b) * 1e3, 1) for a, b in per_set]
+    for a, b in per_set:
+        a.destroy()
+        b.destroy()
     expr = fmi_amd.schedule_expr(Alg.ALLREDUCE, peers, 0)
     win, bad, checked = 4096, 0, 0
-    for o in (0, (n // 2) // 64 * 64, n - win):
-        want = eval_bracketing(expr, [b.view(o, win).numpy() for b in ins])
-        bad += int(np.count_nonzero(out.view(o, win).numpy().view(np.uint32) != want.view(np.uint32)))
-        checked += win
-    for b in ins + [out]:
+    for g in groups:
+        for o in (0, (n // 2) // 64 * 64, n - win):
+            want = eval_bracketing(expr, [b.view(o, win).numpy() for b in g[:peers]])
+            bad += int(np.count_nonzero(g[peers].view(o, win).numpy().view(np.uint32) != want.view(np.uint32)))
+            checked += win
+    for b in [x for g in groups for x in g]:
         b.free()
     algo = (peers + 1) * n * 4
     traffic, src = pmc_traffic(f"tree_kernel<fmi::dev::OpSum, float, 0, {peers}, false>", algo)
@@ -862,11 +884,12 @@ def c4_single(peers: int = 8, mib: int = 1024, launches: int = 10) -> dict:
             "kernel_avg_us": round(ms * 1e3, 2), "algorithmic_bytes": algo,
             "GB_s": round(algo / (ms * 1e-3) / 1e9, 1), "frac": round(algo / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "GiB_s_reduced_buckets": round(peers * n * 4 / GIB / (ms * 1e-3), 2),
-            "traffic": traffic, "traffic_source": src, "launches": launches, "placement": GROUP_PLACEMENT,
+            "traffic": traffic, "traffic_source": src, "launches": launches, "rotating_sets": sets,
+            "per_set_launch_us": per_set_us, "placement": GROUP_PLACEMENT,
             "timing": "two HIP events around back-to-back launches on the library stream (gaps included)",
             "self_check": {"ok": bad == 0, "mismatches": bad, "elements_checked": checked,
                            "against": "numpy float32 evaluation of rank 0's allreduce_no_order bracketing "
-                                      "(fmi_schedule_expr) on three windows, bit-exact"}}
+                                      "(fmi_schedule_expr) on three windows of every set, bit-exact"}}
 
 
 def eval_bracketing(expr: str, xs):

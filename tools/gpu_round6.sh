@@ -25,6 +25,7 @@
 #                                async / synchronised (TAG=r06l)
 #   bash tools/gpu_round6.sh i   the fused kernels' launch knobs re-checked on carved groups (TAG=r06i)
 #   bash tools/gpu_round6.sh cold  C2 as the first work of a fresh box, twice, then after a 60 s pause (TAG=r06k)
+#   bash tools/gpu_round6.sh two the default line twice, separate processes (TAG=r06v)
 #   bash tools/gpu_round6.sh z   the round-end sequence: GPU suite, smoke(), default line, C2 profile (TAG=r06z...)
 set -o pipefail
 cd /root/repo
@@ -200,6 +201,11 @@ r)
     FMI_PROC_TIMEOUT_S=300 timeout -k 10 800 python -m torch.distributed.run --nnodes=1 --nproc-per-node=4 \
         --master-addr 127.0.0.1 --master-port 29666 bench.py --gpus 4 --transport proc --steps 20 --warmup 3 \
         --diag-deadline 500 > gpurun_out/${TAG}_bench_proc4_rehearsal.json 2> gpurun_out/${TAG}_bench_proc4_rehearsal.err
+    ;;
+two)
+    # the default line twice in a row (separate processes)
+    timeout -k 10 600 python bench.py > gpurun_out/${TAG}_bench1.json 2> gpurun_out/${TAG}_bench1.err &&
+    timeout -k 10 600 python bench.py > gpurun_out/${TAG}_bench2.json 2> gpurun_out/${TAG}_bench2.err
     ;;
 z)
     # the round-end sequence on the current library and bench: the whole GPU suite, smoke(), the default line, then
